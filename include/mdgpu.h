@@ -1,0 +1,176 @@
+/*
+ * mdgpu.h -- C ABI of the MI355X-native metabodecon deconvolution engine.
+ *
+ * Drop-in boundary for metabodecon's hot path. Each entry point replaces one
+ * public reference interface (paths relative to SombkeMaximilian/metabodecon-rust):
+ *
+ *   mdg_deconvolute            <- Deconvoluter::deconvolute_spectrum
+ *                                 metabodecon/src/deconvolution/deconvoluter.rs:530-552
+ *                                 and par_deconvolute_spectrum (:591-613, same bits)
+ *   mdg_deconvolute_batch      <- Deconvoluter::{deconvolute_spectra,par_deconvolute_spectra}
+ *                                 deconvoluter.rs:651-661 / :700-710 (per-spectrum status;
+ *                                 the caller reproduces the fail-fast Result collect)
+ *   mdg_deconvolute_batch_device  same, inputs/outputs resident in HBM (no PCIe in the call)
+ *   mdg_superposition_vec      <- Lorentzian::{superposition_vec,par_superposition_vec}
+ *                                 deconvolution/lorentzian.rs:631-663
+ *   mdg_settings_validate      <- SmoothingSettings/SelectionSettings/FittingSettings::validate
+ *                                 smoother.rs:84-100, selector.rs:85-98, fitter.rs:80-90
+ *   mdg_ignore_region_add      <- Deconvoluter::add_ignore_region  deconvoluter.rs:438-472
+ *
+ * Conventions: plain pointers and sizes, no C++/torch types; every function
+ * returns an int status (0 = ok) and never throws/aborts across the boundary.
+ * Host buffers are owned by the caller; device workspaces are owned by the
+ * context and reused across calls. A context is internally locked, so one
+ * context may be shared by threads (Deconvoluter is Send + Sync,
+ * deconvoluter.rs:913-917); calls on one context serialise.
+ *
+ * Numerics: all arithmetic is IEEE binary64 with no FMA contraction and every
+ * order-dependent sum evaluated in the reference's order, so peak index sets
+ * and Lorentzian parameters are bit-identical to the reference CPU path; the
+ * MSE reduction is a fixed-order tree (|rel err| < 1e-12).
+ */
+#ifndef MDGPU_H
+#define MDGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MDG_ABI_VERSION 1
+
+/* Status codes (deconvolution/error.rs:39-95 kinds + engine failures). */
+enum mdg_status {
+    MDG_OK = 0,
+    MDG_NO_PEAKS_DETECTED = 1,        /* Kind::NoPeaksDetected */
+    MDG_EMPTY_SIGNAL_REGION = 2,      /* Kind::EmptySignalRegion */
+    MDG_EMPTY_SIGNAL_FREE_REGION = 3, /* Kind::EmptySignalFreeRegion */
+    MDG_INVALID_SMOOTHING = 10,       /* Kind::InvalidSmoothingSettings */
+    MDG_INVALID_SELECTION = 11,       /* Kind::InvalidSelectionSettings */
+    MDG_INVALID_FITTING = 12,         /* Kind::InvalidFittingSettings */
+    MDG_INVALID_IGNORE_REGION = 13,   /* Kind::InvalidIgnoreRegion */
+    MDG_INVALID_ARGUMENT = 20,        /* null pointer / bad size at the ABI */
+    MDG_CAPACITY = 21,                /* out_cap smaller than the result (count still set) */
+    MDG_REFERENCE_PANIC = 30,         /* input on which the reference panics (slice bounds) */
+    MDG_ERR_HIP = 100,                /* HIP runtime failure */
+    MDG_ERR_NO_DEVICE = 101,
+    MDG_ERR_OUT_OF_MEMORY = 102
+};
+
+enum { MDG_SMOOTH_IDENTITY = 0, MDG_SMOOTH_MOVING_AVERAGE = 1 };
+enum { MDG_SELECT_DETECTOR_ONLY = 0, MDG_SELECT_NOISE_SCORE = 1 };
+enum { MDG_SCORE_MINIMUM_SUM = 0 };
+enum { MDG_FIT_ANALYTICAL = 0 };
+
+/* Deconvoluter settings (smoother.rs:27-65, selector.rs:21-66, fitter.rs:26-63). */
+typedef struct mdg_settings {
+    int32_t smoother;          /* MDG_SMOOTH_* */
+    uint32_t smooth_iterations;
+    uint32_t smooth_window;
+    int32_t selector;          /* MDG_SELECT_* */
+    int32_t scoring;           /* MDG_SCORE_* */
+    uint32_t fit_iterations;
+    int32_t fitter;            /* MDG_FIT_* */
+    int32_t reserved;          /* must be 0 */
+    double threshold;
+} mdg_settings;
+
+/* Lorentzian in transformed parameters (lorentzian.rs:138-145), repr(C). */
+typedef struct mdg_lorentzian {
+    double sfhw;
+    double hw2;
+    double maxp;
+} mdg_lorentzian;
+
+typedef struct mdg_ctx mdg_ctx;
+
+/* ---- host-only helpers (no GPU needed) ---------------------------------- */
+int mdg_abi_version(void);
+const char* mdg_strerror(int status);
+void mdg_settings_default(mdg_settings* s);
+int mdg_settings_validate(const mdg_settings* s);
+/* Merge (a,b) into the sorted ppm region list `regions` (n pairs, capacity cap
+ * pairs) exactly like add_ignore_region; *n_out receives the new count. */
+int mdg_ignore_region_add(double* regions, size_t n, size_t cap, double a, double b,
+                          size_t* n_out);
+
+/* Synthetic-workload generator (bench/test data, not the hot path):
+ * n_peaks Lorentzians on a jittered grid over [lo, hi] ppm (SURVEY 8d recipe),
+ * counter-based splitmix64 so host and device draw identical bits. */
+int mdg_synth_lorentzians(uint64_t seed, size_t n_peaks, double lo, double hi,
+                          mdg_lorentzian* out);
+/* Irwin-Hall(12) noise, exact in binary64: sigma * (sum of 12 u48 - 6). */
+int mdg_synth_noise(uint64_t seed, size_t n, double sigma, double* out);
+
+/* ---- device contexts ------------------------------------------------------ */
+int mdg_device_count(int* count);
+int mdg_ctx_create(int device, mdg_ctx** out);
+int mdg_ctx_destroy(mdg_ctx* ctx);
+/* Run subsequent work on this hipStream_t (NULL = the context's own stream). */
+int mdg_ctx_set_stream(mdg_ctx* ctx, void* hip_stream);
+int mdg_ctx_synchronize(mdg_ctx* ctx);
+/* Per-stage device timing with hipEvents on the context stream (0 = off).
+ * Stages: 0 prep, 1 smooth, 2 detect, 3 select, 4 fit_init, 5 fit_superposition,
+ * 6 fit_update, 7 retain, 8 mse_superposition, 9 mse_reduce, 10 superposition_vec,
+ * 11 synth. times_ms/launches receive accumulated values (arrays of n_stages). */
+int mdg_ctx_set_profiling(mdg_ctx* ctx, int enable);
+int mdg_ctx_stage_times(mdg_ctx* ctx, double* times_ms, uint64_t* launches, int n_stages);
+int mdg_ctx_reset_stage_times(mdg_ctx* ctx);
+
+/* ---- hot path: host buffers ------------------------------------------------
+ * x, y: n chemical shifts / intensities of a validated Spectrum
+ * (spectrum.rs:120-150 invariants). sb0/sb1: signal boundaries in ppm ordered
+ * per monotonicity as Spectrum stores them (spectrum.rs:854-863). ignore:
+ * n_ignore merged (lo,hi) ppm pairs from mdg_ignore_region_add (NULL/0 = None).
+ * out: capacity `cap`; *out_count always receives P_kept; MDG_CAPACITY if it
+ * exceeds cap. */
+int mdg_deconvolute(mdg_ctx* ctx, const double* x, const double* y, size_t n, double sb0,
+                    double sb1, const mdg_settings* s, const double* ignore, size_t n_ignore,
+                    mdg_lorentzian* out, size_t cap, size_t* out_count, double* out_mse);
+
+/* Batch of b spectra of n points. Row i of x is x + i*x_stride (x_stride 0 =
+ * one shared axis), row i of y is y + i*y_stride. sb: b (sb0,sb1) pairs.
+ * out: b*cap Lorentzians (row i at out + i*cap). counts/mse/status: b each.
+ * Returns the first nonzero status (the reference's fail-fast error) or 0. */
+int mdg_deconvolute_batch(mdg_ctx* ctx, size_t b, size_t n, const double* x, size_t x_stride,
+                          const double* y, size_t y_stride, const double* sb,
+                          const mdg_settings* s, const double* ignore, size_t n_ignore,
+                          mdg_lorentzian* out, size_t cap, size_t* counts, double* mse,
+                          int* status);
+
+/* Same, every array resident on the context's device (d_ prefix); enqueued on
+ * the context stream without any host synchronisation (capturable). d_counts and
+ * d_status are int32. Call mdg_ctx_synchronize before reading outputs. */
+int mdg_deconvolute_batch_device(mdg_ctx* ctx, size_t b, size_t n, const double* d_x,
+                                 size_t x_stride, const double* d_y, size_t y_stride,
+                                 const double* d_sb, const mdg_settings* s,
+                                 const double* ignore, size_t n_ignore,
+                                 mdg_lorentzian* d_out, size_t cap, int32_t* d_counts,
+                                 double* d_mse, int32_t* d_status);
+
+/* Diagnostics: copy the peak index triples of spectrum `spectrum` from the last
+ * batch run on this context. which = 0: detected peaks (after the detector and
+ * ignore filters, detector.rs:168-182 + noise_score_filter.rs:41-48),
+ * which = 1: selected peaks (input of the fitter). *count receives the total. */
+int mdg_ctx_last_peaks(mdg_ctx* ctx, size_t spectrum, int which, int32_t* left,
+                       int32_t* center, int32_t* right, size_t cap, size_t* count);
+
+/* Lorentzian::superposition_vec: out[i] = sum_j L[j](x[i]) in slice order. */
+int mdg_superposition_vec(mdg_ctx* ctx, const double* x, size_t n, const mdg_lorentzian* L,
+                          size_t p, double* out);
+int mdg_superposition_vec_device(mdg_ctx* ctx, const double* d_x, size_t n,
+                                 const mdg_lorentzian* d_L, size_t p, double* d_out);
+
+/* Device synthetic batch: d_x (n, shared axis x_i = xmax - (i*width)/(n-1)) and
+ * d_y (b x n): y_s = in-order superposition of mdg_synth_lorentzians(seed0+s) +
+ * mdg_synth_noise(seed0+s). */
+int mdg_synth_batch_device(mdg_ctx* ctx, size_t b, size_t n, double xmax, double width,
+                           uint64_t seed0, size_t n_peaks, double lo, double hi, double sigma,
+                           double* d_x, double* d_y);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MDGPU_H */

@@ -1,0 +1,704 @@
+// mdg_capi.hip -- host engine and C ABI of libmdgpu (see include/mdgpu.h).
+//
+// The engine replaces the body of Deconvoluter::deconvolute_spectrum
+// (deconvoluter.rs:530-552) for a whole batch at once: every stage is one
+// kernel launch over all B spectra, enqueued on one HIP stream with no host
+// synchronisation between stages (the device API is graph-capturable).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "../../include/mdgpu.h"
+#include "mdg_common.hpp"
+#include "mdg_kernels.hpp"
+
+using namespace mdg;
+
+namespace {
+
+constexpr int kStages = 12;
+enum Stage {
+    ST_PREP = 0, ST_SMOOTH, ST_DETECT, ST_SELECT, ST_FIT_INIT, ST_FIT_SUP, ST_FIT_UPDATE,
+    ST_RETAIN, ST_MSE, ST_MSE_REDUCE, ST_SUPVEC, ST_SYNTH
+};
+
+struct Pending {
+    int stage;
+    hipEvent_t a, b;
+};
+
+struct Buffer {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+}  // namespace
+
+struct mdg_ctx {
+    int device = 0;
+    hipStream_t own = nullptr;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    // workspace arena
+    Buffer arena;
+    int ws_B = 0, ws_N = 0;
+    int last_B = 0, last_N = 0;  // shape of the last pipeline run
+    Workspace w{};
+    // staging for the host-pointer API
+    Buffer st_x, st_y, st_sb, st_out, st_cnt, st_mse, st_status, st_L, st_sup;
+    // profiling
+    bool profiling = false;
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> free_events;
+    double stage_ms[kStages] = {0};
+    uint64_t stage_launches[kStages] = {0};
+};
+
+namespace {
+
+int hip_fail(hipError_t e) {
+    if (e == hipErrorOutOfMemory) return MDG_ERR_OUT_OF_MEMORY;
+    return MDG_ERR_HIP;
+}
+
+#define HIPCHK(expr)                              \
+    do {                                          \
+        hipError_t _e = (expr);                   \
+        if (_e != hipSuccess) return hip_fail(_e); \
+    } while (0)
+
+int ensure(Buffer& b, size_t bytes) {
+    if (b.bytes >= bytes) return MDG_OK;
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+    size_t sz = std::max<size_t>(bytes, 256);
+    HIPCHK(hipMalloc(&b.p, sz));
+    b.bytes = sz;
+    return MDG_OK;
+}
+
+hipEvent_t get_event(mdg_ctx* c) {
+    if (!c->free_events.empty()) {
+        hipEvent_t e = c->free_events.back();
+        c->free_events.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+// RAII stage timer: records events around a launch when profiling is on.
+struct StageTimer {
+    mdg_ctx* c;
+    int stage;
+    hipEvent_t a = nullptr;
+    StageTimer(mdg_ctx* c_, int s) : c(c_), stage(s) {
+        if (c->profiling) {
+            a = get_event(c);
+            if (a) (void)hipEventRecord(a, c->stream);
+        }
+    }
+    ~StageTimer() {
+        if (c->profiling && a) {
+            hipEvent_t b = get_event(c);
+            if (b) {
+                (void)hipEventRecord(b, c->stream);
+                c->pending.push_back({stage, a, b});
+            }
+        }
+    }
+};
+
+void drain_timers(mdg_ctx* c) {
+    if (c->pending.empty()) return;
+    (void)hipStreamSynchronize(c->stream);
+    for (auto& p : c->pending) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+            c->stage_ms[p.stage] += ms;
+            c->stage_launches[p.stage] += 1;
+        }
+        c->free_events.push_back(p.a);
+        c->free_events.push_back(p.b);
+    }
+    c->pending.clear();
+}
+
+size_t align256(size_t v) { return (v + 255) & ~size_t(255); }
+
+int ensure_workspace(mdg_ctx* c, int B, int N) {
+    if (!(B <= c->ws_B && N <= c->ws_N && c->arena.p)) {
+        const int nB = std::max(B, c->ws_B), nN = std::max(N, c->ws_N);
+        const size_t W = (size_t)(nN + 63) / 64;
+        const size_t capD = (size_t)nN / 2 + 2;
+        const size_t Bs = (size_t)nB;
+        size_t off = 0;
+        auto take = [&](size_t bytes) { size_t o = off; off = align256(off + bytes); return o; };
+        const size_t o_smooth = take(Bs * nN * 8), o_tmp0 = take(Bs * nN * 8), o_tmp1 = take(Bs * nN * 8);
+        const size_t o_masks = take(Bs * 3 * W * 8);
+        const size_t o_dl = take(Bs * capD * 4), o_dc = take(Bs * capD * 4), o_dr = take(Bs * capD * 4);
+        const size_t o_sl = take(Bs * capD * 4), o_sc = take(Bs * capD * 4), o_sr = take(Bs * capD * 4);
+        const size_t o_scores = take(Bs * capD * 8);
+        const size_t o_params = take(Bs * capD * 24), o_kept = take(Bs * capD * 24);
+        const size_t o_st = take(Bs * capD * 48);
+        const size_t o_rx = take(Bs * capD * 24), o_ry = take(Bs * capD * 24), o_ratio = take(Bs * capD * 24);
+        const size_t o_msep = take(Bs * 1024 * 8);
+        const size_t o_sfr = take(Bs * 16);
+        const size_t o_sbi = take(Bs * 16);
+        const size_t o_ig = take(Bs * 2 * kMaxIgnore * 8);
+        const size_t o_nig = take(Bs * 4), o_panic = take(Bs * 4), o_status = take(Bs * 4);
+        const size_t o_dcnt = take(Bs * 4), o_scnt = take(Bs * 4), o_kcnt = take(Bs * 4);
+        if (c->arena.p) (void)hipFree(c->arena.p);
+        c->arena.p = nullptr;
+        c->arena.bytes = 0;
+        HIPCHK(hipMalloc(&c->arena.p, off));
+        c->arena.bytes = off;
+        char* base = (char*)c->arena.p;
+        Workspace& w = c->w;
+        w.smooth = (double*)(base + o_smooth);
+        w.tmp0 = (double*)(base + o_tmp0);
+        w.tmp1 = (double*)(base + o_tmp1);
+        w.masks = (uint64_t*)(base + o_masks);
+        w.det_l = (int32_t*)(base + o_dl);
+        w.det_c = (int32_t*)(base + o_dc);
+        w.det_r = (int32_t*)(base + o_dr);
+        w.sel_l = (int32_t*)(base + o_sl);
+        w.sel_c = (int32_t*)(base + o_sc);
+        w.sel_r = (int32_t*)(base + o_sr);
+        w.scores = (double*)(base + o_scores);
+        w.params = (double*)(base + o_params);
+        w.kept = (double*)(base + o_kept);
+        w.stencil = (double*)(base + o_st);
+        w.rx = (double*)(base + o_rx);
+        w.ry = (double*)(base + o_ry);
+        w.ratio = (double*)(base + o_ratio);
+        w.mse_part = (double*)(base + o_msep);
+        w.sfr_stats = (double*)(base + o_sfr);
+        w.sbi = (int64_t*)(base + o_sbi);
+        w.ig = (int64_t*)(base + o_ig);
+        w.n_ig = (int32_t*)(base + o_nig);
+        w.mse_panic = (int32_t*)(base + o_panic);
+        w.status = (int32_t*)(base + o_status);
+        w.det_count = (int32_t*)(base + o_dcnt);
+        w.sel_count = (int32_t*)(base + o_scnt);
+        w.kept_count = (int32_t*)(base + o_kcnt);
+        c->ws_B = nB;
+        c->ws_N = nN;
+    }
+    return MDG_OK;
+}
+
+int validate_common(const mdg_settings* s, size_t n_ignore, const double* ignore) {
+    if (!s) return MDG_INVALID_ARGUMENT;
+    int v = mdg_settings_validate(s);
+    if (v) return v;
+    if (n_ignore > (size_t)kMaxIgnore) return MDG_INVALID_ARGUMENT;
+    if (n_ignore > 0 && !ignore) return MDG_INVALID_ARGUMENT;
+    return MDG_OK;
+}
+
+// Runs the whole pipeline for a device-resident batch. Caller holds c->mu.
+int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
+    int rc = ensure_workspace(c, a.B, a.N);
+    if (rc) return rc;
+    // Row strides follow the current shape; the arena is sized for the largest
+    // (B, N) seen so far, so every current-shape row fits.
+    Workspace w = c->w;
+    w.W = (a.N + 63) / 64;
+    w.capD = a.N / 2 + 2;
+    c->last_B = a.B;
+    c->last_N = a.N;
+    hipStream_t st = c->stream;
+    const bool ma = s->smoother == MDG_SMOOTH_MOVING_AVERAGE;
+    if (ma) {
+        w.smooth_ptr = w.smooth;
+        w.smooth_stride = a.N;
+    } else {
+        w.smooth_ptr = a.y;
+        w.smooth_stride = a.y_stride;
+    }
+    const int det_only = s->selector == MDG_SELECT_DETECTOR_ONLY;
+    const int gfit = std::max(1, std::min(64, 4096 / std::max(1, a.B)));
+    const int gupd = std::max(1, std::min(16, 1024 / std::max(1, a.B)));
+    const int nparts = std::max(1, std::min({1024, (a.N + 255) / 256, std::max(1, 4096 / a.B)}));
+    {
+        StageTimer t(c, ST_PREP);
+        launch_prep(a, w, st);
+    }
+    if (ma) {
+        if ((int64_t)(s->smooth_window / 2) > a.N) {
+            // moving_average.rs:63 `values_len - self.right` underflows: reference panics
+            std::vector<int32_t> pan(a.B, MDG_REFERENCE_PANIC);
+            HIPCHK(hipMemcpyAsync(w.status, pan.data(), sizeof(int32_t) * a.B, hipMemcpyHostToDevice, st));
+            HIPCHK(hipStreamSynchronize(st));
+        } else {
+            StageTimer t(c, ST_SMOOTH);
+            launch_smooth(a, w, (int)s->smooth_iterations, (int)s->smooth_window, st);
+        }
+    }
+    {
+        StageTimer t(c, ST_DETECT);
+        launch_flags(a, w, st);
+        launch_peaks(a, w, det_only, st);
+    }
+    {
+        StageTimer t(c, ST_SELECT);
+        launch_select(a, w, det_only, s->threshold, st);
+    }
+    {
+        StageTimer t(c, ST_FIT_INIT);
+        launch_fit_init(a, w, gupd, st);
+    }
+    for (uint32_t it = 0; it < s->fit_iterations; ++it) {
+        {
+            StageTimer t(c, ST_FIT_SUP);
+            launch_fit_sup(a, w, gfit, st);
+        }
+        {
+            StageTimer t(c, ST_FIT_UPDATE);
+            launch_fit_update(a, w, gupd, st);
+        }
+    }
+    {
+        StageTimer t(c, ST_RETAIN);
+        launch_retain(a, w, st);
+    }
+    {
+        StageTimer t(c, ST_MSE);
+        launch_mse(a, w, nparts, st);
+    }
+    {
+        StageTimer t(c, ST_MSE_REDUCE);
+        launch_mse_final(a, w, nparts, st);
+    }
+    HIPCHK(hipGetLastError());
+    return MDG_OK;
+}
+
+void fill_args(BatchArgs& a, size_t b, size_t n, const double* x, size_t xs, const double* y,
+               size_t ys, const double* sb, const double* ignore, size_t n_ignore, double* out,
+               size_t cap, int32_t* cnt, double* mse, int32_t* status) {
+    a.B = (int)b;
+    a.N = (int)n;
+    a.x = x;
+    a.x_stride = (int64_t)xs;
+    a.y = y;
+    a.y_stride = (int64_t)ys;
+    a.sb = sb;
+    a.n_ignore = (int)n_ignore;
+    for (int k = 0; k < 2 * kMaxIgnore; ++k) a.ignore[k] = 0.0;
+    for (size_t k = 0; k < 2 * n_ignore; ++k) a.ignore[k] = ignore[k];
+    a.out = out;
+    a.cap = (int)std::min<size_t>(cap, (size_t)INT32_MAX);
+    a.out_count = cnt;
+    a.out_mse = mse;
+    a.out_status = status;
+}
+
+}  // namespace
+
+// =====================================================================================
+// C ABI
+// =====================================================================================
+extern "C" {
+
+int mdg_abi_version(void) { return MDG_ABI_VERSION; }
+
+const char* mdg_strerror(int st) {
+    // messages of deconvolution/error.rs:105-168 where the kind exists there
+    switch (st) {
+        case MDG_OK: return "ok";
+        case MDG_NO_PEAKS_DETECTED: return "no peaks detected in the spectrum";
+        case MDG_EMPTY_SIGNAL_REGION: return "no peaks found in the signal region of the spectrum";
+        case MDG_EMPTY_SIGNAL_FREE_REGION: return "no peaks found in the signal-free region of the spectrum";
+        case MDG_INVALID_SMOOTHING: return "invalid smoothing settings";
+        case MDG_INVALID_SELECTION: return "invalid selection settings";
+        case MDG_INVALID_FITTING: return "invalid fitting settings";
+        case MDG_INVALID_IGNORE_REGION: return "invalid ignore region";
+        case MDG_INVALID_ARGUMENT: return "invalid argument";
+        case MDG_CAPACITY: return "output capacity too small";
+        case MDG_REFERENCE_PANIC: return "input on which the reference implementation panics";
+        case MDG_ERR_HIP: return "HIP runtime error";
+        case MDG_ERR_NO_DEVICE: return "no HIP device";
+        case MDG_ERR_OUT_OF_MEMORY: return "device out of memory";
+        default: return "unknown status";
+    }
+}
+
+void mdg_settings_default(mdg_settings* s) {
+    if (!s) return;
+    std::memset(s, 0, sizeof(*s));
+    s->smoother = MDG_SMOOTH_MOVING_AVERAGE;  // smoother.rs:58-65
+    s->smooth_iterations = 3;
+    s->smooth_window = 3;
+    s->selector = MDG_SELECT_NOISE_SCORE;  // selector.rs:59-66
+    s->scoring = MDG_SCORE_MINIMUM_SUM;
+    s->threshold = 5.0;
+    s->fitter = MDG_FIT_ANALYTICAL;  // fitter.rs:59-63
+    s->fit_iterations = 10;
+}
+
+int mdg_settings_validate(const mdg_settings* s) {
+    if (!s) return MDG_INVALID_ARGUMENT;
+    if (s->smoother == MDG_SMOOTH_MOVING_AVERAGE) {  // smoother.rs:84-100
+        if (s->smooth_iterations == 0 || s->smooth_window <= 1) return MDG_INVALID_SMOOTHING;
+    } else if (s->smoother != MDG_SMOOTH_IDENTITY) {
+        return MDG_INVALID_SMOOTHING;
+    }
+    if (s->selector == MDG_SELECT_NOISE_SCORE) {  // selector.rs:85-98
+        if (s->threshold <= 0.0 || !std::isfinite(s->threshold) || s->scoring != MDG_SCORE_MINIMUM_SUM)
+            return MDG_INVALID_SELECTION;
+    } else if (s->selector != MDG_SELECT_DETECTOR_ONLY) {
+        return MDG_INVALID_SELECTION;
+    }
+    if (s->fitter != MDG_FIT_ANALYTICAL || s->fit_iterations == 0) return MDG_INVALID_FITTING;  // fitter.rs:80-90
+    if (s->reserved != 0) return MDG_INVALID_ARGUMENT;
+    return MDG_OK;
+}
+
+int mdg_ignore_region_add(double* r, size_t n, size_t cap, double a, double b, size_t* n_out) {
+    // deconvoluter.rs:438-472
+    if (!std::isfinite(a) || !std::isfinite(b) || std::fabs(a - b) < kCheckPrecision)
+        return MDG_INVALID_IGNORE_REGION;
+    if (!r || !n_out || n + 1 > cap) return MDG_INVALID_ARGUMENT;
+    r[2 * n] = std::fmin(a, b);
+    r[2 * n + 1] = std::fmax(a, b);
+    ++n;
+    for (size_t i = 1; i < n; ++i) {  // sort by start
+        const double s0 = r[2 * i], s1 = r[2 * i + 1];
+        size_t j = i;
+        while (j > 0 && r[2 * (j - 1)] > s0) {
+            r[2 * j] = r[2 * (j - 1)];
+            r[2 * j + 1] = r[2 * (j - 1) + 1];
+            --j;
+        }
+        r[2 * j] = s0;
+        r[2 * j + 1] = s1;
+    }
+    for (;;) {  // merge overlapping / adjacent (within CHECK_PRECISION) neighbours
+        size_t pos = n;
+        for (size_t i = 0; i + 1 < n; ++i) {
+            if (r[2 * (i + 1)] < r[2 * i + 1] ||
+                std::fabs(r[2 * i + 1] - r[2 * (i + 1)]) < kCheckPrecision) {
+                pos = i;
+                break;
+            }
+        }
+        if (pos == n) break;
+        const double lo = std::fmin(r[2 * pos], r[2 * (pos + 1)]);
+        const double hi = std::fmax(r[2 * pos + 1], r[2 * (pos + 1) + 1]);
+        r[2 * pos] = lo;
+        r[2 * pos + 1] = hi;
+        for (size_t i = pos + 1; i + 1 < n; ++i) {
+            r[2 * i] = r[2 * (i + 1)];
+            r[2 * i + 1] = r[2 * (i + 1) + 1];
+        }
+        --n;
+    }
+    *n_out = n;
+    return MDG_OK;
+}
+
+int mdg_synth_lorentzians(uint64_t seed, size_t n_peaks, double lo, double hi, mdg_lorentzian* out) {
+    if (!out && n_peaks) return MDG_INVALID_ARGUMENT;
+    const uint64_t key = stream_key(seed, kStreamPeaks);
+    const double delta = (hi - lo) / (double)n_peaks;
+    for (size_t p = 0; p < n_peaks; ++p) {
+        const double u1 = u53(draw(key, 3 * p)), u2 = u53(draw(key, 3 * p + 1)),
+                     u3 = u53(draw(key, 3 * p + 2));
+        const double maxp = lo + ((double)p + 0.5) * delta + (u1 - 0.5) * 0.5 * delta;
+        const double hw = 3.0e-4 + u2 * 5.0e-4;
+        const double amp = std::pow(10.0, 4.5 + 3.5 * u3);
+        const double hw2 = hw * hw;
+        out[p].sfhw = amp * hw2;
+        out[p].hw2 = hw2;
+        out[p].maxp = maxp;
+    }
+    return MDG_OK;
+}
+
+int mdg_synth_noise(uint64_t seed, size_t n, double sigma, double* out) {
+    if (!out && n) return MDG_INVALID_ARGUMENT;
+    const uint64_t key = stream_key(seed, kStreamNoise);
+    for (size_t i = 0; i < n; ++i) out[i] = synth_noise(key, i, sigma);
+    return MDG_OK;
+}
+
+int mdg_device_count(int* count) {
+    if (!count) return MDG_INVALID_ARGUMENT;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return MDG_OK;
+}
+
+int mdg_ctx_create(int device, mdg_ctx** out) {
+    if (!out) return MDG_INVALID_ARGUMENT;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return MDG_ERR_NO_DEVICE;
+    if (device < 0 || device >= n) return MDG_ERR_NO_DEVICE;
+    HIPCHK(hipSetDevice(device));
+    mdg_ctx* c = new (std::nothrow) mdg_ctx();
+    if (!c) return MDG_ERR_OUT_OF_MEMORY;
+    c->device = device;
+    hipError_t e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete c;
+        return hip_fail(e);
+    }
+    c->stream = c->own;
+    *out = c;
+    return MDG_OK;
+}
+
+int mdg_ctx_destroy(mdg_ctx* c) {
+    if (!c) return MDG_OK;
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        (void)hipSetDevice(c->device);
+        (void)hipStreamSynchronize(c->stream);
+        for (auto& p : c->pending) {
+            (void)hipEventDestroy(p.a);
+            (void)hipEventDestroy(p.b);
+        }
+        for (auto e : c->free_events) (void)hipEventDestroy(e);
+        for (Buffer* b : {&c->arena, &c->st_x, &c->st_y, &c->st_sb, &c->st_out, &c->st_cnt,
+                          &c->st_mse, &c->st_status, &c->st_L, &c->st_sup})
+            if (b->p) (void)hipFree(b->p);
+        if (c->own) (void)hipStreamDestroy(c->own);
+    }
+    delete c;
+    return MDG_OK;
+}
+
+int mdg_ctx_set_stream(mdg_ctx* c, void* stream) {
+    if (!c) return MDG_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> g(c->mu);
+    drain_timers(c);
+    c->stream = stream ? (hipStream_t)stream : c->own;
+    return MDG_OK;
+}
+
+int mdg_ctx_synchronize(mdg_ctx* c) {
+    if (!c) return MDG_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    HIPCHK(hipStreamSynchronize(c->stream));
+    drain_timers(c);
+    return MDG_OK;
+}
+
+int mdg_ctx_set_profiling(mdg_ctx* c, int enable) {
+    if (!c) return MDG_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> g(c->mu);
+    drain_timers(c);
+    c->profiling = enable != 0;
+    return MDG_OK;
+}
+
+int mdg_ctx_stage_times(mdg_ctx* c, double* ms, uint64_t* launches, int n) {
+    if (!c) return MDG_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    drain_timers(c);
+    for (int i = 0; i < n && i < kStages; ++i) {
+        if (ms) ms[i] = c->stage_ms[i];
+        if (launches) launches[i] = c->stage_launches[i];
+    }
+    return MDG_OK;
+}
+
+int mdg_ctx_reset_stage_times(mdg_ctx* c) {
+    if (!c) return MDG_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> g(c->mu);
+    drain_timers(c);
+    for (int i = 0; i < kStages; ++i) {
+        c->stage_ms[i] = 0;
+        c->stage_launches[i] = 0;
+    }
+    return MDG_OK;
+}
+
+int mdg_ctx_last_peaks(mdg_ctx* c, size_t spectrum, int which, int32_t* left, int32_t* center,
+                       int32_t* right, size_t cap, size_t* count) {
+    if (!c || !count || (which != 0 && which != 1)) return MDG_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (!c->arena.p || spectrum >= (size_t)c->last_B) return MDG_INVALID_ARGUMENT;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const Workspace& w = c->w;
+    const size_t capD = (size_t)c->last_N / 2 + 2;
+    int32_t n = 0;
+    HIPCHK(hipMemcpy(&n, (which ? w.sel_count : w.det_count) + spectrum, 4, hipMemcpyDeviceToHost));
+    *count = (size_t)std::max(0, n);
+    const size_t k = std::min(cap, (size_t)std::max(0, n));
+    const size_t off = spectrum * capD;
+    if (k) {
+        if (left) HIPCHK(hipMemcpy(left, (which ? w.sel_l : w.det_l) + off, k * 4, hipMemcpyDeviceToHost));
+        if (center) HIPCHK(hipMemcpy(center, (which ? w.sel_c : w.det_c) + off, k * 4, hipMemcpyDeviceToHost));
+        if (right) HIPCHK(hipMemcpy(right, (which ? w.sel_r : w.det_r) + off, k * 4, hipMemcpyDeviceToHost));
+    }
+    return MDG_OK;
+}
+
+int mdg_deconvolute_batch_device(mdg_ctx* c, size_t b, size_t n, const double* d_x,
+                                 size_t x_stride, const double* d_y, size_t y_stride,
+                                 const double* d_sb, const mdg_settings* s, const double* ignore,
+                                 size_t n_ignore, mdg_lorentzian* d_out, size_t cap,
+                                 int32_t* d_counts, double* d_mse, int32_t* d_status) {
+    if (!c) return MDG_INVALID_ARGUMENT;
+    int v = validate_common(s, n_ignore, ignore);
+    if (v) return v;
+    if (b == 0) return MDG_OK;
+    if (n < 2 || n > (size_t)INT32_MAX / 2 || b > (size_t)INT32_MAX) return MDG_INVALID_ARGUMENT;
+    if (!d_x || !d_y || !d_sb || !d_counts || !d_mse || !d_status || (!d_out && cap)) return MDG_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    BatchArgs a;
+    fill_args(a, b, n, d_x, x_stride, d_y, y_stride, d_sb, ignore, n_ignore, (double*)d_out, cap,
+              d_counts, d_mse, d_status);
+    return run_pipeline(c, a, s);
+}
+
+int mdg_deconvolute_batch(mdg_ctx* c, size_t b, size_t n, const double* x, size_t x_stride,
+                          const double* y, size_t y_stride, const double* sb,
+                          const mdg_settings* s, const double* ignore, size_t n_ignore,
+                          mdg_lorentzian* out, size_t cap, size_t* counts, double* mse,
+                          int* status) {
+    if (!c) return MDG_INVALID_ARGUMENT;
+    int v = validate_common(s, n_ignore, ignore);
+    if (v) return v;
+    if (b == 0) return MDG_OK;
+    if (n < 2 || n > (size_t)INT32_MAX / 2 || b > (size_t)INT32_MAX) return MDG_INVALID_ARGUMENT;
+    if (!x || !y || !sb || !counts || !mse || !status || (!out && cap)) return MDG_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    const size_t xrows = x_stride ? b : 1;
+    int rc;
+    if ((rc = ensure(c->st_x, xrows * n * 8))) return rc;
+    if ((rc = ensure(c->st_y, b * n * 8))) return rc;
+    if ((rc = ensure(c->st_sb, b * 16))) return rc;
+    if ((rc = ensure(c->st_out, std::max<size_t>(1, b * cap) * 24))) return rc;
+    if ((rc = ensure(c->st_cnt, b * 4))) return rc;
+    if ((rc = ensure(c->st_mse, b * 8))) return rc;
+    if ((rc = ensure(c->st_status, b * 4))) return rc;
+    double* dx = (double*)c->st_x.p;
+    double* dy = (double*)c->st_y.p;
+    if (x_stride == 0 || x_stride == n) {
+        HIPCHK(hipMemcpyAsync(dx, x, xrows * n * 8, hipMemcpyHostToDevice, st));
+    } else {
+        HIPCHK(hipMemcpy2DAsync(dx, n * 8, x, x_stride * 8, n * 8, b, hipMemcpyHostToDevice, st));
+    }
+    if (y_stride == n) {
+        HIPCHK(hipMemcpyAsync(dy, y, b * n * 8, hipMemcpyHostToDevice, st));
+    } else {
+        HIPCHK(hipMemcpy2DAsync(dy, n * 8, y, y_stride * 8, n * 8, b, hipMemcpyHostToDevice, st));
+    }
+    HIPCHK(hipMemcpyAsync(c->st_sb.p, sb, b * 16, hipMemcpyHostToDevice, st));
+    BatchArgs a;
+    fill_args(a, b, n, dx, x_stride ? n : 0, dy, n, (const double*)c->st_sb.p, ignore, n_ignore,
+              (double*)c->st_out.p, cap, (int32_t*)c->st_cnt.p, (double*)c->st_mse.p,
+              (int32_t*)c->st_status.p);
+    rc = run_pipeline(c, a, s);
+    if (rc) return rc;
+    std::vector<int32_t> cnt(b), stv(b);
+    HIPCHK(hipMemcpyAsync(cnt.data(), c->st_cnt.p, b * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(stv.data(), c->st_status.p, b * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(mse, c->st_mse.p, b * 8, hipMemcpyDeviceToHost, st));
+    if (cap) HIPCHK(hipMemcpyAsync(out, c->st_out.p, b * cap * 24, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    drain_timers(c);
+    int first = MDG_OK;
+    for (size_t i = 0; i < b; ++i) {
+        counts[i] = (size_t)std::max(0, cnt[i]);
+        status[i] = stv[i];
+        if (first == MDG_OK && stv[i] != MDG_OK) first = stv[i];
+    }
+    return first;
+}
+
+int mdg_deconvolute(mdg_ctx* c, const double* x, const double* y, size_t n, double sb0,
+                    double sb1, const mdg_settings* s, const double* ignore, size_t n_ignore,
+                    mdg_lorentzian* out, size_t cap, size_t* out_count, double* out_mse) {
+    if (!out_count || !out_mse) return MDG_INVALID_ARGUMENT;
+    const double sb[2] = {sb0, sb1};
+    int status = 0;
+    int rc = mdg_deconvolute_batch(c, 1, n, x, 0, y, n, sb, s, ignore, n_ignore, out, cap,
+                                   out_count, out_mse, &status);
+    return rc;
+}
+
+int mdg_superposition_vec_device(mdg_ctx* c, const double* d_x, size_t n, const mdg_lorentzian* d_L,
+                                 size_t p, double* d_out) {
+    if (!c || (!d_x && n) || (!d_L && p) || (!d_out && n)) return MDG_INVALID_ARGUMENT;
+    if (p > (size_t)INT32_MAX) return MDG_INVALID_ARGUMENT;
+    if (n == 0) return MDG_OK;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    {
+        StageTimer t(c, ST_SUPVEC);
+        launch_superposition_vec(d_x, (int64_t)n, (const double*)d_L, (int)p, d_out, c->stream);
+    }
+    HIPCHK(hipGetLastError());
+    return MDG_OK;
+}
+
+int mdg_superposition_vec(mdg_ctx* c, const double* x, size_t n, const mdg_lorentzian* L, size_t p,
+                          double* out) {
+    if (!c || (!x && n) || (!L && p) || (!out && n)) return MDG_INVALID_ARGUMENT;
+    if (p > (size_t)INT32_MAX) return MDG_INVALID_ARGUMENT;
+    if (n == 0) return MDG_OK;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    int rc;
+    if ((rc = ensure(c->st_x, n * 8))) return rc;
+    if ((rc = ensure(c->st_L, std::max<size_t>(p, 1) * 24))) return rc;
+    if ((rc = ensure(c->st_sup, n * 8))) return rc;
+    HIPCHK(hipMemcpyAsync(c->st_x.p, x, n * 8, hipMemcpyHostToDevice, st));
+    if (p) HIPCHK(hipMemcpyAsync(c->st_L.p, L, p * 24, hipMemcpyHostToDevice, st));
+    {
+        StageTimer t(c, ST_SUPVEC);
+        launch_superposition_vec((const double*)c->st_x.p, (int64_t)n, (const double*)c->st_L.p,
+                                 (int)p, (double*)c->st_sup.p, st);
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(out, c->st_sup.p, n * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    drain_timers(c);
+    return MDG_OK;
+}
+
+int mdg_synth_batch_device(mdg_ctx* c, size_t b, size_t n, double xmax, double width,
+                           uint64_t seed0, size_t n_peaks, double lo, double hi, double sigma,
+                           double* d_x, double* d_y) {
+    if (!c || !d_x || !d_y || n < 2 || b == 0 || n_peaks > (size_t)INT32_MAX) return MDG_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    std::vector<mdg_lorentzian> params(b * n_peaks);
+    for (size_t s = 0; s < b; ++s) mdg_synth_lorentzians(seed0 + s, n_peaks, lo, hi, params.data() + s * n_peaks);
+    int rc;
+    if ((rc = ensure(c->st_L, std::max<size_t>(1, params.size()) * 24))) return rc;
+    HIPCHK(hipMemcpyAsync(c->st_L.p, params.data(), params.size() * 24, hipMemcpyHostToDevice, c->stream));
+    {
+        StageTimer t(c, ST_SYNTH);
+        launch_synth(d_x, d_y, (int64_t)n, (int)b, xmax, width, (const double*)c->st_L.p,
+                     (int)n_peaks, seed0, sigma, c->stream);
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));  // params staging buffer is reused
+    drain_timers(c);
+    return MDG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,771 @@
+// mdg_kernels.hip -- CDNA4 (gfx950) kernels of the metabodecon deconvolution hot path.
+//
+// One batch = B spectra of N points. Per-spectrum work is indexed by
+// blockIdx.y (or by the block for the per-spectrum scan kernels), so every
+// wave belongs to exactly one spectrum and all peak-parameter reads are
+// wave-uniform: they compile to scalar (SMEM) loads that feed VALU operands
+// straight from SGPRs -- no LDS traffic and no barriers in the O(N*P) loops.
+//
+// Numerics contract (DESIGN.md "Parity"): binary64 everywhere, compiled with
+// -ffp-contract=off, correctly rounded '/' and sqrt, and every order-dependent
+// sum evaluated in the reference's order (left folds starting at -0.0).
+#include <hip/hip_runtime.h>
+
+#include "mdg_common.hpp"
+#include "mdg_kernels.hpp"
+
+namespace mdg {
+
+// ----------------------------------------------------------------------------------
+// small device helpers
+// ----------------------------------------------------------------------------------
+__device__ __forceinline__ double lorentz(double x, double sfhw, double hw2, double maxp) {
+    // lorentzian.rs:546-548  sfhw / (hw2 + (x - maxp).powi(2))
+    const double d = x - maxp;
+    return sfhw / (hw2 + d * d);
+}
+
+// In-order superposition (lorentzian.rs:606-611) of P wave-uniform Lorentzians.
+// params is AoS {sfhw, hw2, maxp}; the address is uniform so the compiler emits
+// s_load_dwordx* and uses SGPR operands.
+typedef const __attribute__((address_space(4))) double* const_f64_ptr;
+
+__device__ __forceinline__ double superpose(double x, const double* __restrict__ params_g, int P) {
+    // Parameters are read-only for the whole launch: address space 4 (constant)
+    // lets the backend issue s_load_dwordx* and feed SGPR operands to the VALU.
+    const const_f64_ptr params = (const_f64_ptr)(params_g);
+    double acc = -0.0;
+    int j = 0;
+    for (; j + 4 <= P; j += 4) {
+        const_f64_ptr L = params + 3 * j;
+        const double e0 = lorentz(x, L[0], L[1], L[2]);
+        const double e1 = lorentz(x, L[3], L[4], L[5]);
+        const double e2 = lorentz(x, L[6], L[7], L[8]);
+        const double e3 = lorentz(x, L[9], L[10], L[11]);
+        acc += e0;
+        acc += e1;
+        acc += e2;
+        acc += e3;
+    }
+    for (; j < P; ++j) {
+        const_f64_ptr L = params + 3 * j;
+        acc += lorentz(x, L[0], L[1], L[2]);
+    }
+    return acc;
+}
+
+// D[k] := sd[k-1] = (s[k-1] - 2*s[k]) + s[k+1]   (common.rs:5-10, intensity aligned)
+__device__ __forceinline__ double dsd(const double* __restrict__ s, int k) {
+    return s[k - 1] - 2.0 * s[k] + s[k + 1];
+}
+
+template <int BS>
+__device__ __forceinline__ int block_exclusive_scan(int v, int* lds, int* total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    constexpr int NW = BS / 64;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) lds[wid] = x;
+    __syncthreads();
+    if (wid == 0) {
+        int t = lane < NW ? lds[lane] : 0;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(t, o, 64);
+            if (lane >= o) t += y;
+        }
+        if (lane < NW) lds[lane] = t;
+    }
+    __syncthreads();
+    const int prefix = wid > 0 ? lds[wid - 1] : 0;
+    *total = lds[NW - 1];
+    __syncthreads();
+    return prefix + x - v;
+}
+
+template <int BS>
+__device__ __forceinline__ long long block_sum_ll(long long v, long long* lds) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    constexpr int NW = BS / 64;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) lds[wid] = v;
+    __syncthreads();
+    long long t = 0;
+    for (int w = 0; w < NW; ++w) t += lds[w];
+    __syncthreads();
+    return t;
+}
+
+// first set bit at position >= pos and <= limit, or -1
+__device__ __forceinline__ int find_next_bit(const uint64_t* __restrict__ m, int pos, int limit) {
+    if (pos > limit) return -1;
+    int w = pos >> 6;
+    const int lastw = limit >> 6;
+    uint64_t bits = m[w] & (~0ull << (pos & 63));
+    for (;;) {
+        if (bits) {
+            const int r = (w << 6) + __ffsll((unsigned long long)bits) - 1;
+            return r <= limit ? r : -1;
+        }
+        if (++w > lastw) return -1;
+        bits = m[w];
+    }
+}
+
+// last set bit at position <= pos and >= lo, or -1
+__device__ __forceinline__ int find_prev_bit(const uint64_t* __restrict__ m, int pos, int lo) {
+    if (pos < lo || pos < 0) return -1;
+    int w = pos >> 6;
+    const int firstw = lo >> 6;
+    const int b = pos & 63;
+    uint64_t bits = m[w] & (b == 63 ? ~0ull : ((1ull << (b + 1)) - 1ull));
+    for (;;) {
+        if (bits) {
+            const int r = (w << 6) + 63 - __clzll((long long)bits);
+            return r >= lo ? r : -1;
+        }
+        if (--w < firstw) return -1;
+        bits = m[w];
+    }
+}
+
+// ----------------------------------------------------------------------------------
+// K0  prep: signal-boundary indices, ignore-region indices, MSE regions
+// spectrum.rs:633-635,741-746 ; deconvoluter.rs:828-904
+// ----------------------------------------------------------------------------------
+__global__ void k_prep(BatchArgs a, Workspace w) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= a.B) return;
+    const double* x = a.x + (size_t)s * a.x_stride;
+    const double x0 = x[0];
+    const double step = x[1] - x[0];
+    const double sb0 = a.sb[2 * s], sb1 = a.sb[2 * s + 1];
+    const int64_t bi0 = as_index(floor((sb0 - x0) / step));
+    const int64_t bi1 = as_index(ceil((sb1 - x0) / step));
+    w.sbi[2 * s] = bi0;
+    w.sbi[2 * s + 1] = bi1;
+    int nig = 0;
+    int64_t* pairs = w.ig + (size_t)s * 2 * kMaxIgnore;
+    if (a.n_ignore > 0) {
+        const double lower_b = fmin(sb0, sb1), upper_b = fmax(sb0, sb1);
+        const int64_t lower = bi0 < bi1 ? bi0 : bi1, upper = bi0 < bi1 ? bi1 : bi0;
+        for (int k = 0; k < a.n_ignore; ++k) {
+            const double st = a.ignore[2 * k], en = a.ignore[2 * k + 1];
+            if ((st < lower_b && en < lower_b) || (st > upper_b && en > upper_b)) continue;
+            int64_t fi = as_index(floor((st - x0) / step));
+            if (fi < lower) fi = lower;
+            int64_t si = as_index(ceil((en - x0) / step));
+            if (si > upper) si = upper;
+            const int64_t b0 = fi < si ? fi : si, b1 = fi < si ? si : fi;
+            // `boundaries.0 < boundaries.1 - 1` in usize (wraps in release when b1 == 0)
+            if (b1 == 0 || b0 < b1 - 1) {
+                pairs[2 * nig] = b0;
+                pairs[2 * nig + 1] = b1;
+                ++nig;
+            }
+        }
+    }
+    w.n_ig[s] = nig;
+    // MSE regions (sbi.0, ig0.s), (ig0.e, ig1.s), ... (igk.e, sbi.1); Rust slicing
+    // panics when start > end or end > len.
+    int panic = 0;
+    for (int r = 0; r <= nig; ++r) {
+        const int64_t lo = r == 0 ? bi0 : pairs[2 * (r - 1) + 1];
+        const int64_t hi = r == nig ? bi1 : pairs[2 * r];
+        if (lo > hi || hi > (int64_t)a.N) panic = 1;
+    }
+    w.mse_panic[s] = panic;
+    w.status[s] = (a.N < 2) ? MDG_INVALID_ARGUMENT : 0;
+    w.det_count[s] = 0;
+    w.sel_count[s] = 0;
+    w.kept_count[s] = 0;
+}
+
+// ----------------------------------------------------------------------------------
+// K1  iterated moving average, exact running-sum recurrence
+// smoothing/moving_average.rs:53-83, circular_buffer.rs:34-59
+// One lane per spectrum: the recurrence is order dependent (hard part 2).
+// ----------------------------------------------------------------------------------
+__device__ void ma_pass(const double* __restrict__ src, double* __restrict__ dst, int N, int ws) {
+    const int right = ws / 2;
+    double sum = 0.0;  // T::zero()
+    double div = 1.0;  // T::one()
+    for (int k = 0; k < right; ++k) sum += src[k];
+    int len = right;
+    const int nmain = N - right;
+    int i = 0;
+    // steady state (window full) is the hot loop; growth phase first
+    for (; i < nmain && len < ws; ++i) {
+        sum += src[i + right];
+        ++len;
+        div = 1.0 / (double)len;
+        dst[i] = sum * div;
+    }
+    constexpr int U = 8;
+    for (; i + U <= nmain; i += U) {
+        double add[U], sub[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            add[u] = src[i + u + right];
+            sub[u] = src[i + u + right - ws];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            sum += add[u];
+            sum -= sub[u];
+            dst[i + u] = sum * div;
+        }
+    }
+    for (; i < nmain; ++i) {
+        sum += src[i + right];
+        sum -= src[i + right - ws];
+        dst[i] = sum * div;
+    }
+    // tail: the FIFO holds src[N-len .. N)
+    int head = N - len;
+    for (int t = nmain; t < N; ++t) {
+        if (len > 0) {
+            sum -= src[head];
+            ++head;
+            --len;
+            div = 1.0 / (double)len;
+            dst[t] = sum * div;
+        } else {
+            dst[t] = src[t];
+        }
+    }
+}
+
+__global__ void k_smooth(BatchArgs a, Workspace w, int iters, int ws) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= a.B) return;
+    if (w.status[s]) return;
+    const int N = a.N;
+    const double* src = a.y + (size_t)s * a.y_stride;
+    double* out = w.smooth + (size_t)s * N;
+    double* tmp0 = w.tmp0 + (size_t)s * N;
+    double* tmp1 = w.tmp1 + (size_t)s * N;
+    for (int it = 0; it < iters; ++it) {
+        double* dst = (it == iters - 1) ? out : ((it & 1) ? tmp1 : tmp0);
+        ma_pass(src, dst, N, ws);
+        src = dst;
+    }
+}
+
+// ----------------------------------------------------------------------------------
+// K2  curvature flags: center / right-border / left-border predicates as bitmasks
+// peak_selection/detector.rs:189-233 restated on intensity-aligned D[k]=sd[k-1]:
+//   center c : D[c]<0 && D[c]<D[c-1] && D[c]<D[c+1]                    c in [2,N-3]
+//   right  r : D[r]>D[r-1] && (D[r]>=D[r+1] || (D[r]<0 && D[r+1]>=0))
+//   left   l : D[l]>D[l+1] && (D[l]>=D[l-1] || (D[l]<0 && D[l-1]>=0))
+// The per-center border scans of the reference become next/previous-set-bit
+// searches on these masks (K3): the predicates do not depend on the center.
+// ----------------------------------------------------------------------------------
+__global__ void k_flags(BatchArgs a, Workspace w) {
+    const int s = blockIdx.y;
+    if (w.status[s]) return;
+    const int N = a.N;
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const double* sm = w.smooth_ptr + (size_t)s * w.smooth_stride;
+    bool fc = false, fr = false, fl = false;
+    if (k >= 2 && k <= N - 3) {
+        const double dm = dsd(sm, k - 1), d0 = dsd(sm, k), dp = dsd(sm, k + 1);
+        fc = d0 < 0. && d0 < dm && d0 < dp;
+        fr = d0 > dm && (d0 >= dp || (d0 < 0. && dp >= 0.));
+        fl = d0 > dp && (d0 >= dm || (d0 < 0. && dm >= 0.));
+    }
+    const uint64_t bc = __ballot(fc), br = __ballot(fr), bl = __ballot(fl);
+    if ((threadIdx.x & 63) == 0 && k < N) {
+        const int word = k >> 6;
+        uint64_t* m = w.masks + (size_t)s * 3 * w.W;
+        m[word] = bc;
+        m[w.W + word] = br;
+        m[2 * w.W + word] = bl;
+    }
+}
+
+// ----------------------------------------------------------------------------------
+// K3  peak list: borders, detector filter, ignore filter, ordered compaction
+// detector.rs:168-212, noise_score_filter.rs:41-48, detector_only.rs:305-315
+// One 1024-thread workgroup per spectrum; thread t owns a contiguous word range so
+// the block scan preserves center order.
+// ----------------------------------------------------------------------------------
+__device__ __forceinline__ bool in_ignore(int v, const int64_t* pairs, int n) {
+    for (int k = 0; k < n; ++k)
+        if (v >= pairs[2 * k] && v < pairs[2 * k + 1]) return true;
+    return false;
+}
+
+template <int BS>
+__global__ __launch_bounds__(BS) void k_peaks(BatchArgs a, Workspace w, int detector_only) {
+    const int s = blockIdx.x;
+    __shared__ int lds_i[BS / 64 + 1];
+    __shared__ long long lds_l[BS / 64 + 1];
+    if (w.status[s]) return;  // uniform per block
+    const int N = a.N;
+    const int W = w.W;
+    const uint64_t* mc = w.masks + (size_t)s * 3 * W;
+    const uint64_t* mr = mc + W;
+    const uint64_t* ml = mc + 2 * W;
+    const int64_t* pairs = w.ig + (size_t)s * 2 * kMaxIgnore;
+    const int nig = w.n_ig[s];
+    const int64_t sbi0 = w.sbi[2 * s], sbi1 = w.sbi[2 * s + 1];
+    const int wpt = (W + BS - 1) / BS;
+    const int w0 = threadIdx.x * wpt;
+    const int w1 = min(W, w0 + wpt);
+    int n_bordered = 0, n_keep = 0;
+    for (int pass = 0; pass < 2; ++pass) {
+        int out = 0;
+        if (pass == 1) {
+            int total;
+            out = block_exclusive_scan<BS>(n_keep, lds_i, &total);
+            if (threadIdx.x == 0) w.det_count[s] = total;
+        }
+        for (int wd = w0; wd < w1; ++wd) {
+            uint64_t bits = mc[wd];
+            while (bits) {
+                const int b = __ffsll((unsigned long long)bits) - 1;
+                bits &= bits - 1;
+                const int c = (wd << 6) + b;
+                const int r = find_next_bit(mr, c + 1, N - 3);
+                const int l = find_prev_bit(ml, c - 1, 2);
+                if (r < 0 || l < 0) continue;  // right == N-1 or left == 0: dropped
+                bool keep = true;
+                if (detector_only) keep = (int64_t)l >= sbi0 && (int64_t)r <= sbi1;
+                if (keep && a.n_ignore > 0) keep = !(in_ignore(l, pairs, nig) || in_ignore(r, pairs, nig));
+                if (pass == 0) {
+                    ++n_bordered;
+                    n_keep += keep ? 1 : 0;
+                } else if (keep) {
+                    const size_t o = (size_t)s * w.capD + out;
+                    w.det_l[o] = l;
+                    w.det_c[o] = c;
+                    w.det_r[o] = r;
+                    ++out;
+                }
+            }
+        }
+        if (pass == 0) {
+            const long long tot = block_sum_ll<BS>(n_bordered, lds_l);
+            if (tot == 0) {
+                if (threadIdx.x == 0) w.status[s] = MDG_NO_PEAKS_DETECTED;
+                return;
+            }
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------------
+// K4  noise-score selection (noise_score_filter.rs:91-138, scorer.rs:65-75, common.rs:26-40)
+// ----------------------------------------------------------------------------------
+__device__ __forceinline__ double score_min_sum(const double* __restrict__ sm, int l, int c, int r) {
+    double left = -0.0, right = -0.0;
+    for (int k = l; k <= c; ++k) left += fabs(dsd(sm, k));
+    for (int k = c; k <= r; ++k) right += fabs(dsd(sm, k));
+    return fmin(left, right);
+}
+
+template <int BS>
+__global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double threshold) {
+    const int s = blockIdx.x;
+    __shared__ int lds_i[BS / 64 + 1];
+    __shared__ long long lds_l[BS / 64 + 1];
+    __shared__ double thr_sh;
+    if (w.status[s]) return;
+    const int P = w.det_count[s];
+    if (P == 0) {  // peaks.len() - 1 underflows in peak_region_boundaries
+        if (threadIdx.x == 0) w.status[s] = MDG_REFERENCE_PANIC;
+        return;
+    }
+    const size_t base = (size_t)s * w.capD;
+    const int* pl = w.det_l + base;
+    const int* pc = w.det_c + base;
+    const int* pr = w.det_r + base;
+    const int64_t sbi0 = w.sbi[2 * s], sbi1 = w.sbi[2 * s + 1];
+    const double* sm = w.smooth_ptr + (size_t)s * w.smooth_stride;
+    double* scores = w.scores + base;
+    long long c0 = 0, c1 = 0;
+    for (int p = threadIdx.x; p < P; p += BS) {
+        const int64_t c = pc[p];
+        c0 += c <= sbi0;
+        c1 += c <= sbi1;
+        scores[p] = score_min_sum(sm, pl[p], pc[p], pr[p]);
+    }
+    const long long cnt0 = block_sum_ll<BS>(c0, lds_l);
+    const long long cnt1 = block_sum_ll<BS>(c1, lds_l);
+    // centers ascend: position(center > sb) == #(center <= sb)
+    const int left = cnt0 < P ? (int)cnt0 : 0;
+    const long long r1 = cnt1 > left ? cnt1 : left;
+    const int right = r1 < P ? (int)r1 : P - 1;
+    if (left == 0 && right >= P) {
+        if (threadIdx.x == 0) w.status[s] = MDG_EMPTY_SIGNAL_FREE_REGION;
+        return;
+    }
+    if (left == right) {
+        if (threadIdx.x == 0) w.status[s] = MDG_EMPTY_SIGNAL_REGION;
+        return;
+    }
+    __syncthreads();  // scores visible to the whole block
+    if (threadIdx.x == 0) {
+        // mean_sd_scores: sequential left folds over SFR = peaks[..left] ++ peaks[right..]
+        const int n = left + (P - right);
+        double sum = -0.0;
+        for (int p = 0; p < left; ++p) sum += scores[p];
+        for (int p = right; p < P; ++p) sum += scores[p];
+        const double mean = sum / (double)n;
+        double var = -0.0;
+        for (int p = 0; p < left; ++p) {
+            const double d = scores[p] - mean;
+            var += d * d;
+        }
+        for (int p = right; p < P; ++p) {
+            const double d = scores[p] - mean;
+            var += d * d;
+        }
+        var = var / (double)n;
+        const double sd = __builtin_sqrt(var);
+        thr_sh = mean + threshold * sd;
+        w.sfr_stats[2 * s] = mean;
+        w.sfr_stats[2 * s + 1] = sd;
+    }
+    __syncthreads();
+    const double thr = thr_sh;
+    // ordered compaction of peaks[left..right] with score >= thr
+    const int len = right - left;
+    const int per = (len + BS - 1) / BS;
+    const int q0 = left + threadIdx.x * per;
+    const int q1 = min(right, q0 + per);
+    int keep = 0;
+    for (int q = q0; q < q1; ++q) keep += scores[q] >= thr;
+    int total;
+    int out = block_exclusive_scan<BS>(keep, lds_i, &total);
+    for (int q = q0; q < q1; ++q) {
+        if (scores[q] >= thr) {
+            const size_t o = base + out;
+            w.sel_l[o] = pl[q];
+            w.sel_c[o] = pc[q];
+            w.sel_r[o] = pr[q];
+            ++out;
+        }
+    }
+    if (threadIdx.x == 0) {
+        w.sel_count[s] = total;
+        if (total == 0) w.status[s] = MDG_EMPTY_SIGNAL_REGION;
+    }
+}
+
+// DetectorOnly: the detector output is the selection (detector_only.rs:17-39)
+__global__ void k_select_detector_only(BatchArgs a, Workspace w) {
+    const int s = blockIdx.y;
+    if (w.status[s]) return;
+    const int P = w.det_count[s];
+    if (blockIdx.x == 0 && threadIdx.x == 0) w.sel_count[s] = P;
+    const size_t base = (size_t)s * w.capD;
+    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
+        w.sel_l[base + p] = w.det_l[base + p];
+        w.sel_c[base + p] = w.det_c[base + p];
+        w.sel_r[base + p] = w.det_r[base + p];
+    }
+}
+
+// ----------------------------------------------------------------------------------
+// K5  fit: stencil gather, shoulder mirroring, closed-form 3x3 solve
+// fitting/fitter_analytical.rs:19-37,147-172, peak_stencil.rs:27-36,113-131,
+// reduced_spectrum.rs:16-43. Fitting uses the RAW intensities.
+// ----------------------------------------------------------------------------------
+struct Stencil {
+    double x1, x2, x3, y1, y2, y3;
+};
+
+__device__ __forceinline__ void mirror_shoulder(Stencil& q) {
+    const bool increasing = q.y1 <= q.y2 && q.y2 <= q.y3;
+    const bool decreasing = q.y1 >= q.y2 && q.y2 >= q.y3;
+    if (increasing) {
+        q.y3 = q.y1;
+        q.x3 = 2.0 * q.x2 - q.x1;
+    } else if (decreasing) {
+        q.y1 = q.y3;
+        q.x1 = 2.0 * q.x2 - q.x3;
+    }
+}
+
+__device__ __forceinline__ void solve(const Stencil& q, double* out3) {
+    const double x1 = q.x1, x2 = q.x2, x3 = q.x3, y1 = q.y1, y2 = q.y2, y3 = q.y3;
+    const double numerator =
+        x1 * x1 * y1 * (y2 - y3) + x2 * x2 * y2 * (y3 - y1) + x3 * x3 * y3 * (y1 - y2);
+    const double divisor =
+        2.0 * (x1 - x2) * y1 * y2 + 2.0 * (x2 - x3) * y2 * y3 + 2.0 * (x3 - x1) * y3 * y1;
+    const double m = numerator / divisor;
+    const double t1 = x1 - m, t2 = x2 - m, t3 = x3 - m;
+    const double left = (y1 * (t1 * t1) - y2 * (t2 * t2)) / (y2 - y1);
+    const double right = (y2 * (t2 * t2) - y3 * (t3 * t3)) / (y3 - y2);
+    const double h = fmax((left + right) / 2.0, kEpsilon);
+    out3[0] = y2 * (h + t2 * t2);
+    out3[1] = h;
+    out3[2] = m;
+}
+
+__global__ void k_fit_init(BatchArgs a, Workspace w) {
+    const int s = blockIdx.y;
+    if (w.status[s]) return;
+    const int P = w.sel_count[s];
+    const size_t base = (size_t)s * w.capD;
+    const double* x = a.x + (size_t)s * a.x_stride;
+    const double* y = a.y + (size_t)s * a.y_stride;
+    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
+        const int l = w.sel_l[base + p], c = w.sel_c[base + p], r = w.sel_r[base + p];
+        Stencil q{x[l], x[c], x[r], y[l], y[c], y[r]};
+        double* rx = w.rx + 3 * base + 3 * (size_t)p;
+        double* ry = w.ry + 3 * base + 3 * (size_t)p;
+        rx[0] = q.x1; rx[1] = q.x2; rx[2] = q.x3;
+        ry[0] = q.y1; ry[1] = q.y2; ry[2] = q.y3;
+        mirror_shoulder(q);
+        double* st = w.stencil + 6 * base + 6 * (size_t)p;
+        st[0] = q.x1; st[1] = q.x2; st[2] = q.x3; st[3] = q.y1; st[4] = q.y2; st[5] = q.y3;
+        solve(q, w.params + 3 * base + 3 * (size_t)p);
+    }
+}
+
+// K6  fit superposition at the 3P reduced points + ratio (fitter_analytical.rs:40-47)
+__global__ void k_fit_sup(BatchArgs a, Workspace w) {
+    const int s = blockIdx.y;
+    if (w.status[s]) return;
+    const int P = w.sel_count[s];
+    const size_t base = (size_t)s * w.capD;
+    const double* __restrict__ params = w.params + 3 * base;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < 3 * P; i += gridDim.x * blockDim.x) {
+        const double sup = superpose(w.rx[3 * base + i], params, P);
+        w.ratio[3 * base + i] = w.ry[3 * base + i] / sup;
+    }
+}
+
+// K7  stencil update + re-solve (fitter_analytical.rs:48-65)
+__global__ void k_fit_update(BatchArgs a, Workspace w) {
+    const int s = blockIdx.y;
+    if (w.status[s]) return;
+    const int P = w.sel_count[s];
+    const size_t base = (size_t)s * w.capD;
+    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
+        double* st = w.stencil + 6 * base + 6 * (size_t)p;
+        const double* ra = w.ratio + 3 * base + 3 * (size_t)p;
+        Stencil q{st[0], st[1], st[2], st[3], st[4], st[5]};
+        q.y1 = q.y1 * ra[0];
+        q.y2 = q.y2 * ra[1];
+        q.y3 = q.y3 * ra[2];
+        mirror_shoulder(q);
+        st[0] = q.x1; st[1] = q.x2; st[2] = q.x3; st[3] = q.y1; st[4] = q.y2; st[5] = q.y3;
+        solve(q, w.params + 3 * base + 3 * (size_t)p);
+    }
+}
+
+// K8  retain sfhw > CHECK_PRECISION && hw2 > CHECK_PRECISION, order preserving
+// (fitter_analytical.rs:67-69); copies min(count, cap) rows to the caller's output.
+template <int BS>
+__global__ __launch_bounds__(BS) void k_retain(BatchArgs a, Workspace w) {
+    const int s = blockIdx.x;
+    __shared__ int lds_i[BS / 64 + 1];
+    if (w.status[s]) {
+        if (threadIdx.x == 0) {
+            a.out_count[s] = 0;
+            a.out_mse[s] = 0.0;
+            a.out_status[s] = w.status[s];
+        }
+        return;
+    }
+    const int P = w.sel_count[s];
+    const size_t base = (size_t)s * w.capD;
+    const double* params = w.params + 3 * base;
+    const int per = (P + BS - 1) / BS;
+    const int p0 = threadIdx.x * per, p1 = min(P, p0 + per);
+    int keep = 0;
+    for (int p = p0; p < p1; ++p)
+        keep += (params[3 * p] > kCheckPrecision && params[3 * p + 1] > kCheckPrecision);
+    int total;
+    int o = block_exclusive_scan<BS>(keep, lds_i, &total);
+    double* kept = w.kept + 3 * base;
+    double* out = a.out + 3 * (size_t)s * a.cap;
+    for (int p = p0; p < p1; ++p) {
+        if (params[3 * p] > kCheckPrecision && params[3 * p + 1] > kCheckPrecision) {
+            kept[3 * o] = params[3 * p];
+            kept[3 * o + 1] = params[3 * p + 1];
+            kept[3 * o + 2] = params[3 * p + 2];
+            if (o < a.cap) {
+                out[3 * o] = params[3 * p];
+                out[3 * o + 1] = params[3 * p + 1];
+                out[3 * o + 2] = params[3 * p + 2];
+            }
+            ++o;
+        }
+    }
+    if (threadIdx.x == 0) {
+        w.kept_count[s] = total;
+        a.out_count[s] = total;
+    }
+}
+
+// ----------------------------------------------------------------------------------
+// K9  superposition over the MSE regions + squared residual, fixed-order tree
+// (deconvoluter.rs:540-543, compute_mse :828-862). Regions are walked as one
+// virtual concatenation so overlapping regions count twice, like the reference.
+// ----------------------------------------------------------------------------------
+__device__ __forceinline__ void mse_region(const Workspace& w, int s, int r, int nig, int64_t* lo,
+                                           int64_t* hi) {
+    const int64_t* pairs = w.ig + (size_t)s * 2 * kMaxIgnore;
+    *lo = r == 0 ? w.sbi[2 * s] : pairs[2 * (r - 1) + 1];
+    *hi = r == nig ? w.sbi[2 * s + 1] : pairs[2 * r];
+}
+
+template <int BS>
+__global__ __launch_bounds__(BS) void k_mse_partial(BatchArgs a, Workspace w) {
+    const int s = blockIdx.y;
+    __shared__ double red[BS / 64];
+    if (w.status[s] || w.mse_panic[s]) return;
+    const int P = w.kept_count[s];
+    const double* __restrict__ kept = w.kept + 3 * (size_t)s * w.capD;
+    const double* x = a.x + (size_t)s * a.x_stride;
+    const double* y = a.y + (size_t)s * a.y_stride;
+    const int nig = w.n_ig[s];
+    int64_t total = 0;
+    for (int r = 0; r <= nig; ++r) {
+        int64_t lo, hi;
+        mse_region(w, s, r, nig, &lo, &hi);
+        total += hi - lo;
+    }
+    double acc = 0.0;
+    for (int64_t v = (int64_t)blockIdx.x * BS + threadIdx.x; v < total;
+         v += (int64_t)gridDim.x * BS) {
+        int64_t rem = v, idx = 0;
+        for (int r = 0; r <= nig; ++r) {
+            int64_t lo, hi;
+            mse_region(w, s, r, nig, &lo, &hi);
+            if (rem < hi - lo) {
+                idx = lo + rem;
+                break;
+            }
+            rem -= hi - lo;
+        }
+        const double sup = superpose(x[idx], kept, P);
+        const double d = sup - y[idx];
+        acc += d * d;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int k = 0; k < BS / 64; ++k) t += red[k];
+        w.mse_part[(size_t)s * gridDim.x + blockIdx.x] = t;
+    }
+}
+
+__global__ void k_mse_final(BatchArgs a, Workspace w, int nparts) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= a.B) return;
+    if (w.status[s]) return;  // already reported by k_retain
+    if (w.mse_panic[s]) {
+        a.out_status[s] = MDG_REFERENCE_PANIC;
+        a.out_mse[s] = 0.0;
+        return;
+    }
+    const int nig = w.n_ig[s];
+    int64_t total = 0;
+    for (int r = 0; r <= nig; ++r) {
+        int64_t lo, hi;
+        mse_region(w, s, r, nig, &lo, &hi);
+        total += hi - lo;
+    }
+    double t = 0.0;
+    for (int k = 0; k < nparts; ++k) t += w.mse_part[(size_t)s * nparts + k];
+    a.out_mse[s] = t / (double)total;
+    a.out_status[s] = (w.kept_count[s] > a.cap) ? MDG_CAPACITY : MDG_OK;
+}
+
+// ----------------------------------------------------------------------------------
+// standalone Lorentzian::superposition_vec (lorentzian.rs:631-663)
+// ----------------------------------------------------------------------------------
+__global__ void k_superposition_vec(const double* __restrict__ x, int64_t n,
+                                    const double* __restrict__ params, int P,
+                                    double* __restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = superpose(x[i], params, P);
+}
+
+// synthetic batch: x shared, y_s = superposition(params_s) + noise(seed_s)
+__global__ void k_synth_x(double* x, int64_t n, double xmax, double width) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) x[i] = xmax - ((double)i * width) / ((double)n - 1.0);
+}
+
+__global__ void k_synth_y(const double* __restrict__ x, int64_t n,
+                          const double* __restrict__ params, int P, uint64_t seed0,
+                          double sigma, double* __restrict__ y) {
+    const int s = blockIdx.y;
+    const uint64_t key = stream_key(seed0 + (uint64_t)s, kStreamNoise);
+    const double* ps = params + 3 * (size_t)s * P;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        y[(size_t)s * n + i] = superpose(x[i], ps, P) + synth_noise(key, (uint64_t)i, sigma);
+}
+
+// ----------------------------------------------------------------------------------
+// launchers
+// ----------------------------------------------------------------------------------
+static inline unsigned cdiv(int64_t a, int64_t b) { return (unsigned)((a + b - 1) / b); }
+
+void launch_prep(const BatchArgs& a, const Workspace& w, hipStream_t st) {
+    hipLaunchKernelGGL(k_prep, dim3(cdiv(a.B, 64)), dim3(64), 0, st, a, w);
+}
+void launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int ws, hipStream_t st) {
+    hipLaunchKernelGGL(k_smooth, dim3(cdiv(a.B, 64)), dim3(64), 0, st, a, w, iters, ws);
+}
+void launch_flags(const BatchArgs& a, const Workspace& w, hipStream_t st) {
+    hipLaunchKernelGGL(k_flags, dim3(cdiv(a.N, 256), a.B), dim3(256), 0, st, a, w);
+}
+void launch_peaks(const BatchArgs& a, const Workspace& w, int detector_only, hipStream_t st) {
+    hipLaunchKernelGGL(k_peaks<1024>, dim3(a.B), dim3(1024), 0, st, a, w, detector_only);
+}
+void launch_select(const BatchArgs& a, const Workspace& w, int detector_only, double threshold,
+                   hipStream_t st) {
+    if (detector_only)
+        hipLaunchKernelGGL(k_select_detector_only, dim3(16, a.B), dim3(256), 0, st, a, w);
+    else
+        hipLaunchKernelGGL(k_select<1024>, dim3(a.B), dim3(1024), 0, st, a, w, threshold);
+}
+void launch_fit_init(const BatchArgs& a, const Workspace& w, int gx, hipStream_t st) {
+    hipLaunchKernelGGL(k_fit_init, dim3(gx, a.B), dim3(256), 0, st, a, w);
+}
+void launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, hipStream_t st) {
+    hipLaunchKernelGGL(k_fit_sup, dim3(gx, a.B), dim3(256), 0, st, a, w);
+}
+void launch_fit_update(const BatchArgs& a, const Workspace& w, int gx, hipStream_t st) {
+    hipLaunchKernelGGL(k_fit_update, dim3(gx, a.B), dim3(256), 0, st, a, w);
+}
+void launch_retain(const BatchArgs& a, const Workspace& w, hipStream_t st) {
+    hipLaunchKernelGGL(k_retain<1024>, dim3(a.B), dim3(1024), 0, st, a, w);
+}
+void launch_mse(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st) {
+    hipLaunchKernelGGL(k_mse_partial<256>, dim3(nparts, a.B), dim3(256), 0, st, a, w);
+}
+void launch_mse_final(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st) {
+    hipLaunchKernelGGL(k_mse_final, dim3(cdiv(a.B, 64)), dim3(64), 0, st, a, w, nparts);
+}
+void launch_superposition_vec(const double* x, int64_t n, const double* params, int P,
+                              double* out, hipStream_t st) {
+    const unsigned g = std::max(1u, std::min(cdiv(n, 256), 65535u));
+    hipLaunchKernelGGL(k_superposition_vec, dim3(g), dim3(256), 0, st, x, n, params, P, out);
+}
+void launch_synth(double* x, double* y, int64_t n, int B, double xmax, double width,
+                  const double* params, int P, uint64_t seed0, double sigma, hipStream_t st) {
+    hipLaunchKernelGGL(k_synth_x, dim3(cdiv(n, 256)), dim3(256), 0, st, x, n, xmax, width);
+    const unsigned g = std::max(1u, std::min(cdiv(n, 256), 2048u));
+    hipLaunchKernelGGL(k_synth_y, dim3(g, B), dim3(256), 0, st, x, n, params, P, seed0, sigma, y);
+}
+
+}  // namespace mdg

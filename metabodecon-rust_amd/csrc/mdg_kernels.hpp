@@ -1,0 +1,92 @@
+// mdg_kernels.hpp -- kernel argument blocks and launchers (internal to libmdgpu).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+
+#include "../../include/mdgpu.h"
+#include "mdg_common.hpp"
+
+namespace mdg {
+
+// Per-call arguments: caller-owned device arrays (inputs resident in HBM).
+struct BatchArgs {
+    int B;                // spectra in the batch
+    int N;                // points per spectrum
+    const double* x;      // row s at x + s*x_stride (x_stride 0: shared axis)
+    int64_t x_stride;
+    const double* y;      // row s at y + s*y_stride
+    int64_t y_stride;
+    const double* sb;     // 2B signal boundaries (ppm, ordered as Spectrum stores them)
+    int n_ignore;         // merged ignore regions (ppm), shared by the batch
+    double ignore[2 * kMaxIgnore];
+    double* out;          // B x cap x {sfhw, hw2, maxp}
+    int cap;
+    int32_t* out_count;
+    double* out_mse;
+    int32_t* out_status;
+};
+
+// Context-owned device workspace (sized for the worst case of the batch shape).
+// Layout in HBM, all per-spectrum rows contiguous ("spectrum-major"):
+//   smooth/tmp0/tmp1   B x N f64
+//   masks              B x 3 x W u64   (center / right / left predicate bits)
+//   det_* / sel_*      B x capD i32    (peak index triples, SoA)
+//   scores             B x capD f64
+//   params, kept       B x capD x 3 f64 (AoS {sfhw,hw2,maxp}: wave-uniform SMEM reads)
+//   stencil            B x capD x 6 f64
+//   rx, ry, ratio      B x 3capD f64   (reduced spectrum, fitter order l,c,r)
+struct Workspace {
+    int W;                    // mask words per spectrum = ceil(N/64)
+    int capD;                 // peak capacity per spectrum = N/2 + 2
+    const double* smooth_ptr; // smoothed intensities (== y for the identity smoother)
+    int64_t smooth_stride;
+    double* smooth;
+    double* tmp0;
+    double* tmp1;
+    uint64_t* masks;
+    int32_t* det_l;
+    int32_t* det_c;
+    int32_t* det_r;
+    int32_t* sel_l;
+    int32_t* sel_c;
+    int32_t* sel_r;
+    double* scores;
+    double* params;
+    double* kept;
+    double* stencil;
+    double* rx;
+    double* ry;
+    double* ratio;
+    double* mse_part;         // B x nparts
+    double* sfr_stats;        // B x {mean, sd}
+    int64_t* sbi;             // B x 2
+    int64_t* ig;              // B x 2*kMaxIgnore
+    int32_t* n_ig;
+    int32_t* mse_panic;
+    int32_t* status;
+    int32_t* det_count;
+    int32_t* sel_count;
+    int32_t* kept_count;
+};
+
+void launch_prep(const BatchArgs& a, const Workspace& w, hipStream_t st);
+void launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int ws, hipStream_t st);
+void launch_flags(const BatchArgs& a, const Workspace& w, hipStream_t st);
+void launch_peaks(const BatchArgs& a, const Workspace& w, int detector_only, hipStream_t st);
+void launch_select(const BatchArgs& a, const Workspace& w, int detector_only, double threshold,
+                   hipStream_t st);
+void launch_fit_init(const BatchArgs& a, const Workspace& w, int gx, hipStream_t st);
+void launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, hipStream_t st);
+void launch_fit_update(const BatchArgs& a, const Workspace& w, int gx, hipStream_t st);
+void launch_retain(const BatchArgs& a, const Workspace& w, hipStream_t st);
+void launch_mse(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st);
+void launch_mse_final(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st);
+void launch_superposition_vec(const double* x, int64_t n, const double* params, int P,
+                              double* out, hipStream_t st);
+void launch_synth(double* x, double* y, int64_t n, int B, double xmax, double width,
+                  const double* params, int P, uint64_t seed0, double sigma, hipStream_t st);
+
+}  // namespace mdg

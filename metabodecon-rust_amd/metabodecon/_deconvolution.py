@@ -1,0 +1,393 @@
+"""``Deconvoluter`` / ``Deconvolution`` / ``Lorentzian`` over the C ABI.
+
+Mirrors metabodecon-python/src/bindings/{deconvoluter,deconvolution,lorentzian}.rs
+(method names, argument meaning and exceptions). Every ``deconvolute_*`` and
+``*superposition_vec`` call runs the HIP path in libmdgpu.so; scalar helpers
+(``evaluate``, ``superposition`` at one point) are evaluated on the host with
+the same operation order as lorentzian.rs:546-611.
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import math
+
+import numpy as np
+
+from . import _native as nat
+from . import exceptions as exc
+from ._spectrum import Spectrum
+
+_sz = ctypes.c_size_t
+
+
+# =====================================================================================
+# Lorentzian (bindings/lorentzian.rs:24-113, lorentzian.rs:138-663)
+# =====================================================================================
+class Lorentzian:
+    __slots__ = ("sfhw", "hw2", "_maxp")
+
+    def __init__(self, sf: float, hw: float, maxp: float):
+        # bindings/lorentzian.rs:26-31: untransformed parameters
+        self.sfhw = float(sf) * float(hw)
+        self.hw2 = float(hw) * float(hw)
+        self._maxp = float(maxp)
+
+    @staticmethod
+    def from_transformed(sfhw: float, hw2: float, maxp: float) -> "Lorentzian":
+        lz = Lorentzian.__new__(Lorentzian)
+        lz.sfhw, lz.hw2, lz._maxp = float(sfhw), float(hw2), float(maxp)
+        return lz
+
+    @property
+    def hw(self) -> float:
+        return math.sqrt(self.hw2)  # lorentzian.rs:428
+
+    @hw.setter
+    def hw(self, hw: float):  # lorentzian.rs:501-504
+        self.sfhw = self.sf * hw
+        self.hw2 = hw * hw
+
+    @property
+    def sf(self) -> float:
+        return self.sfhw / self.hw  # lorentzian.rs:406
+
+    @sf.setter
+    def sf(self, sf: float):  # lorentzian.rs:477-479
+        self.sfhw = sf * self.hw
+
+    @property
+    def maxp(self) -> float:
+        return self._maxp
+
+    @maxp.setter
+    def maxp(self, v: float):
+        self._maxp = float(v)
+
+    def parameters(self) -> tuple[float, float, float]:
+        return self.sfhw, self.hw2, self._maxp
+
+    def evaluate(self, x: float) -> float:
+        d = float(x) - self._maxp
+        return self.sfhw / (self.hw2 + d * d)
+
+    def evaluate_vec(self, x) -> np.ndarray:
+        x = np.asarray(x, dtype=np.float64)
+        d = x - self._maxp
+        return self.sfhw / (self.hw2 + d * d)
+
+    def integral(self) -> float:
+        return math.pi * self.sf
+
+    @staticmethod
+    def superposition(x: float, lorentzians) -> float:
+        acc = -0.0
+        for lz in lorentzians:
+            acc += lz.evaluate(x)
+        return acc
+
+    @staticmethod
+    def superposition_vec(x, lorentzians) -> np.ndarray:
+        return superposition_vec(x, _params_of(lorentzians))
+
+    @staticmethod
+    def par_superposition_vec(x, lorentzians) -> np.ndarray:
+        return superposition_vec(x, _params_of(lorentzians))
+
+    def __repr__(self) -> str:
+        return f"Lorentzian(sfhw={self.sfhw!r}, hw2={self.hw2!r}, maxp={self._maxp!r})"
+
+
+def _params_of(lorentzians) -> np.ndarray:
+    if isinstance(lorentzians, np.ndarray):
+        return np.ascontiguousarray(lorentzians, dtype=np.float64).reshape(-1, 3)
+    return np.array([lz.parameters() for lz in lorentzians], dtype=np.float64).reshape(-1, 3)
+
+
+def superposition_vec(x, params: np.ndarray, device: int | None = None) -> np.ndarray:
+    """Lorentzian::superposition_vec on the GPU (lorentzian.rs:631-663)."""
+    xa = np.asarray(x, dtype=np.float64)
+    if xa.ndim != 1 or not xa.flags.c_contiguous:
+        # the reference's `as_slice().unwrap()` panics on non-contiguous input
+        # (bindings/deconvolution.rs:63-75); we accept it and copy instead.
+        xa = np.ascontiguousarray(xa.reshape(-1))
+    params = np.ascontiguousarray(params, dtype=np.float64).reshape(-1, 3)
+    out = np.empty(xa.size)
+    ctx = nat.context(device)
+    with ctx.lock:
+        st = nat.lib().mdg_superposition_vec(ctx.handle, nat.ptr(xa), xa.size, nat.ptr(params),
+                                             params.shape[0], nat.ptr(out))
+    if st:
+        raise exc.UnexpectedError(f"superposition_vec failed: {nat.strerror(st)}")
+    return out
+
+
+# =====================================================================================
+# settings serialisation (serde forms, smoother.rs/selector.rs/fitter.rs)
+# =====================================================================================
+def _settings_json(s: nat.Settings) -> tuple[dict, dict, dict]:
+    sm = ({"method": "MovingAverage", "iterations": s.smooth_iterations,
+           "windowSize": s.smooth_window} if s.smoother == 1 else {"method": "Identity"})
+    se = ({"method": "NoiseScoreFilter", "scoringMethod": {"method": "MinimumSum"},
+           "threshold": s.threshold} if s.selector == 1 else {"method": "DetectorOnly"})
+    fi = {"method": "Analytical", "iterations": s.fit_iterations}
+    return sm, se, fi
+
+
+def _settings_from_json(sm: dict, se: dict, fi: dict) -> nat.Settings:
+    s = nat.default_settings()
+    if sm["method"] == "Identity":
+        s.smoother = 0
+    else:
+        s.smoother = 1
+        s.smooth_iterations = int(sm["iterations"])
+        s.smooth_window = int(sm["windowSize"])
+    if se["method"] == "DetectorOnly":
+        s.selector = 0
+    else:
+        s.selector = 1
+        s.threshold = float(se["threshold"])
+    s.fit_iterations = int(fi["iterations"])
+    st = nat.validate(s)
+    if st:
+        raise exc.from_status(st)
+    return s
+
+
+# =====================================================================================
+# Deconvolution (bindings/deconvolution.rs:45-116, deconvolution.rs:45-115)
+# =====================================================================================
+class Deconvolution:
+    def __init__(self, params: np.ndarray, mse: float, settings: nat.Settings):
+        self._params = np.ascontiguousarray(params, dtype=np.float64).reshape(-1, 3)
+        self._params.setflags(write=False)
+        self._mse = float(mse)
+        self._settings = settings.copy()
+
+    @property
+    def lorentzians(self) -> list[Lorentzian]:
+        return [Lorentzian.from_transformed(*row) for row in self._params.tolist()]
+
+    @property
+    def params(self) -> np.ndarray:
+        """(P, 3) array of transformed parameters (sfhw, hw2, maxp)."""
+        return self._params
+
+    @property
+    def mse(self) -> float:
+        return self._mse
+
+    def superposition(self, x: float) -> float:
+        acc = -0.0
+        for sfhw, hw2, maxp in self._params.tolist():
+            d = float(x) - maxp
+            acc += sfhw / (hw2 + d * d)
+        return acc
+
+    def superposition_vec(self, x) -> np.ndarray:
+        return superposition_vec(x, self._params)
+
+    def par_superposition_vec(self, x) -> np.ndarray:
+        return superposition_vec(x, self._params)
+
+    # serde JSON form of serialized_deconvolution.rs:18-31 / serialized_lorentzian.rs:16-43
+    def to_json_dict(self) -> dict:
+        sm, se, fi = _settings_json(self._settings)
+        lz = []
+        for sfhw, hw2, maxp in self._params.tolist():
+            hw = math.sqrt(hw2)
+            lz.append({"sf": sfhw / hw, "hw": hw, "maxp": maxp})
+        return {"smoothingSettings": sm, "selectionSettings": se, "fittingSettings": fi,
+                "mse": self._mse, "lorentzians": lz}
+
+    def write_json(self, path: str) -> None:
+        with open(path, "w") as f:
+            json.dump(self.to_json_dict(), f, indent=2)
+
+    @staticmethod
+    def read_json(path: str) -> "Deconvolution":
+        try:
+            with open(path) as f:
+                d = json.load(f)
+            s = _settings_from_json(d["smoothingSettings"], d["selectionSettings"],
+                                    d["fittingSettings"])
+            p = np.array([[l["sf"] * l["hw"], l["hw"] * l["hw"], l["maxp"]]
+                          for l in d["lorentzians"]], dtype=np.float64).reshape(-1, 3)
+            return Deconvolution(p, d["mse"], s)
+        except (KeyError, TypeError, ValueError) as e:
+            raise exc.SerializationError(str(e)) from None
+
+    def __repr__(self) -> str:
+        return f"Deconvolution(lorentzians={self._params.shape[0]}, mse={self._mse!r})"
+
+
+# =====================================================================================
+# Deconvoluter (bindings/deconvoluter.rs:17-165, deconvoluter.rs:118-905)
+# =====================================================================================
+class Deconvoluter:
+    MAX_IGNORE = 16
+
+    def __init__(self):
+        self._s = nat.default_settings()
+        self._ignore: list[tuple[float, float]] | None = None
+        self._threads: int | None = None
+        self.device: int | None = None
+
+    # ---- settings -----------------------------------------------------------------
+    def _apply(self, s: nat.Settings):
+        st = nat.validate(s)
+        if st:
+            raise exc.from_status(st)
+        self._s = s
+
+    def set_identity_smoother(self) -> None:
+        s = self._s.copy()
+        s.smoother = 0
+        self._apply(s)
+
+    def set_moving_average_smoother(self, iterations: int, window_size: int) -> None:
+        if iterations < 0 or window_size < 0:
+            raise OverflowError("can't convert negative int to unsigned")
+        s = self._s.copy()
+        s.smoother, s.smooth_iterations, s.smooth_window = 1, iterations, window_size
+        self._apply(s)
+
+    def set_detector_only(self) -> None:
+        s = self._s.copy()
+        s.selector = 0
+        self._apply(s)
+
+    def set_noise_score_selector(self, threshold: float) -> None:
+        s = self._s.copy()
+        s.selector, s.scoring, s.threshold = 1, 0, float(threshold)
+        self._apply(s)
+
+    def set_analytical_fitter(self, iterations: int) -> None:
+        if iterations < 0:
+            raise OverflowError("can't convert negative int to unsigned")
+        s = self._s.copy()
+        s.fitter, s.fit_iterations = 0, iterations
+        self._apply(s)
+
+    @property
+    def settings(self) -> nat.Settings:
+        return self._s.copy()
+
+    def add_ignore_region(self, boundaries) -> None:
+        a, b = float(boundaries[0]), float(boundaries[1])
+        cur = self._ignore or []
+        cap = len(cur) + 1
+        buf = np.zeros(2 * cap)
+        for i, (lo, hi) in enumerate(cur):
+            buf[2 * i], buf[2 * i + 1] = lo, hi
+        n = _sz(0)
+        st = nat.lib().mdg_ignore_region_add(nat.ptr(buf), len(cur), cap, a, b, ctypes.byref(n))
+        if st:
+            raise exc.InvalidIgnoreRegion(
+                f"ignore region boundaries [{a}, {b}] are invalid")
+        self._ignore = [(float(buf[2 * i]), float(buf[2 * i + 1])) for i in range(n.value)]
+
+    def clear_ignore_regions(self) -> None:
+        self._ignore = None
+
+    @property
+    def ignore_regions(self) -> list[tuple[float, float]] | None:
+        return None if self._ignore is None else list(self._ignore)
+
+    def set_threads(self, threads: int) -> None:
+        # bindings/deconvoluter.rs:92-106; the GPU engine has no CPU pool to size
+        if threads <= 1:
+            raise ValueError("number of threads must be greater than 1")
+        self._threads = threads
+
+    def clear_threads(self) -> None:
+        self._threads = None
+
+    # ---- hot path -------------------------------------------------------------------
+    def _ignore_array(self) -> np.ndarray:
+        if not self._ignore:
+            return np.zeros(0)
+        if len(self._ignore) > self.MAX_IGNORE:
+            raise exc.UnexpectedError(f"more than {self.MAX_IGNORE} ignore regions")
+        return np.array(self._ignore, dtype=np.float64).reshape(-1)
+
+    def _run(self, spectra: list[Spectrum]) -> list[tuple[int, np.ndarray, float]]:
+        """One batched GPU call per distinct spectrum length; returns per-spectrum
+        (status, params, mse) in input order."""
+        results: list = [None] * len(spectra)
+        by_n: dict[int, list[int]] = {}
+        for i, sp in enumerate(spectra):
+            if not isinstance(sp, Spectrum):
+                raise TypeError("expected metabodecon.Spectrum")
+            by_n.setdefault(len(sp), []).append(i)
+        ign = self._ignore_array()
+        ctx = nat.context(self.device)
+        for n, idx in by_n.items():
+            b = len(idx)
+            x = np.stack([spectra[i].chemical_shifts for i in idx])
+            y = np.stack([spectra[i].intensities for i in idx])
+            sb = np.array([spectra[i].signal_boundaries for i in idx], dtype=np.float64)
+            cap = n // 2 + 2
+            out = np.empty((b, cap, 3))
+            counts = np.zeros(b, dtype=np.uintp)
+            mse = np.zeros(b)
+            status = np.zeros(b, dtype=np.intc)
+            with ctx.lock:
+                rc = nat.lib().mdg_deconvolute_batch(
+                    ctx.handle, b, n, nat.ptr(x), n, nat.ptr(y), n, nat.ptr(sb),
+                    ctypes.byref(self._s), nat.ptr(ign) if ign.size else None, ign.size // 2,
+                    nat.ptr(out), cap, nat.ptr(counts, nat._szp), nat.ptr(mse),
+                    status.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+            if rc >= 100 or rc == nat.INVALID_ARGUMENT:
+                raise exc.UnexpectedError(f"GPU engine failure: {nat.strerror(rc)}")
+            for k, i in enumerate(idx):
+                results[i] = (int(status[k]), out[k, : int(counts[k])].copy(), float(mse[k]))
+        return results
+
+    def _collect(self, results) -> list[Deconvolution]:
+        out = []
+        for st, params, mse in results:  # fail-fast Result collect (deconvoluter.rs:655-658)
+            if st:
+                raise exc.from_status(st)
+            out.append(Deconvolution(params, mse, self._s))
+        return out
+
+    def deconvolute_spectrum(self, spectrum: Spectrum) -> Deconvolution:
+        return self._collect(self._run([spectrum]))[0]
+
+    def par_deconvolute_spectrum(self, spectrum: Spectrum) -> Deconvolution:
+        return self._collect(self._run([spectrum]))[0]
+
+    def deconvolute_spectra(self, spectra) -> list[Deconvolution]:
+        spectra = list(spectra)
+        if not spectra:
+            return []
+        return self._collect(self._run(spectra))
+
+    def par_deconvolute_spectra(self, spectra) -> list[Deconvolution]:
+        return self.deconvolute_spectra(spectra)
+
+    def optimize_settings(self, reference: Spectrum) -> float:
+        """deconvoluter.rs:762-825: grid of 27 smoothing x 10 selection x 3 fitting
+        settings, keep the first minimum MSE. Each combination runs on the GPU."""
+        smoothing = [(it, ws) for it in range(2, 11) for ws in (3, 5, 7)]
+        selection = [5.0 + (c * (8.0 - 5.0)) / 9.0 for c in range(10)]
+        fitting = [5, 10, 15]
+        best = None
+        for it, ws in smoothing:
+            for thr in selection:
+                for fit in fitting:
+                    d = Deconvoluter()
+                    d._ignore = self._ignore
+                    d.device = self.device
+                    d.set_moving_average_smoother(it, ws)
+                    d.set_noise_score_selector(thr)
+                    d.set_analytical_fitter(fit)
+                    res = d.deconvolute_spectrum(reference)
+                    if best is None or res.mse < best[0]:
+                        best = (res.mse, it, ws, thr, fit)
+        mse, it, ws, thr, fit = best
+        self.set_moving_average_smoother(it, ws)
+        self.set_noise_score_selector(thr)
+        self.set_analytical_fitter(fit)
+        return mse

@@ -1,0 +1,236 @@
+"""ctypes binding of libmdgpu.so (the C ABI declared in include/mdgpu.h).
+
+This is the only way the Python package reaches the hot path. There is no CPU
+fallback: if the HIP library is missing or no MI355X is visible, the compute
+entry points raise ``NativeLibraryError``/``DeviceUnavailableError`` loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MDGPU_LIB", os.path.join(_HERE, "libmdgpu.so"))
+
+OK = 0
+NO_PEAKS_DETECTED = 1
+EMPTY_SIGNAL_REGION = 2
+EMPTY_SIGNAL_FREE_REGION = 3
+INVALID_SMOOTHING = 10
+INVALID_SELECTION = 11
+INVALID_FITTING = 12
+INVALID_IGNORE_REGION = 13
+INVALID_ARGUMENT = 20
+CAPACITY = 21
+REFERENCE_PANIC = 30
+ERR_HIP = 100
+ERR_NO_DEVICE = 101
+ERR_OUT_OF_MEMORY = 102
+
+N_STAGES = 12
+STAGE_NAMES = ["prep", "smooth", "detect", "select", "fit_init", "fit_superposition",
+               "fit_update", "retain", "mse_superposition", "mse_reduce", "superposition_vec",
+               "synth"]
+
+# every symbol include/mdgpu.h declares (checked by tests/test_capi_exports.py)
+EXPORTS = [
+    "mdg_abi_version", "mdg_strerror", "mdg_settings_default", "mdg_settings_validate",
+    "mdg_ignore_region_add", "mdg_synth_lorentzians", "mdg_synth_noise", "mdg_device_count",
+    "mdg_ctx_create", "mdg_ctx_destroy", "mdg_ctx_set_stream", "mdg_ctx_synchronize",
+    "mdg_ctx_set_profiling", "mdg_ctx_stage_times", "mdg_ctx_reset_stage_times",
+    "mdg_deconvolute", "mdg_deconvolute_batch", "mdg_deconvolute_batch_device",
+    "mdg_superposition_vec", "mdg_superposition_vec_device", "mdg_synth_batch_device",
+    "mdg_ctx_last_peaks",
+]
+
+
+class NativeLibraryError(ImportError):
+    pass
+
+
+class DeviceUnavailableError(RuntimeError):
+    pass
+
+
+class Settings(ctypes.Structure):
+    _fields_ = [
+        ("smoother", ctypes.c_int32),
+        ("smooth_iterations", ctypes.c_uint32),
+        ("smooth_window", ctypes.c_uint32),
+        ("selector", ctypes.c_int32),
+        ("scoring", ctypes.c_int32),
+        ("fit_iterations", ctypes.c_uint32),
+        ("fitter", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+        ("threshold", ctypes.c_double),
+    ]
+
+    def copy(self) -> "Settings":
+        s = Settings()
+        ctypes.memmove(ctypes.byref(s), ctypes.byref(self), ctypes.sizeof(Settings))
+        return s
+
+
+_dp = ctypes.POINTER(ctypes.c_double)
+_szp = ctypes.POINTER(ctypes.c_size_t)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_vp = ctypes.c_void_p
+_sz = ctypes.c_size_t
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        with _lib_lock:
+            if _lib is None:
+                if not os.path.exists(LIB_PATH):
+                    raise NativeLibraryError(
+                        f"libmdgpu.so not found at {LIB_PATH}; build it with "
+                        "`make -C metabodecon-rust_amd` (hipcc, gfx950)")
+                L = ctypes.CDLL(LIB_PATH)
+                _declare(L)
+                _lib = L
+    return _lib
+
+
+def _declare(L):
+    sp = ctypes.POINTER(Settings)
+    L.mdg_abi_version.restype = ctypes.c_int
+    L.mdg_strerror.argtypes = [ctypes.c_int]
+    L.mdg_strerror.restype = ctypes.c_char_p
+    L.mdg_settings_default.argtypes = [sp]
+    L.mdg_settings_default.restype = None
+    L.mdg_settings_validate.argtypes = [sp]
+    L.mdg_ignore_region_add.argtypes = [_dp, _sz, _sz, ctypes.c_double, ctypes.c_double, _szp]
+    L.mdg_synth_lorentzians.argtypes = [ctypes.c_uint64, _sz, ctypes.c_double, ctypes.c_double, _dp]
+    L.mdg_synth_noise.argtypes = [ctypes.c_uint64, _sz, ctypes.c_double, _dp]
+    L.mdg_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
+    L.mdg_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(_vp)]
+    L.mdg_ctx_destroy.argtypes = [_vp]
+    L.mdg_ctx_set_stream.argtypes = [_vp, _vp]
+    L.mdg_ctx_synchronize.argtypes = [_vp]
+    L.mdg_ctx_set_profiling.argtypes = [_vp, ctypes.c_int]
+    L.mdg_ctx_stage_times.argtypes = [_vp, _dp, _u64p, ctypes.c_int]
+    L.mdg_ctx_reset_stage_times.argtypes = [_vp]
+    L.mdg_deconvolute.argtypes = [_vp, _dp, _dp, _sz, ctypes.c_double, ctypes.c_double, sp, _dp,
+                                  _sz, _dp, _sz, _szp, _dp]
+    L.mdg_deconvolute_batch.argtypes = [_vp, _sz, _sz, _dp, _sz, _dp, _sz, _dp, sp, _dp, _sz,
+                                        _dp, _sz, _szp, _dp, ctypes.POINTER(ctypes.c_int)]
+    L.mdg_deconvolute_batch_device.argtypes = [_vp, _sz, _sz, _vp, _sz, _vp, _sz, _vp, sp, _dp,
+                                               _sz, _vp, _sz, _vp, _vp, _vp]
+    L.mdg_superposition_vec.argtypes = [_vp, _dp, _sz, _dp, _sz, _dp]
+    L.mdg_superposition_vec_device.argtypes = [_vp, _vp, _sz, _vp, _sz, _vp]
+    L.mdg_ctx_last_peaks.argtypes = [_vp, _sz, ctypes.c_int, _i32p, _i32p, _i32p, _sz, _szp]
+    L.mdg_synth_batch_device.argtypes = [_vp, _sz, _sz, ctypes.c_double, ctypes.c_double,
+                                         ctypes.c_uint64, _sz, ctypes.c_double, ctypes.c_double,
+                                         ctypes.c_double, _vp, _vp]
+
+
+def strerror(status: int) -> str:
+    return lib().mdg_strerror(status).decode()
+
+
+def default_settings() -> Settings:
+    s = Settings()
+    lib().mdg_settings_default(ctypes.byref(s))
+    return s
+
+
+def validate(s: Settings) -> int:
+    return lib().mdg_settings_validate(ctypes.byref(s))
+
+
+def ptr(a: np.ndarray, t=_dp):
+    return a.ctypes.data_as(t)
+
+
+class Context:
+    """One device context (stream + reusable HBM workspace) of libmdgpu."""
+
+    def __init__(self, device: int = 0):
+        n = ctypes.c_int(0)
+        lib().mdg_device_count(ctypes.byref(n))
+        if n.value <= 0:
+            raise DeviceUnavailableError(
+                "no HIP device visible: the metabodecon GPU engine needs an MI355X "
+                "(there is deliberately no CPU fallback)")
+        h = _vp()
+        st = lib().mdg_ctx_create(device, ctypes.byref(h))
+        if st:
+            raise DeviceUnavailableError(f"mdg_ctx_create({device}) failed: {strerror(st)}")
+        self.handle = h
+        self.device = device
+        self.lock = threading.Lock()
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib().mdg_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream_ptr: int | None):
+        lib().mdg_ctx_set_stream(self.handle, _vp(stream_ptr or 0))
+
+    def synchronize(self):
+        st = lib().mdg_ctx_synchronize(self.handle)
+        if st:
+            raise RuntimeError(strerror(st))
+
+    def set_profiling(self, on: bool):
+        lib().mdg_ctx_set_profiling(self.handle, 1 if on else 0)
+
+    def stage_times(self) -> dict:
+        ms = np.zeros(N_STAGES)
+        n = np.zeros(N_STAGES, dtype=np.uint64)
+        lib().mdg_ctx_stage_times(self.handle, ptr(ms), ptr(n, _u64p), N_STAGES)
+        return {STAGE_NAMES[i]: (float(ms[i]), int(n[i])) for i in range(N_STAGES)}
+
+    def last_peaks(self, spectrum: int, which: str = "selected") -> np.ndarray:
+        """(count, 3) int32 (left, center, right) of the last batch run."""
+        k = 0 if which == "detected" else 1
+        cnt = ctypes.c_size_t(0)
+        lib().mdg_ctx_last_peaks(self.handle, spectrum, k, None, None, None, 0, ctypes.byref(cnt))
+        n = cnt.value
+        l, c, r = (np.zeros(max(n, 1), dtype=np.int32) for _ in range(3))
+        st = lib().mdg_ctx_last_peaks(self.handle, spectrum, k, ptr(l, _i32p), ptr(c, _i32p),
+                                      ptr(r, _i32p), n, ctypes.byref(cnt))
+        if st:
+            raise RuntimeError(strerror(st))
+        return np.stack([l[:n], c[:n], r[:n]], axis=1)
+
+    def reset_stage_times(self):
+        lib().mdg_ctx_reset_stage_times(self.handle)
+
+
+_ctx: dict[int, Context] = {}
+_ctx_lock = threading.Lock()
+
+
+def default_device() -> int:
+    env = os.environ.get("MDGPU_DEVICE")
+    if env is not None:
+        return int(env)
+    return 0
+
+
+def context(device: int | None = None) -> Context:
+    if device is None:
+        device = default_device()
+    with _ctx_lock:
+        c = _ctx.get(device)
+        if c is None:
+            c = Context(device)
+            _ctx[device] = c
+        return c

@@ -1,0 +1,43 @@
+"""Regenerate the golden fixtures under tests/golden/expected/ from the C oracle.
+
+The oracle (oracle/md_oracle.c) is pinned by the reference's own known-answer
+tests (tests/test_oracle_known_answers.py). The Rust reference cannot be built
+in this image (no cargo/rustc), so these end-to-end outputs are the oracle's;
+they freeze it so that a later change to either side shows up as a diff.
+
+Inputs: the reference's Bruker fixtures copied verbatim to tests/golden/bruker/
+(data files only) and the synthetic generator of libmdgpu (host functions
+mdg_synth_lorentzians / mdg_synth_noise; no GPU needed).
+
+    python tests/golden/make_golden.py
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "metabodecon-rust_amd")]
+
+import oracle  # noqa: E402
+from tests.golden.cases import CASES, load_case  # noqa: E402
+
+
+def main():
+    out_dir = os.path.join(HERE, "expected")
+    os.makedirs(out_dir, exist_ok=True)
+    for name in CASES:
+        x, y, sb, settings, ignore = load_case(name)
+        r = oracle.deconvolute(x, y, sb, settings, ignore=ignore)
+        np.savez_compressed(
+            os.path.join(out_dir, f"{name}.npz"),
+            status=np.int64(r.status), params=r.params, mse=np.float64(r.mse),
+            selected=r.selected, n_detected=np.int64(r.n_detected),
+            sbi=np.array(r.sbi, dtype=np.int64), sfr=np.array([r.sfr_mean, r.sfr_sd]))
+        print(f"{name:28s} status={r.status} det={r.n_detected} sel={r.n_selected} "
+              f"kept={r.params.shape[0]} mse={r.mse:.6e}")
+
+
+if __name__ == "__main__":
+    main()

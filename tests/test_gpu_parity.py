@@ -1,0 +1,270 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and goldens.
+
+Tolerances (north star: Lorentzians within 1e-6 relative, peak index sets
+bit-identical): we require MORE -- peak index sets, Lorentzian parameters and
+superposition vectors bit-identical (np.array_equal), and the MSE within
+MSE_RTOL = 1e-12 relative (its residual sum is a fixed-order tree on the GPU
+instead of the reference's left fold, deconvoluter.rs:850-856).
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from tests.conftest import GOLDEN
+from tests.golden.cases import CASES, load_case, synth_spectrum
+
+pytestmark = pytest.mark.gpu
+
+MSE_RTOL = 1e-12
+
+nat = pytest.importorskip("metabodecon._native")
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return nat.context(0)
+
+
+def gpu_batch(ctx, xs, ys, sbs, settings, ignore=()):
+    """Run mdg_deconvolute_batch on host arrays; returns status, counts, params, mse."""
+    ys = np.ascontiguousarray(ys, dtype=np.float64)
+    b, n = ys.shape
+    xs = np.ascontiguousarray(xs, dtype=np.float64)
+    x_stride = 0 if xs.ndim == 1 else n
+    sbs = np.ascontiguousarray(np.broadcast_to(np.asarray(sbs, dtype=np.float64), (b, 2)))
+    s = nat.Settings()
+    for f, _ in nat.Settings._fields_:
+        setattr(s, f, getattr(settings, f))
+    ign = np.asarray(ignore, dtype=np.float64).reshape(-1)
+    cap = n // 2 + 2
+    out = np.zeros((b, cap, 3))
+    counts = np.zeros(b, dtype=np.uintp)
+    mse = np.zeros(b)
+    status = np.zeros(b, dtype=np.intc)
+    rc = nat.lib().mdg_deconvolute_batch(
+        ctx.handle, b, n, nat.ptr(xs), x_stride, nat.ptr(ys), n, nat.ptr(sbs), ctypes.byref(s),
+        nat.ptr(ign) if ign.size else None, ign.size // 2, nat.ptr(out), cap,
+        nat.ptr(counts, nat._szp), nat.ptr(mse), status.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+    assert rc < 100, nat.strerror(rc)
+    return status, counts.astype(int), out, mse
+
+
+def check_against(golden_params, golden_mse, status, count, params, mse, gstatus=0):
+    assert status == gstatus
+    if gstatus:
+        return
+    assert count == golden_params.shape[0]
+    assert np.array_equal(params[:count], golden_params), \
+        np.max(np.abs(params[:count] - golden_params) / np.abs(golden_params))
+    assert abs(mse - golden_mse) <= MSE_RTOL * abs(golden_mse)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_golden_case_bit_exact(ctx, name):
+    g = np.load(os.path.join(GOLDEN, "expected", f"{name}.npz"))
+    x, y, sb, st, ign = load_case(name)
+    status, counts, out, mse = gpu_batch(ctx, x, y[None, :], [sb], st, ign)
+    check_against(g["params"], float(g["mse"]), status[0], counts[0], out[0], mse[0],
+                  int(g["status"]))
+    sel = ctx.last_peaks(0, "selected")
+    assert np.array_equal(sel.astype(np.int64), g["selected"])
+
+
+def test_blood_batch_all_16(ctx):
+    names = [f"blood_{i:02d}" for i in range(1, 17)]
+    data = [load_case(n) for n in names]
+    xs = np.stack([d[0] for d in data])
+    ys = np.stack([d[1] for d in data])
+    sbs = [d[2] for d in data]
+    status, counts, out, mse = gpu_batch(ctx, xs, ys, sbs, data[0][3])
+    for k, n in enumerate(names):
+        g = np.load(os.path.join(GOLDEN, "expected", f"{n}.npz"))
+        check_against(g["params"], float(g["mse"]), status[k], counts[k], out[k], mse[k])
+        assert np.array_equal(ctx.last_peaks(k, "selected").astype(np.int64), g["selected"])
+
+
+def test_detected_peaks_match_oracle(ctx):
+    x, y, sb, st, ign = load_case("blood_01")
+    gpu_batch(ctx, x, y[None, :], [sb], st)
+    det = ctx.last_peaks(0, "detected").astype(np.int64)
+    sm = oracle.moving_average(y, 3, 3)
+    l, c, r = oracle.detect_peaks(oracle.second_derivative(sm))
+    assert np.array_equal(det, np.stack([l, c, r], axis=1))
+
+
+def test_python_api_end_to_end():
+    import metabodecon as md
+    spectra = md.Spectrum.read_bruker_set(os.path.join(GOLDEN, "bruker", "blood"), 10, 10,
+                                          (-2.2, 11.8))
+    decs = md.Deconvoluter().par_deconvolute_spectra(spectra)
+    for k, d in enumerate(decs):
+        g = np.load(os.path.join(GOLDEN, "expected", f"blood_{k + 1:02d}.npz"))
+        assert np.array_equal(d.params, g["params"])
+        assert abs(d.mse - float(g["mse"])) <= MSE_RTOL * abs(float(g["mse"]))
+    # Deconvolution.par_superposition_vec == oracle superposition, bitwise
+    sup = decs[0].par_superposition_vec(spectra[0].chemical_shifts)
+    ref = oracle.superposition_vec(spectra[0].chemical_shifts, decs[0].params, threads=16)
+    assert np.array_equal(sup, ref)
+    dec = md.Deconvoluter()
+    dec.add_ignore_region((4.7, 4.9))
+    d = dec.deconvolute_spectrum(spectra[0])
+    g = np.load(os.path.join(GOLDEN, "expected", "blood_01_water.npz"))
+    assert np.array_equal(d.params, g["params"])
+
+
+@pytest.mark.parametrize("n,p", [(1, 1), (1000, 0), (4097, 3), (131072, 766), (70001, 2048)])
+def test_superposition_vec_bit_exact(ctx, n, p):
+    rng = np.random.default_rng(n + p)
+    x = np.sort(rng.uniform(-5, 15, n))[::-1].copy()
+    params = np.stack([rng.uniform(1e-3, 1e3, p), rng.uniform(1e-8, 1e-5, p),
+                       rng.uniform(-2, 12, p)], axis=1)
+    import metabodecon as md
+    got = md.superposition_vec(x, params)
+    ref = oracle.superposition_vec(x, params, threads=16)
+    assert np.array_equal(got, ref)
+
+
+def test_reference_unit_superposition(ctx):
+    # lorentzian.rs:741-788 through the GPU path
+    import metabodecon as md
+    L = [md.Lorentzian.from_transformed(1.0, 0.5, -2.0), md.Lorentzian.from_transformed(2.0, 0.75, 0.0),
+         md.Lorentzian.from_transformed(1.0, 0.5, 2.0)]
+    x = np.array([-5.0 + i for i in range(11)])
+    got = md.Lorentzian.par_superposition_vec(x, L)
+    assert np.array_equal(got, oracle.superposition_vec(x, [l.parameters() for l in L]))
+    trip = [md.Lorentzian.from_transformed(0.03, 0.0009, 4.8),
+            md.Lorentzian.from_transformed(0.02, 0.0004, 5.0),
+            md.Lorentzian.from_transformed(0.03, 0.0009, 5.2)]
+    assert abs(md.Lorentzian.superposition_vec(np.array([5.0]), trip)[0] - 51.466992) <= 1e-6
+
+
+def test_error_statuses(ctx):
+    import metabodecon as md
+    from metabodecon import exceptions as ex
+    st = oracle.default_settings()
+    n = 4096
+    x = np.linspace(14.0, -6.0, n)
+    # constant spectrum: no curvature anywhere -> NoPeaksDetected
+    flat = np.full(n, 7.0)
+    status, *_ = gpu_batch(ctx, x, flat[None, :], [(11.8, -2.2)], st)
+    assert status[0] == oracle.deconvolute(x, flat, (11.8, -2.2)).status == 1
+    with pytest.raises(ex.NoPeaksDetected):
+        md.Deconvoluter().deconvolute_spectrum(md.Spectrum(x, flat, (-2.2, 11.8)))
+    # peaks only outside a narrow signal region -> EmptySignalRegion
+    rng = np.random.default_rng(1)
+    noisy = rng.normal(0, 1, n)
+    for sb in [(11.8, 11.79), (1.0, 0.99)]:
+        o = oracle.deconvolute(x, noisy, sb)
+        status, counts, out, mse = gpu_batch(ctx, x, noisy[None, :], [sb], st)
+        assert status[0] == o.status
+        if o.status == 0:
+            assert np.array_equal(out[0, : counts[0]], o.params)
+    # two ignore regions on a decreasing axis: the reference panics in compute_mse
+    sim = load_case("sim_01")
+    ign = ((3.40, 3.42), (3.45, 3.47))
+    o = oracle.deconvolute(sim[0], sim[1], sim[2], st, ignore=ign)
+    status, *_ = gpu_batch(ctx, sim[0], sim[1][None, :], [sim[2]], st, ign)
+    assert status[0] == o.status == 30
+    # detector-only may legitimately select nothing: Ok with zero Lorentzians
+    dso = oracle.make_settings(selector="detector_only")
+    o = oracle.deconvolute(x, noisy, (11.8, 11.79), dso)
+    status, counts, out, mse = gpu_batch(ctx, x, noisy[None, :], [(11.8, 11.79)], dso)
+    assert status[0] == o.status
+    assert counts[0] == o.params.shape[0]
+    if o.status == 0:
+        assert abs(mse[0] - o.mse) <= MSE_RTOL * abs(o.mse)
+
+
+def test_mixed_batch_statuses_are_per_spectrum(ctx):
+    st = oracle.default_settings()
+    x, y, sb, _, _ = load_case("sim_02")
+    flat = np.full_like(y, 3.0)
+    status, counts, out, mse = gpu_batch(ctx, x, np.stack([y, flat, y]), [sb] * 3, st)
+    assert list(status) == [0, 1, 0]
+    g = np.load(os.path.join(GOLDEN, "expected", "sim_02.npz"))
+    for k in (0, 2):
+        check_against(g["params"], float(g["mse"]), status[k], counts[k], out[k], mse[k])
+
+
+def test_small_and_odd_shapes(ctx):
+    st = oracle.default_settings()
+    rng = np.random.default_rng(11)
+    for n in [2, 3, 5, 17, 64, 65, 127, 1000, 1023]:
+        x = np.linspace(12.0, -4.0, n)
+        y = rng.normal(0, 1, n) + 50.0 * np.exp(-((x - 4.0) / 0.3) ** 2)
+        sb = (11.8, -2.2) if n > 2 else (12.0, -4.0)
+        o = oracle.deconvolute(x, y, sb, st)
+        status, counts, out, mse = gpu_batch(ctx, x, y[None, :], [sb], st)
+        assert status[0] == o.status, n
+        if o.status == 0:
+            assert np.array_equal(out[0, : counts[0]], o.params)
+            assert abs(mse[0] - o.mse) <= MSE_RTOL * abs(o.mse)
+
+
+@pytest.mark.parametrize("it,ws", [(1, 2), (2, 4), (5, 7), (3, 31)])
+def test_smoother_settings_sweep(ctx, it, ws):
+    x, y, sb, _, _ = load_case("blood_05")
+    st = oracle.make_settings(smooth_iterations=it, smooth_window=ws)
+    o = oracle.deconvolute(x, y, sb, st)
+    status, counts, out, mse = gpu_batch(ctx, x, y[None, :], [sb], st)
+    assert status[0] == o.status
+    if o.status == 0:
+        assert np.array_equal(out[0, : counts[0]], o.params)
+        assert np.array_equal(ctx.last_peaks(0).astype(np.int64), o.selected)
+
+
+def test_device_synth_matches_host_and_oracle(ctx):
+    torch = pytest.importorskip("torch")
+    b, n = 3, 131072
+    x = torch.empty(n, dtype=torch.float64, device="cuda")
+    y = torch.empty((b, n), dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    rc = nat.lib().mdg_synth_batch_device(ctx.handle, b, n, 14.8, 20.0, 0, 2048, -1.8, 11.4,
+                                          1.0e3, x.data_ptr(), y.data_ptr())
+    assert rc == 0
+    ctx.synchronize()
+    for s in range(b):
+        hx, hy, _ = synth_spectrum(s)
+        assert np.array_equal(x.cpu().numpy(), hx)
+        assert np.array_equal(y[s].cpu().numpy(), hy)
+    # device-resident deconvolution of the same batch vs oracle (configs[1] shape)
+    sb = torch.tensor([[11.8, -2.2]] * b, dtype=torch.float64, device="cuda")
+    cap = 4096
+    out = torch.zeros((b, cap, 3), dtype=torch.float64, device="cuda")
+    cnt = torch.zeros(b, dtype=torch.int32, device="cuda")
+    mse = torch.zeros(b, dtype=torch.float64, device="cuda")
+    status = torch.zeros(b, dtype=torch.int32, device="cuda")
+    s = nat.default_settings()
+    rc = nat.lib().mdg_deconvolute_batch_device(
+        ctx.handle, b, n, x.data_ptr(), 0, y.data_ptr(), n, sb.data_ptr(), ctypes.byref(s), None,
+        0, out.data_ptr(), cap, cnt.data_ptr(), mse.data_ptr(), status.data_ptr())
+    assert rc == 0
+    ctx.synchronize()
+    for k in range(b):
+        g = np.load(os.path.join(GOLDEN, "expected", f"synth_128k_2k_s{k}.npz")) if k < 2 else None
+        hx, hy, _ = synth_spectrum(k)
+        o = oracle.deconvolute(hx, hy, (11.8, -2.2), threads=16) if g is None else None
+        ref_p = g["params"] if g is not None else o.params
+        ref_m = float(g["mse"]) if g is not None else o.mse
+        check_against(ref_p, ref_m, int(status[k]), int(cnt[k]), out[k].cpu().numpy(),
+                      float(mse[k]))
+
+
+def test_deterministic_bits(ctx):
+    x, y, sb, st, _ = load_case("blood_07")
+    a = gpu_batch(ctx, x, y[None, :], [sb], st)
+    b = gpu_batch(ctx, x, y[None, :], [sb], st)
+    assert np.array_equal(a[2], b[2]) and a[3][0] == b[3][0]
+
+
+def test_stage_profiling(ctx):
+    ctx.reset_stage_times()
+    ctx.set_profiling(True)
+    x, y, sb, st, _ = load_case("blood_01")
+    gpu_batch(ctx, x, y[None, :], [sb], st)
+    t = ctx.stage_times()
+    ctx.set_profiling(False)
+    assert t["fit_superposition"][1] == 10 and t["mse_superposition"][0] > 0
