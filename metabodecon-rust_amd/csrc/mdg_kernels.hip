@@ -241,6 +241,147 @@ __device__ void ma_pass(const double* __restrict__ src, double* __restrict__ dst
     }
 }
 
+// ----------------------------------------------------------------------------------
+// K1b  lane-pipelined moving average (the fast path of K1)
+//
+// The recurrence of every pass is inherently sequential, so the parallelism is
+// across (spectrum, pass) pairs: lane = g*P + p runs pass p of spectrum g of the
+// wave. Pass p emits its output o[i] at its tick i+R (R = ws/2); a wave_shr:1 DPP
+// move hands it to lane p+1, which runs D = R+WS ticks behind and consumes it WS
+// steps later from a register ring (slot = step mod WS). The extra WS-1 ticks of
+// lag take the DPP/select/multiply off the recurrence's critical path, which is
+// then just the reference's two dependent adds per tick. No LDS, no barriers,
+// one wave per floor(64/P) spectra; the latency of P passes is ~ one pass.
+//
+// Per tick q of one pass (moving_average.rs:53-83), with the FIFO of pushed
+// values kept in registers at slot (global step mod WS):
+//   q <  R        : push in, sum += in                          (prefill)
+//   R <= q < N    : sum += in; pop if full (q >= WS) else div = 1/(q+1); emit sum*div
+//   N <= q < N+R  : sum -= pop; div = 1/(N+WS-1-q); emit sum*div  (tail)
+// The popped value is always the one pushed WS ticks earlier, in the tail too.
+// ----------------------------------------------------------------------------------
+__device__ __forceinline__ double dpp_shr1(double v) {
+    const long long b = __double_as_longlong(v);
+    int lo = (int)(unsigned)(b & 0xffffffffll), hi = (int)(b >> 32);
+    lo = __builtin_amdgcn_mov_dpp(lo, 0x138, 0xf, 0xf, true);  // wave_shr:1, lane 0 <- 0
+    hi = __builtin_amdgcn_mov_dpp(hi, 0x138, 0xf, 0xf, true);
+    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
+template <int WS>
+struct MAState {
+    double sum, div;
+    double fifo[WS];
+};
+
+template <int WS>
+__device__ __forceinline__ double ma_tick_generic(MAState<WS>& st, const int slot, int q, int N,
+                                                  double in) {
+    constexpr int R = WS / 2;
+    double emit = 0.0;
+    if (q >= 0 && q < N + R) {
+        if (q < R) {
+            st.sum += in;
+            st.fifo[slot] = in;
+        } else if (q < N) {
+            st.sum += in;
+            if (q >= WS) st.sum -= st.fifo[slot];
+            else st.div = 1.0 / (double)(q + 1);
+            st.fifo[slot] = in;
+            emit = st.sum * st.div;
+        } else {
+            st.sum -= st.fifo[slot];
+            st.div = 1.0 / (double)(N + WS - 1 - q);
+            emit = st.sum * st.div;
+        }
+    }
+    return emit;
+}
+
+template <int WS>
+__device__ __forceinline__ double ma_tick_steady(MAState<WS>& st, const int slot, double in) {
+    st.sum += in;
+    st.sum -= st.fifo[slot];
+    st.fifo[slot] = in;
+    return st.sum * st.div;
+}
+
+template <int WS>
+__global__ __launch_bounds__(64) void k_smooth_pipe(BatchArgs a, Workspace w, int P, int spw) {
+    constexpr int R = WS / 2, D = R + WS;
+    constexpr int U = WS * ((32 + WS - 1) / WS);  // steps per prefetch block (multiple of WS)
+    const int lane = threadIdx.x;
+    const int g = lane / P, p = lane - g * P;
+    const int s = blockIdx.x * spw + g;
+    const bool valid = g < spw && s < a.B;
+    const bool ok = valid && w.status[valid ? s : 0] == 0;
+    const int N = a.N;
+    const double* yrow = a.y + (size_t)(valid ? s : 0) * a.y_stride;
+    double* orow = w.smooth + (size_t)(valid ? s : 0) * N;
+    const bool feeder = p == 0;
+    const bool writer = ok && p == P - 1;
+    const int off = p * D;  // tick = step - off
+    MAState<WS> st;
+    st.sum = 0.0;  // T::zero()
+    st.div = 1.0;  // T::one()
+#pragma unroll
+    for (int k = 0; k < WS; ++k) st.fifo[k] = 0.0;
+    double rq[WS];  // received emits of the previous pass, consumed WS steps later
+#pragma unroll
+    for (int k = 0; k < WS; ++k) rq[k] = 0.0;
+    const int T = (P - 1) * D + N + R;
+    int tA = ((P - 1) * D + WS + WS - 1) / WS * WS;
+    const int nblk = N > tA ? (N - tA) / U : 0;
+    int tB = tA + nblk * U;
+    if (nblk == 0) tA = tB = 0;
+
+    auto generic = [&](int t0, int t1) {
+        for (int tt = t0; tt < t1; tt += WS) {
+#pragma unroll
+            for (int k = 0; k < WS; ++k) {
+                const int q = tt + k - off;
+                double in = rq[k];
+                if (feeder) in = (q >= 0 && q < N) ? yrow[q] : 0.0;
+                const double e = ma_tick_generic<WS>(st, k, q, N, in);
+                if (writer && q >= R && q < N + R) orow[q - R] = e;
+                rq[k] = dpp_shr1(e);
+            }
+        }
+    };
+    generic(0, tA);
+    if (tB > tA) {
+        double buf[U], nbuf[U], ob[U];
+        if (feeder) {
+#pragma unroll
+            for (int k = 0; k < U; ++k) buf[k] = yrow[tA + k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < U; ++k) buf[k] = 0.0;
+        }
+        for (int t0 = tA; t0 < tB; t0 += U) {
+            if (feeder && t0 + U < tB) {
+#pragma unroll
+                for (int k = 0; k < U; ++k) nbuf[k] = yrow[t0 + U + k];
+            }
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const double in = feeder ? buf[k] : rq[k % WS];
+                const double e = ma_tick_steady<WS>(st, k % WS, in);
+                ob[k] = e;
+                rq[k % WS] = dpp_shr1(e);
+            }
+            if (writer) {  // one exec-masked burst of U stores per block
+                double* o = orow + (t0 - off - R);
+#pragma unroll
+                for (int k = 0; k < U; ++k) o[k] = ob[k];
+            }
+#pragma unroll
+            for (int k = 0; k < U; ++k) buf[k] = nbuf[k];
+        }
+    }
+    generic(tB, T);
+}
+
 __global__ void k_smooth(BatchArgs a, Workspace w, int iters, int ws) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= a.B) return;
@@ -370,6 +511,49 @@ __device__ __forceinline__ double score_min_sum(const double* __restrict__ sm, i
     return fmin(left, right);
 }
 
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(unsigned)(b & 0xffffffffll), l);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
+// Left fold over the signal-free-region scores peaks[..left] ++ peaks[right..P]
+// in the reference's order (noise_score_filter.rs:129-138), by ONE wave: lanes
+// load 64 consecutive terms (coalesced, one block ahead), then the running sum
+// consumes them lane by lane through readlane -> SGPR operands. The only serial
+// part is the chain of dependent adds the reference itself performs.
+template <bool SQUARE>
+__device__ double sfr_fold(const double* __restrict__ scores, int left, int right, int P,
+                           double mean) {
+    const int lane = threadIdx.x & 63;
+    const int n = left + (P - right);
+    auto term = [&](int k) -> double {
+        if (k >= n) return 0.0;
+        const int idx = k < left ? k : right + (k - left);
+        const double v = scores[idx];
+        if (SQUARE) {
+            const double d = v - mean;
+            return d * d;
+        }
+        return v;
+    };
+    double acc = -0.0;
+    double cur = term(lane);
+    for (int base = 0; base < n; base += 64) {
+        const double nxt = term(base + 64 + lane);  // prefetch the next block
+        const int cnt = min(64, n - base);
+        if (cnt == 64) {
+#pragma unroll
+            for (int l = 0; l < 64; ++l) acc += readlane_f64(cur, l);
+        } else {
+            for (int l = 0; l < cnt; ++l) acc += readlane_f64(cur, l);
+        }
+        cur = nxt;
+    }
+    return acc;
+}
+
 template <int BS>
 __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double threshold) {
     const int s = blockIdx.x;
@@ -411,27 +595,17 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
         return;
     }
     __syncthreads();  // scores visible to the whole block
-    if (threadIdx.x == 0) {
+    if (threadIdx.x < 64) {
         // mean_sd_scores: sequential left folds over SFR = peaks[..left] ++ peaks[right..]
         const int n = left + (P - right);
-        double sum = -0.0;
-        for (int p = 0; p < left; ++p) sum += scores[p];
-        for (int p = right; p < P; ++p) sum += scores[p];
-        const double mean = sum / (double)n;
-        double var = -0.0;
-        for (int p = 0; p < left; ++p) {
-            const double d = scores[p] - mean;
-            var += d * d;
-        }
-        for (int p = right; p < P; ++p) {
-            const double d = scores[p] - mean;
-            var += d * d;
-        }
-        var = var / (double)n;
+        const double mean = sfr_fold<false>(scores, left, right, P, 0.0) / (double)n;
+        const double var = sfr_fold<true>(scores, left, right, P, mean) / (double)n;
         const double sd = __builtin_sqrt(var);
-        thr_sh = mean + threshold * sd;
-        w.sfr_stats[2 * s] = mean;
-        w.sfr_stats[2 * s + 1] = sd;
+        if (threadIdx.x == 0) {
+            thr_sh = mean + threshold * sd;
+            w.sfr_stats[2 * s] = mean;
+            w.sfr_stats[2 * s + 1] = sd;
+        }
     }
     __syncthreads();
     const double thr = thr_sh;
@@ -541,6 +715,70 @@ __global__ void k_fit_sup(BatchArgs a, Workspace w) {
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < 3 * P; i += gridDim.x * blockDim.x) {
         const double sup = superpose(w.rx[3 * base + i], params, P);
         w.ratio[3 * base + i] = w.ry[3 * base + i] / sup;
+    }
+}
+
+// K6b  fit superposition for small batches (B*3P too small to fill 256 CUs with
+// one thread per point). A 128-thread workgroup owns FQ=16 reduced points; the
+// evaluations of a chunk of FJ=64 peaks are spread over (point, peak) lane pairs
+// and parked in LDS, then one wave folds them into each point's running sum in
+// peak order -- the reference's exact summation order (lorentzian.rs:606-611),
+// so the result is bit-identical to K6 while ~30x more lanes do the divisions.
+// Triple-buffered chunks: evals of chunk c overlap the fold of chunk c-1, and a
+// buffer is rewritten only two barriers after its fold.
+constexpr int kFQ = 16;
+constexpr int kFJ = 64;
+__global__ __launch_bounds__(128) void k_fit_sup_split(BatchArgs a, Workspace w) {
+    const int s = blockIdx.y;
+    __shared__ double ev[3][kFJ][kFQ];
+    __shared__ double accs[kFQ];
+    if (w.status[s]) return;
+    const int P = w.sel_count[s];
+    const size_t base = (size_t)s * w.capD;
+    const double* __restrict__ params = w.params + 3 * base;
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    const int pt = lane & (kFQ - 1);
+    const int jsub = (lane >> 4) + 4 * wv;  // 0..7
+    const int npts = 3 * P;
+    const int nch = (P + kFJ - 1) / kFJ;
+    for (int g0 = blockIdx.x * kFQ; g0 < npts; g0 += gridDim.x * kFQ) {
+        const int i = g0 + pt;
+        const double xi = i < npts ? w.rx[3 * base + i] : 0.0;
+        for (int c = 0; c <= nch; ++c) {
+            if (c < nch) {
+                double (*e)[kFQ] = ev[c % 3];
+#pragma unroll
+                for (int r = 0; r < kFJ / 8; ++r) {
+                    const int jl = jsub + 8 * r;
+                    const int j = c * kFJ + jl;
+                    double v = 0.0;
+                    if (j < P) v = lorentz(xi, params[3 * j], params[3 * j + 1], params[3 * j + 2]);
+                    e[jl][pt] = v;
+                }
+            }
+            __syncthreads();
+            if (c > 0) {
+                const int cc = c - 1;
+                if (wv == (cc & 1) && lane < kFQ) {
+                    const double (*e)[kFQ] = ev[cc % 3];
+                    const int jn = min(kFJ, P - cc * kFJ);
+                    double acc = cc == 0 ? -0.0 : accs[lane];
+                    if (jn == kFJ) {
+#pragma unroll 16
+                        for (int jl = 0; jl < kFJ; ++jl) acc += e[jl][lane];
+                    } else {
+                        for (int jl = 0; jl < jn; ++jl) acc += e[jl][lane];
+                    }
+                    accs[lane] = acc;
+                }
+            }
+        }
+        __syncthreads();
+        if (tid < kFQ && g0 + tid < npts) {
+            const double sup = nch > 0 ? accs[tid] : -0.0;
+            w.ratio[3 * base + g0 + tid] = w.ry[3 * base + g0 + tid] / sup;
+        }
+        __syncthreads();
     }
 }
 
@@ -722,7 +960,29 @@ static inline unsigned cdiv(int64_t a, int64_t b) { return (unsigned)((a + b - 1
 void launch_prep(const BatchArgs& a, const Workspace& w, hipStream_t st) {
     hipLaunchKernelGGL(k_prep, dim3(cdiv(a.B, 64)), dim3(64), 0, st, a, w);
 }
+template <int WS>
+static void launch_pipe(const BatchArgs& a, const Workspace& w, int iters, hipStream_t st) {
+    const int spw = 64 / iters;
+    hipLaunchKernelGGL(k_smooth_pipe<WS>, dim3(cdiv(a.B, spw)), dim3(64), 0, st, a, w, iters, spw);
+}
+
 void launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int ws, hipStream_t st) {
+    // lane-pipelined kernel whenever the window fits the register FIFO and the
+    // spectrum is longer than the window; the one-lane-per-spectrum kernel otherwise
+    if (iters >= 1 && iters <= 32 && a.N > ws + 1) {
+        switch (ws) {
+            case 2: return launch_pipe<2>(a, w, iters, st);
+            case 3: return launch_pipe<3>(a, w, iters, st);
+            case 4: return launch_pipe<4>(a, w, iters, st);
+            case 5: return launch_pipe<5>(a, w, iters, st);
+            case 6: return launch_pipe<6>(a, w, iters, st);
+            case 7: return launch_pipe<7>(a, w, iters, st);
+            case 8: return launch_pipe<8>(a, w, iters, st);
+            case 9: return launch_pipe<9>(a, w, iters, st);
+            case 11: return launch_pipe<11>(a, w, iters, st);
+            default: break;
+        }
+    }
     hipLaunchKernelGGL(k_smooth, dim3(cdiv(a.B, 64)), dim3(64), 0, st, a, w, iters, ws);
 }
 void launch_flags(const BatchArgs& a, const Workspace& w, hipStream_t st) {
@@ -742,7 +1002,14 @@ void launch_fit_init(const BatchArgs& a, const Workspace& w, int gx, hipStream_t
     hipLaunchKernelGGL(k_fit_init, dim3(gx, a.B), dim3(256), 0, st, a, w);
 }
 void launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, hipStream_t st) {
-    hipLaunchKernelGGL(k_fit_sup, dim3(gx, a.B), dim3(256), 0, st, a, w);
+    if (a.B <= 16) {
+        // ~16 points per workgroup: enough workgroups to cover 3P points of every
+        // spectrum in one sweep for P up to ~4k and to occupy all 256 CUs
+        const int g = std::max(64, std::min(2048, 8192 / a.B));
+        hipLaunchKernelGGL(k_fit_sup_split, dim3(g, a.B), dim3(128), 0, st, a, w);
+    } else {
+        hipLaunchKernelGGL(k_fit_sup, dim3(gx, a.B), dim3(256), 0, st, a, w);
+    }
 }
 void launch_fit_update(const BatchArgs& a, const Workspace& w, int gx, hipStream_t st) {
     hipLaunchKernelGGL(k_fit_update, dim3(gx, a.B), dim3(256), 0, st, a, w);

@@ -85,6 +85,19 @@ _lib = None
 _lib_lock = threading.Lock()
 
 
+def _share_torch_hip_runtime():
+    """torch (ROCm wheel) bundles its own libamdhip64.so.7 with the same SONAME as
+    /opt/rocm's. Whichever is loaded first serves every later NEEDED entry, so
+    load torch's first: then libmdgpu and torch share ONE HIP runtime and device
+    pointers/streams from torch are valid here (and torch keeps working)."""
+    if os.environ.get("MDGPU_NO_TORCH"):
+        return
+    try:
+        import torch  # noqa: F401  (loads libamdhip64 without initialising a device)
+    except Exception:
+        pass
+
+
 def lib() -> ctypes.CDLL:
     global _lib
     if _lib is None:
@@ -94,6 +107,7 @@ def lib() -> ctypes.CDLL:
                     raise NativeLibraryError(
                         f"libmdgpu.so not found at {LIB_PATH}; build it with "
                         "`make -C metabodecon-rust_amd` (hipcc, gfx950)")
+                _share_torch_hip_runtime()
                 L = ctypes.CDLL(LIB_PATH)
                 _declare(L)
                 _lib = L
