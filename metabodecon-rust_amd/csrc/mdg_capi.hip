@@ -51,7 +51,7 @@ struct mdg_ctx {
     int last_B = 0, last_N = 0;  // shape of the last pipeline run
     Workspace w{};
     // staging for the host-pointer API
-    Buffer st_x, st_y, st_sb, st_out, st_cnt, st_mse, st_status, st_L, st_sup;
+    Buffer st_x, st_y, st_sb, st_out, st_cnt, st_mse, st_status, st_L, st_sup, st_flag;
     // profiling
     bool profiling = false;
     std::vector<Pending> pending;
@@ -156,6 +156,8 @@ int ensure_workspace(mdg_ctx* c, int B, int N) {
         const size_t o_ig = take(Bs * 2 * kMaxIgnore * 8);
         const size_t o_nig = take(Bs * 4), o_panic = take(Bs * 4), o_status = take(Bs * 4);
         const size_t o_dcnt = take(Bs * 4), o_scnt = take(Bs * 4), o_kcnt = take(Bs * 4);
+        const size_t o_xok = take(Bs * 4), o_unsafe = take(Bs * 8), o_uk = take(Bs * 4);
+
         if (c->arena.p) (void)hipFree(c->arena.p);
         c->arena.p = nullptr;
         c->arena.bytes = 0;
@@ -190,6 +192,10 @@ int ensure_workspace(mdg_ctx* c, int B, int N) {
         w.det_count = (int32_t*)(base + o_dcnt);
         w.sel_count = (int32_t*)(base + o_scnt);
         w.kept_count = (int32_t*)(base + o_kcnt);
+        w.x_ok = (int32_t*)(base + o_xok);
+        w.unsafe = (int32_t*)(base + o_unsafe);
+        w.unsafe_kept = (int32_t*)(base + o_uk);
+
         c->ws_B = nB;
         c->ws_N = nN;
     }
@@ -260,11 +266,11 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     for (uint32_t it = 0; it < s->fit_iterations; ++it) {
         {
             StageTimer t(c, ST_FIT_SUP);
-            launch_fit_sup(a, w, gfit, st);
+            launch_fit_sup(a, w, gfit, (int)it, st);
         }
         {
             StageTimer t(c, ST_FIT_UPDATE);
-            launch_fit_update(a, w, gupd, st);
+            launch_fit_update(a, w, gupd, (int)it, st);
         }
     }
     {
@@ -472,7 +478,7 @@ int mdg_ctx_destroy(mdg_ctx* c) {
         }
         for (auto e : c->free_events) (void)hipEventDestroy(e);
         for (Buffer* b : {&c->arena, &c->st_x, &c->st_y, &c->st_sb, &c->st_out, &c->st_cnt,
-                          &c->st_mse, &c->st_status, &c->st_L, &c->st_sup})
+                          &c->st_mse, &c->st_status, &c->st_L, &c->st_sup, &c->st_flag})
             if (b->p) (void)hipFree(b->p);
         if (c->own) (void)hipStreamDestroy(c->own);
     }
@@ -645,9 +651,12 @@ int mdg_superposition_vec_device(mdg_ctx* c, const double* d_x, size_t n, const 
     if (n == 0) return MDG_OK;
     std::lock_guard<std::mutex> g(c->mu);
     HIPCHK(hipSetDevice(c->device));
+    int rc = ensure(c->st_flag, 256);
+    if (rc) return rc;
     {
         StageTimer t(c, ST_SUPVEC);
-        launch_superposition_vec(d_x, (int64_t)n, (const double*)d_L, (int)p, d_out, c->stream);
+        launch_superposition_vec(d_x, (int64_t)n, (const double*)d_L, (int)p, d_out,
+                                 (int*)c->st_flag.p, c->stream);
     }
     HIPCHK(hipGetLastError());
     return MDG_OK;
@@ -665,12 +674,13 @@ int mdg_superposition_vec(mdg_ctx* c, const double* x, size_t n, const mdg_loren
     if ((rc = ensure(c->st_x, n * 8))) return rc;
     if ((rc = ensure(c->st_L, std::max<size_t>(p, 1) * 24))) return rc;
     if ((rc = ensure(c->st_sup, n * 8))) return rc;
+    if ((rc = ensure(c->st_flag, 256))) return rc;
     HIPCHK(hipMemcpyAsync(c->st_x.p, x, n * 8, hipMemcpyHostToDevice, st));
     if (p) HIPCHK(hipMemcpyAsync(c->st_L.p, L, p * 24, hipMemcpyHostToDevice, st));
     {
         StageTimer t(c, ST_SUPVEC);
         launch_superposition_vec((const double*)c->st_x.p, (int64_t)n, (const double*)c->st_L.p,
-                                 (int)p, (double*)c->st_sup.p, st);
+                                 (int)p, (double*)c->st_sup.p, (int*)c->st_flag.p, st);
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(out, c->st_sup.p, n * 8, hipMemcpyDeviceToHost, st));

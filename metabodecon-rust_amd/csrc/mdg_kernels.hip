@@ -25,12 +25,48 @@ __device__ __forceinline__ double lorentz(double x, double sfhw, double hw2, dou
     return sfhw / (hw2 + d * d);
 }
 
+// Correctly rounded binary64 quotient without the div_scale/div_fmas/div_fixup
+// wrappers. hipcc expands `n / d` to: div_scale x2, rcp, two Newton steps
+// (fma, fma), q0 = n*r, rem = fma(-d, q0, n), div_fmas(rem, r, q0), div_fixup.
+// When div_scale does not scale (|n|, |d| in [2^-200, 2^203], quotient normal)
+// div_fmas is a plain fma and div_fixup returns its input, so this sequence
+// yields the SAME bits. Callers use it only for spectra whose flags prove the
+// operand ranges (peak_fast_ok + x_ok below); everything else takes `/`.
+__device__ __forceinline__ double div_rn_fast(double n, double d) {
+    const double r0 = __builtin_amdgcn_rcp(d);
+    const double e0 = __builtin_fma(-d, r0, 1.0);
+    const double r1 = __builtin_fma(r0, e0, r0);
+    const double e1 = __builtin_fma(-d, r1, 1.0);
+    const double r2 = __builtin_fma(r1, e1, r1);
+    const double q0 = n * r2;
+    const double rem = __builtin_fma(-d, q0, n);
+    return __builtin_fma(rem, r2, q0);
+}
+
+// Ranges under which sfhw / (hw2 + (x - maxp)^2) may use div_rn_fast: with
+// |x|, |maxp| <= 2^100 the denominator lies in [2^-200, 2^203) and the quotient
+// in (2^-404, 2^400] -- no scaling, no denormals, no overflow.
+__device__ __forceinline__ bool peak_fast_ok(double sfhw, double hw2, double maxp) {
+    const double as = fabs(sfhw);
+    return as >= 0x1p-200 && as <= 0x1p200 && hw2 >= 0x1p-200 && hw2 <= 0x1p200 &&
+           fabs(maxp) <= 0x1p100;
+}
+__device__ __forceinline__ bool x_fast_ok(double x) { return fabs(x) <= 0x1p100; }
+
+template <bool FAST>
+__device__ __forceinline__ double lorentz_t(double x, double sfhw, double hw2, double maxp) {
+    const double d = x - maxp;
+    const double den = hw2 + d * d;
+    return FAST ? div_rn_fast(sfhw, den) : sfhw / den;
+}
+
 // In-order superposition (lorentzian.rs:606-611) of P wave-uniform Lorentzians.
 // params is AoS {sfhw, hw2, maxp}; the address is uniform so the compiler emits
 // s_load_dwordx* and uses SGPR operands.
 typedef const __attribute__((address_space(4))) double* const_f64_ptr;
 
-__device__ __forceinline__ double superpose(double x, const double* __restrict__ params_g, int P) {
+template <bool FAST>
+__device__ __forceinline__ double superpose_t(double x, const double* __restrict__ params_g, int P) {
     // Parameters are read-only for the whole launch: address space 4 (constant)
     // lets the backend issue s_load_dwordx* and feed SGPR operands to the VALU.
     const const_f64_ptr params = (const_f64_ptr)(params_g);
@@ -38,10 +74,10 @@ __device__ __forceinline__ double superpose(double x, const double* __restrict__
     int j = 0;
     for (; j + 4 <= P; j += 4) {
         const_f64_ptr L = params + 3 * j;
-        const double e0 = lorentz(x, L[0], L[1], L[2]);
-        const double e1 = lorentz(x, L[3], L[4], L[5]);
-        const double e2 = lorentz(x, L[6], L[7], L[8]);
-        const double e3 = lorentz(x, L[9], L[10], L[11]);
+        const double e0 = lorentz_t<FAST>(x, L[0], L[1], L[2]);
+        const double e1 = lorentz_t<FAST>(x, L[3], L[4], L[5]);
+        const double e2 = lorentz_t<FAST>(x, L[6], L[7], L[8]);
+        const double e3 = lorentz_t<FAST>(x, L[9], L[10], L[11]);
         acc += e0;
         acc += e1;
         acc += e2;
@@ -49,9 +85,14 @@ __device__ __forceinline__ double superpose(double x, const double* __restrict__
     }
     for (; j < P; ++j) {
         const_f64_ptr L = params + 3 * j;
-        acc += lorentz(x, L[0], L[1], L[2]);
+        acc += lorentz_t<FAST>(x, L[0], L[1], L[2]);
     }
     return acc;
+}
+
+__device__ __forceinline__ double superpose(double x, const double* __restrict__ params, int P,
+                                            bool fast) {
+    return fast ? superpose_t<true>(x, params, P) : superpose_t<false>(x, params, P);
 }
 
 // D[k] := sd[k-1] = (s[k-1] - 2*s[k]) + s[k+1]   (common.rs:5-10, intensity aligned)
@@ -180,6 +221,11 @@ __global__ void k_prep(BatchArgs a, Workspace w) {
         if (lo > hi || hi > (int64_t)a.N) panic = 1;
     }
     w.mse_panic[s] = panic;
+    // the axis is monotone (Spectrum invariant): its end points bound every x
+    w.x_ok[s] = x_fast_ok(x0) && x_fast_ok(x[a.N - 1]);
+    w.unsafe[2 * s] = 0;
+    w.unsafe[2 * s + 1] = 0;
+    w.unsafe_kept[s] = 0;
     w.status[s] = (a.N < 2) ? MDG_INVALID_ARGUMENT : 0;
     w.det_count[s] = 0;
     w.sel_count[s] = 0;
@@ -701,71 +747,106 @@ __global__ void k_fit_init(BatchArgs a, Workspace w) {
         mirror_shoulder(q);
         double* st = w.stencil + 6 * base + 6 * (size_t)p;
         st[0] = q.x1; st[1] = q.x2; st[2] = q.x3; st[3] = q.y1; st[4] = q.y2; st[5] = q.y3;
-        solve(q, w.params + 3 * base + 3 * (size_t)p);
+        double* L = w.params + 3 * base + 3 * (size_t)p;
+        solve(q, L);
+        if (!peak_fast_ok(L[0], L[1], L[2])) atomicAdd(&w.unsafe[2 * s], 1);
     }
 }
 
 // K6  fit superposition at the 3P reduced points + ratio (fitter_analytical.rs:40-47)
-__global__ void k_fit_sup(BatchArgs a, Workspace w) {
+// Ping-pong range flags: iteration `it` reads unsafe[it&1] (written by the
+// producer of its parameters) and clears unsafe[(it+1)&1] for k_fit_update(it).
+__device__ __forceinline__ bool fit_fast(const Workspace& w, int s, int it) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) w.unsafe[2 * s + ((it + 1) & 1)] = 0;
+    return w.x_ok[s] && w.unsafe[2 * s + (it & 1)] == 0;
+}
+
+__global__ void k_fit_sup(BatchArgs a, Workspace w, int it) {
     const int s = blockIdx.y;
     if (w.status[s]) return;
     const int P = w.sel_count[s];
     const size_t base = (size_t)s * w.capD;
     const double* __restrict__ params = w.params + 3 * base;
+    const bool fast = fit_fast(w, s, it);
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < 3 * P; i += gridDim.x * blockDim.x) {
-        const double sup = superpose(w.rx[3 * base + i], params, P);
+        const double sup = superpose(w.rx[3 * base + i], params, P, fast);
         w.ratio[3 * base + i] = w.ry[3 * base + i] / sup;
     }
 }
 
 // K6b  fit superposition for small batches (B*3P too small to fill 256 CUs with
-// one thread per point). A 128-thread workgroup owns FQ=16 reduced points; the
-// evaluations of a chunk of FJ=64 peaks are spread over (point, peak) lane pairs
-// and parked in LDS, then one wave folds them into each point's running sum in
-// peak order -- the reference's exact summation order (lorentzian.rs:606-611),
-// so the result is bit-identical to K6 while ~30x more lanes do the divisions.
-// Triple-buffered chunks: evals of chunk c overlap the fold of chunk c-1, and a
-// buffer is rewritten only two barriers after its fold.
-constexpr int kFQ = 16;
-constexpr int kFJ = 64;
-__global__ __launch_bounds__(128) void k_fit_sup_split(BatchArgs a, Workspace w) {
+// one thread per point). A 1024-thread workgroup owns Q reduced points; the
+// evaluations of a chunk of J peaks are spread over (point, peak) lane pairs and
+// parked in LDS, then one wave folds them into each point's running sum in peak
+// order -- the reference's exact summation order (lorentzian.rs:606-611), so the
+// result is bit-identical to K6 while every CU does divisions. Chunks are
+// triple-buffered: the evals of chunk c overlap the fold of chunk c-1, a buffer is
+// rewritten only two barriers after its fold, and the folding wave rotates.
+// The next chunk's parameters are prefetched into registers across the barrier.
+template <int Q, int J, int BS>
+__global__ __launch_bounds__(BS) void k_fit_sup_split(BatchArgs a, Workspace w, int it) {
+    constexpr int SUBS = BS / Q;      // peak lanes per point
+    constexpr int EPT = J / SUBS;     // evals per thread per chunk
+    constexpr int NW = BS / 64;
+    static_assert(Q <= 64 && J % SUBS == 0, "shape");
     const int s = blockIdx.y;
-    __shared__ double ev[3][kFJ][kFQ];
-    __shared__ double accs[kFQ];
+    __shared__ double ev[3][J][Q];
+    __shared__ double accs[Q];
     if (w.status[s]) return;
     const int P = w.sel_count[s];
     const size_t base = (size_t)s * w.capD;
     const double* __restrict__ params = w.params + 3 * base;
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-    const int pt = lane & (kFQ - 1);
-    const int jsub = (lane >> 4) + 4 * wv;  // 0..7
+    const int pt = tid % Q;
+    const int sub = tid / Q;
     const int npts = 3 * P;
-    const int nch = (P + kFJ - 1) / kFJ;
-    for (int g0 = blockIdx.x * kFQ; g0 < npts; g0 += gridDim.x * kFQ) {
+    const int nch = (P + J - 1) / J;
+    const bool fast = fit_fast(w, s, it);
+    for (int g0 = blockIdx.x * Q; g0 < npts; g0 += gridDim.x * Q) {
         const int i = g0 + pt;
         const double xi = i < npts ? w.rx[3 * base + i] : 0.0;
+        double pf[EPT][3];
+#pragma unroll
+        for (int r = 0; r < EPT; ++r) {
+            const int j = sub + SUBS * r;
+            const bool ok = j < P;
+            pf[r][0] = ok ? params[3 * j] : 0.0;
+            pf[r][1] = ok ? params[3 * j + 1] : 1.0;
+            pf[r][2] = ok ? params[3 * j + 2] : 0.0;
+        }
         for (int c = 0; c <= nch; ++c) {
             if (c < nch) {
-                double (*e)[kFQ] = ev[c % 3];
+                double (*e)[Q] = ev[c % 3];
+                double v[EPT];
+                if (fast) {
 #pragma unroll
-                for (int r = 0; r < kFJ / 8; ++r) {
-                    const int jl = jsub + 8 * r;
-                    const int j = c * kFJ + jl;
-                    double v = 0.0;
-                    if (j < P) v = lorentz(xi, params[3 * j], params[3 * j + 1], params[3 * j + 2]);
-                    e[jl][pt] = v;
+                    for (int r = 0; r < EPT; ++r) v[r] = lorentz_t<true>(xi, pf[r][0], pf[r][1], pf[r][2]);
+                } else {
+#pragma unroll
+                    for (int r = 0; r < EPT; ++r) v[r] = lorentz_t<false>(xi, pf[r][0], pf[r][1], pf[r][2]);
+                }
+#pragma unroll
+                for (int r = 0; r < EPT; ++r) e[sub + SUBS * r][pt] = v[r];
+                // prefetch chunk c+1 (out-of-range peaks evaluate to 0 and are never folded)
+#pragma unroll
+                for (int r = 0; r < EPT; ++r) {
+                    const int j = (c + 1) * J + sub + SUBS * r;
+                    const bool ok = j < P;
+                    pf[r][0] = ok ? params[3 * j] : 0.0;
+                    pf[r][1] = ok ? params[3 * j + 1] : 1.0;
+                    pf[r][2] = ok ? params[3 * j + 2] : 0.0;
                 }
             }
             __syncthreads();
             if (c > 0) {
                 const int cc = c - 1;
-                if (wv == (cc & 1) && lane < kFQ) {
-                    const double (*e)[kFQ] = ev[cc % 3];
-                    const int jn = min(kFJ, P - cc * kFJ);
+                if (wv == cc % NW && lane < Q) {
+                    const double (*e)[Q] = ev[cc % 3];
+                    const int jn = min(J, P - cc * J);
                     double acc = cc == 0 ? -0.0 : accs[lane];
-                    if (jn == kFJ) {
+                    if (jn == J) {
 #pragma unroll 16
-                        for (int jl = 0; jl < kFJ; ++jl) acc += e[jl][lane];
+                        for (int jl = 0; jl < J; ++jl) acc += e[jl][lane];
                     } else {
                         for (int jl = 0; jl < jn; ++jl) acc += e[jl][lane];
                     }
@@ -774,7 +855,7 @@ __global__ __launch_bounds__(128) void k_fit_sup_split(BatchArgs a, Workspace w)
             }
         }
         __syncthreads();
-        if (tid < kFQ && g0 + tid < npts) {
+        if (tid < Q && g0 + tid < npts) {
             const double sup = nch > 0 ? accs[tid] : -0.0;
             w.ratio[3 * base + g0 + tid] = w.ry[3 * base + g0 + tid] / sup;
         }
@@ -783,7 +864,7 @@ __global__ __launch_bounds__(128) void k_fit_sup_split(BatchArgs a, Workspace w)
 }
 
 // K7  stencil update + re-solve (fitter_analytical.rs:48-65)
-__global__ void k_fit_update(BatchArgs a, Workspace w) {
+__global__ void k_fit_update(BatchArgs a, Workspace w, int it) {
     const int s = blockIdx.y;
     if (w.status[s]) return;
     const int P = w.sel_count[s];
@@ -797,7 +878,9 @@ __global__ void k_fit_update(BatchArgs a, Workspace w) {
         q.y3 = q.y3 * ra[2];
         mirror_shoulder(q);
         st[0] = q.x1; st[1] = q.x2; st[2] = q.x3; st[3] = q.y1; st[4] = q.y2; st[5] = q.y3;
-        solve(q, w.params + 3 * base + 3 * (size_t)p);
+        double* L = w.params + 3 * base + 3 * (size_t)p;
+        solve(q, L);
+        if (!peak_fast_ok(L[0], L[1], L[2])) atomicAdd(&w.unsafe[2 * s + ((it + 1) & 1)], 1);
     }
 }
 
@@ -832,6 +915,8 @@ __global__ __launch_bounds__(BS) void k_retain(BatchArgs a, Workspace w) {
             kept[3 * o] = params[3 * p];
             kept[3 * o + 1] = params[3 * p + 1];
             kept[3 * o + 2] = params[3 * p + 2];
+            if (!peak_fast_ok(params[3 * p], params[3 * p + 1], params[3 * p + 2]))
+                atomicAdd(&w.unsafe_kept[s], 1);
             if (o < a.cap) {
                 out[3 * o] = params[3 * p];
                 out[3 * o + 1] = params[3 * p + 1];
@@ -874,6 +959,7 @@ __global__ __launch_bounds__(BS) void k_mse_partial(BatchArgs a, Workspace w) {
         mse_region(w, s, r, nig, &lo, &hi);
         total += hi - lo;
     }
+    const bool fast = w.x_ok[s] && w.unsafe_kept[s] == 0;
     double acc = 0.0;
     for (int64_t v = (int64_t)blockIdx.x * BS + threadIdx.x; v < total;
          v += (int64_t)gridDim.x * BS) {
@@ -887,7 +973,7 @@ __global__ __launch_bounds__(BS) void k_mse_partial(BatchArgs a, Workspace w) {
             }
             rem -= hi - lo;
         }
-        const double sup = superpose(x[idx], kept, P);
+        const double sup = superpose(x[idx], kept, P, fast);
         const double d = sup - y[idx];
         acc += d * d;
     }
@@ -927,12 +1013,26 @@ __global__ void k_mse_final(BatchArgs a, Workspace w, int nparts) {
 // ----------------------------------------------------------------------------------
 // standalone Lorentzian::superposition_vec (lorentzian.rs:631-663)
 // ----------------------------------------------------------------------------------
+// range pre-pass: flag[0] = number of Lorentzians / x values outside the fast ranges
+__global__ void k_range_check(const double* __restrict__ x, int64_t n,
+                              const double* __restrict__ params, int P, int* flag) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < P;
+         i += (int64_t)gridDim.x * blockDim.x)
+        if (!peak_fast_ok(params[3 * i], params[3 * i + 1], params[3 * i + 2])) atomicAdd(flag, 1);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && n > 0)
+        if (!x_fast_ok(x[0]) || !x_fast_ok(x[n - 1])) atomicAdd(flag, 1);
+}
+
 __global__ void k_superposition_vec(const double* __restrict__ x, int64_t n,
                                     const double* __restrict__ params, int P,
-                                    double* __restrict__ out) {
+                                    double* __restrict__ out, const int* flag) {
+    // x need not be monotone here: lanes check their own x
+    const bool fast_peaks = *flag == 0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * blockDim.x)
-        out[i] = superpose(x[i], params, P);
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const double xi = x[i];
+        out[i] = superpose(xi, params, P, fast_peaks && x_fast_ok(xi));
+    }
 }
 
 // synthetic batch: x shared, y_s = superposition(params_s) + noise(seed_s)
@@ -949,7 +1049,7 @@ __global__ void k_synth_y(const double* __restrict__ x, int64_t n,
     const double* ps = params + 3 * (size_t)s * P;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x)
-        y[(size_t)s * n + i] = superpose(x[i], ps, P) + synth_noise(key, (uint64_t)i, sigma);
+        y[(size_t)s * n + i] = superpose(x[i], ps, P, false) + synth_noise(key, (uint64_t)i, sigma);
 }
 
 // ----------------------------------------------------------------------------------
@@ -1001,18 +1101,18 @@ void launch_select(const BatchArgs& a, const Workspace& w, int detector_only, do
 void launch_fit_init(const BatchArgs& a, const Workspace& w, int gx, hipStream_t st) {
     hipLaunchKernelGGL(k_fit_init, dim3(gx, a.B), dim3(256), 0, st, a, w);
 }
-void launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, hipStream_t st) {
+void launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st) {
     if (a.B <= 16) {
-        // ~16 points per workgroup: enough workgroups to cover 3P points of every
-        // spectrum in one sweep for P up to ~4k and to occupy all 256 CUs
-        const int g = std::max(64, std::min(2048, 8192 / a.B));
-        hipLaunchKernelGGL(k_fit_sup_split, dim3(g, a.B), dim3(128), 0, st, a, w);
+        // 16 points per 1024-thread workgroup: 3P/16 workgroups per spectrum (384 at
+        // P = 2048) keep every CU busy; grid-stride beyond that
+        const int g = std::max(64, std::min(1024, 2048 / a.B));
+        hipLaunchKernelGGL((k_fit_sup_split<16, 128, 1024>), dim3(g, a.B), dim3(1024), 0, st, a, w, it);
     } else {
-        hipLaunchKernelGGL(k_fit_sup, dim3(gx, a.B), dim3(256), 0, st, a, w);
+        hipLaunchKernelGGL(k_fit_sup, dim3(gx, a.B), dim3(256), 0, st, a, w, it);
     }
 }
-void launch_fit_update(const BatchArgs& a, const Workspace& w, int gx, hipStream_t st) {
-    hipLaunchKernelGGL(k_fit_update, dim3(gx, a.B), dim3(256), 0, st, a, w);
+void launch_fit_update(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st) {
+    hipLaunchKernelGGL(k_fit_update, dim3(gx, a.B), dim3(256), 0, st, a, w, it);
 }
 void launch_retain(const BatchArgs& a, const Workspace& w, hipStream_t st) {
     hipLaunchKernelGGL(k_retain<1024>, dim3(a.B), dim3(1024), 0, st, a, w);
@@ -1024,9 +1124,13 @@ void launch_mse_final(const BatchArgs& a, const Workspace& w, int nparts, hipStr
     hipLaunchKernelGGL(k_mse_final, dim3(cdiv(a.B, 64)), dim3(64), 0, st, a, w, nparts);
 }
 void launch_superposition_vec(const double* x, int64_t n, const double* params, int P,
-                              double* out, hipStream_t st) {
+                              double* out, int* flag, hipStream_t st) {
+    (void)hipMemsetAsync(flag, 0, sizeof(int), st);
+    hipLaunchKernelGGL(k_range_check, dim3(std::max(1u, std::min(cdiv(P, 256), 1024u))), dim3(256),
+                       0, st, x, n, params, P, flag);
     const unsigned g = std::max(1u, std::min(cdiv(n, 256), 65535u));
-    hipLaunchKernelGGL(k_superposition_vec, dim3(g), dim3(256), 0, st, x, n, params, P, out);
+    hipLaunchKernelGGL(k_superposition_vec, dim3(g), dim3(256), 0, st, x, n, params, P, out,
+                       (const int*)flag);
 }
 void launch_synth(double* x, double* y, int64_t n, int B, double xmax, double width,
                   const double* params, int P, uint64_t seed0, double sigma, hipStream_t st) {

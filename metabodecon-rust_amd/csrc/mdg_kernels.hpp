@@ -70,6 +70,9 @@ struct Workspace {
     int32_t* det_count;
     int32_t* sel_count;
     int32_t* kept_count;
+    int32_t* x_ok;            // B: axis inside the fast-division range
+    int32_t* unsafe;          // B x 2: ping-pong count of fit params outside it
+    int32_t* unsafe_kept;     // B: same for the retained Lorentzians
 };
 
 void launch_prep(const BatchArgs& a, const Workspace& w, hipStream_t st);
@@ -79,13 +82,13 @@ void launch_peaks(const BatchArgs& a, const Workspace& w, int detector_only, hip
 void launch_select(const BatchArgs& a, const Workspace& w, int detector_only, double threshold,
                    hipStream_t st);
 void launch_fit_init(const BatchArgs& a, const Workspace& w, int gx, hipStream_t st);
-void launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, hipStream_t st);
-void launch_fit_update(const BatchArgs& a, const Workspace& w, int gx, hipStream_t st);
+void launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st);
+void launch_fit_update(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st);
 void launch_retain(const BatchArgs& a, const Workspace& w, hipStream_t st);
 void launch_mse(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st);
 void launch_mse_final(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st);
 void launch_superposition_vec(const double* x, int64_t n, const double* params, int P,
-                              double* out, hipStream_t st);
+                              double* out, int* flag, hipStream_t st);
 void launch_synth(double* x, double* y, int64_t n, int B, double xmax, double width,
                   const double* params, int P, uint64_t seed0, double sigma, hipStream_t st);
 
