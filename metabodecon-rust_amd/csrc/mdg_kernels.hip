@@ -14,6 +14,9 @@
 #include "mdg_common.hpp"
 #include "mdg_kernels.hpp"
 
+#include <cstdlib>
+#include <string>
+
 namespace mdg {
 
 // ----------------------------------------------------------------------------------
@@ -426,6 +429,101 @@ __global__ __launch_bounds__(64) void k_smooth_pipe(BatchArgs a, Workspace w, in
         }
     }
     generic(tB, T);
+}
+
+// ----------------------------------------------------------------------------------
+// K1c  wave-per-pass moving average (small batches; measured: one wave issues one
+// f64 add per ~4.7 cycles whether dependent or not, so the recurrence is
+// issue-bound and the passes must run on separate SIMDs).
+//
+// Workgroup = one spectrum, wave p = pass p, and only lane 0 of each wave runs
+// the recurrence (tick: ds_read in, add, sub, mul, ds_write emit). Pass p emits
+// o_p[i] at tick i+R into LDS ring p (4 blocks of U ticks); pass p+1 runs two
+// blocks behind and reads it back, so one barrier per block of U ticks orders
+// every hand-off. Wave 0's 64 lanes prefetch raw input blocks into LDS one block
+// ahead; the last wave's 64 lanes copy its ring block to HBM coalesced.
+// ----------------------------------------------------------------------------------
+template <int WS>
+__global__ __launch_bounds__(512) void k_smooth_waves(BatchArgs a, Workspace w, int P) {
+    constexpr int R = WS / 2;
+    constexpr int U = WS * ((64 + WS - 1) / WS);  // ticks per block (multiple of WS)
+    constexpr int RING = 4 * U;                   // 4 blocks per ring
+    constexpr int LAG = 2;                        // blocks between consecutive passes
+    static_assert(R < U, "block shorter than the window");
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double* raw = lds;              // 2 blocks of raw input (pass 0)
+    double* rings = lds + 2 * U;    // ring p: emits of pass p stored at their tick slot
+    const int s = blockIdx.x;
+    if (w.status[s]) return;  // uniform per workgroup
+    const int p = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int N = a.N;
+    const double* yrow = a.y + (size_t)s * a.y_stride;
+    double* orow = w.smooth + (size_t)s * N;
+    const int nkb = (N + R + U - 1) / U;  // blocks of ticks per pass
+    const int total = nkb + LAG * (P - 1);
+    double* my_ring = rings + p * RING;
+    const double* in_ring = rings + (p > 0 ? p - 1 : 0) * RING;
+    MAState<WS> st;
+    st.sum = 0.0;
+    st.div = 1.0;
+#pragma unroll
+    for (int k = 0; k < WS; ++k) st.fifo[k] = 0.0;
+    if (p == 0)
+        for (int k = lane; k < U; k += 64) raw[k] = k < N ? yrow[k] : 0.0;
+    __syncthreads();
+    for (int gb = 0; gb < total; ++gb) {
+        const int kb = gb - LAG * p;
+        // wave 0 prefetches raw block kb+1 into registers; stored to LDS after the work
+        double pre0 = 0.0, pre1 = 0.0;
+        const int nb = kb + 1;
+        if (p == 0 && nb < nkb) {
+            const int q0 = nb * U + lane, q1 = nb * U + 64 + lane;
+            pre0 = q0 < N ? yrow[q0] : 0.0;
+            if (64 + lane < U) pre1 = q1 < N ? yrow[q1] : 0.0;
+        }
+        if (lane == 0 && kb >= 0 && kb < nkb) {
+            const int q0 = kb * U;
+            double* out = my_ring + (kb & 3) * U;  // slot of tick q0 + k
+            // gather the whole block's inputs first: every LDS read is issued before
+            // the first write (the compiler cannot reorder reads past ring writes)
+            double in[U];
+            if (p == 0) {
+                const double* src = raw + (kb & 1) * U;
+#pragma unroll
+                for (int k = 0; k < U; ++k) in[k] = src[k];
+            } else {
+                const double* in0 = in_ring + (kb & 3) * U + R;  // o_{p-1}[q] sits at tick q+R
+                const double* in1 = in_ring + ((kb + 1) & 3) * U + R - U;
+#pragma unroll
+                for (int k = 0; k < U; ++k) in[k] = k + R < U ? in0[k] : in1[k];
+            }
+            if (q0 >= WS && q0 + U <= N) {
+#pragma unroll
+                for (int k = 0; k < U; ++k) out[k] = ma_tick_steady<WS>(st, k % WS, in[k]);
+            } else {
+#pragma unroll
+                for (int k = 0; k < U; ++k) {
+                    const int q = q0 + k;
+                    out[k] = ma_tick_generic<WS>(st, k % WS, q, N, q < N ? in[k] : 0.0);
+                }
+            }
+        }
+        if (p == 0 && nb < nkb) {
+            double* dst = raw + (nb & 1) * U;
+            dst[lane] = pre0;
+            if (64 + lane < U) dst[64 + lane] = pre1;
+        }
+        __syncthreads();
+        // last pass: slot k of block kb holds o[kb*U + k - R]
+        if (p == P - 1 && kb >= 0 && kb < nkb) {
+            const double* blk = my_ring + (kb & 3) * U;
+            for (int k = lane; k < U; k += 64) {
+                const int i = kb * U + k - R;
+                if (i >= 0 && i < N) orow[i] = blk[k];
+            }
+        }
+    }
 }
 
 __global__ void k_smooth(BatchArgs a, Workspace w, int iters, int ws) {
@@ -1061,6 +1159,13 @@ void launch_prep(const BatchArgs& a, const Workspace& w, hipStream_t st) {
     hipLaunchKernelGGL(k_prep, dim3(cdiv(a.B, 64)), dim3(64), 0, st, a, w);
 }
 template <int WS>
+static void launch_waves(const BatchArgs& a, const Workspace& w, int iters, hipStream_t st) {
+    constexpr int U = WS * ((64 + WS - 1) / WS);
+    const size_t lds = sizeof(double) * (2 * U + (size_t)iters * 4 * U);
+    hipLaunchKernelGGL(k_smooth_waves<WS>, dim3(a.B), dim3(64 * iters), lds, st, a, w, iters);
+}
+
+template <int WS>
 static void launch_pipe(const BatchArgs& a, const Workspace& w, int iters, hipStream_t st) {
     const int spw = 64 / iters;
     hipLaunchKernelGGL(k_smooth_pipe<WS>, dim3(cdiv(a.B, spw)), dim3(64), 0, st, a, w, iters, spw);
@@ -1069,6 +1174,22 @@ static void launch_pipe(const BatchArgs& a, const Workspace& w, int iters, hipSt
 void launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int ws, hipStream_t st) {
     // lane-pipelined kernel whenever the window fits the register FIFO and the
     // spectrum is longer than the window; the one-lane-per-spectrum kernel otherwise
+    const bool waves = std::getenv("MDG_SMOOTH") ? std::string(std::getenv("MDG_SMOOTH")) == "waves"
+                                                 : a.B <= 512;
+    if (waves && iters >= 1 && iters <= 8 && a.N > ws + 1) {
+        switch (ws) {
+            case 2: return launch_waves<2>(a, w, iters, st);
+            case 3: return launch_waves<3>(a, w, iters, st);
+            case 4: return launch_waves<4>(a, w, iters, st);
+            case 5: return launch_waves<5>(a, w, iters, st);
+            case 6: return launch_waves<6>(a, w, iters, st);
+            case 7: return launch_waves<7>(a, w, iters, st);
+            case 8: return launch_waves<8>(a, w, iters, st);
+            case 9: return launch_waves<9>(a, w, iters, st);
+            case 11: return launch_waves<11>(a, w, iters, st);
+            default: break;
+        }
+    }
     if (iters >= 1 && iters <= 32 && a.N > ws + 1) {
         switch (ws) {
             case 2: return launch_pipe<2>(a, w, iters, st);

@@ -204,8 +204,13 @@ def test_small_and_odd_shapes(ctx):
             assert abs(mse[0] - o.mse) <= MSE_RTOL * abs(o.mse)
 
 
-@pytest.mark.parametrize("it,ws", [(1, 2), (2, 4), (5, 7), (3, 31)])
-def test_smoother_settings_sweep(ctx, it, ws):
+@pytest.mark.parametrize("path", ["waves", "pipe"])
+@pytest.mark.parametrize("it,ws", [(1, 2), (2, 4), (3, 3), (5, 7), (8, 5), (10, 3), (3, 31),
+                                   (4, 9), (2, 11)])
+def test_smoother_settings_sweep(ctx, it, ws, path, monkeypatch):
+    """Both exact smoother kernels (wave-per-pass and lane-pipelined, chosen by
+    MDG_SMOOTH) against the oracle; (3, 31) and iterations > 8 exercise fallbacks."""
+    monkeypatch.setenv("MDG_SMOOTH", path)
     x, y, sb, _, _ = load_case("blood_05")
     st = oracle.make_settings(smooth_iterations=it, smooth_window=ws)
     o = oracle.deconvolute(x, y, sb, st)
