@@ -16,6 +16,7 @@
 
 #include <cstdlib>
 #include <string>
+#include <type_traits>
 
 namespace mdg {
 
@@ -96,6 +97,40 @@ __device__ __forceinline__ double superpose_t(double x, const double* __restrict
 __device__ __forceinline__ double superpose(double x, const double* __restrict__ params, int P,
                                             bool fast) {
     return fast ? superpose_t<true>(x, params, P) : superpose_t<false>(x, params, P);
+}
+
+// Diagnostic stamps (tools/ubench/smooth_diag.hip builds with -DMDG_DIAG): per-wave
+// cycle sums of kernel phases, written to a side buffer only. Empty otherwise.
+#ifdef MDG_DIAG
+__device__ long long* g_diag = nullptr;
+#define DIAG_DECL unsigned long long _d_t = __builtin_amdgcn_s_memtime(); unsigned long long _d_acc[8] = {0};
+#define DIAG_STAMP(i)                                                       \
+    do {                                                                    \
+        __builtin_amdgcn_sched_barrier(0);                                  \
+        const unsigned long long _n = __builtin_amdgcn_s_memtime();         \
+        _d_acc[i] += _n - _d_t;                                             \
+        _d_t = _n;                                                          \
+        __builtin_amdgcn_sched_barrier(0);                                  \
+    } while (0)
+#define DIAG_FLUSH()                                                        \
+    do {                                                                    \
+        if ((threadIdx.x & 63) == 0 && g_diag)                              \
+            for (int _i = 0; _i < 8; ++_i)                                  \
+                g_diag[(blockIdx.x * 16 + (threadIdx.x >> 6)) * 8 + _i] = (long long)_d_acc[_i]; \
+    } while (0)
+#else
+#define DIAG_DECL
+#define DIAG_STAMP(i)
+#define DIAG_FLUSH()
+#endif
+
+// Workgroup barrier that orders LDS only. __syncthreads() also waits vmcnt(0), i.e.
+// for every global load/store the wave has in flight -- that would drain the
+// HBM prefetches and the write-back stores these pipelines keep in flight across
+// barriers. Register results of global loads are still waited for by the
+// compiler at their first use.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 // D[k] := sd[k-1] = (s[k-1] - 2*s[k]) + s[k+1]   (common.rs:5-10, intensity aligned)
@@ -446,75 +481,111 @@ __global__ __launch_bounds__(64) void k_smooth_pipe(BatchArgs a, Workspace w, in
 template <int WS>
 __global__ __launch_bounds__(512) void k_smooth_waves(BatchArgs a, Workspace w, int P) {
     constexpr int R = WS / 2;
-    constexpr int U = WS * ((64 + WS - 1) / WS);  // ticks per block (multiple of WS)
-    constexpr int RING = 4 * U;                   // 4 blocks per ring
+    constexpr int U = WS * ((32 + WS - 1) / WS);  // ticks per block (multiple of WS)
+    constexpr int RING = 4 * U;                   // 4 blocks per emit ring
     constexpr int LAG = 2;                        // blocks between consecutive passes
+    constexpr int PIECES = (U * 8 + 255) / 256;   // 256-byte DMA pieces per raw block
+    constexpr int RAWSLOT = PIECES * 32;          // raw slot stride in doubles (padded)
     static_assert(R < U, "block shorter than the window");
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    double* raw = lds;              // 2 blocks of raw input (pass 0)
-    double* rings = lds + 2 * U;    // ring p: emits of pass p stored at their tick slot
+    double* raw = lds;                   // 4 slots of one raw block each (wave 0's input)
+    double* rings = lds + 4 * RAWSLOT;   // ring p: emits of pass p at their tick slot
     const int s = blockIdx.x;
     if (w.status[s]) return;  // uniform per workgroup
+    // waves >= P are idle and only join the barriers: the workgroup is padded to a
+    // multiple of 4 waves because 3-wave workgroups measured ~2x slower per op
+    // (tools/ubench: 9-12 vs 5 cycles per dependent f64 add)
     const int p = threadIdx.x >> 6;
+    const bool active = p < P;
     const int lane = threadIdx.x & 63;
     const int N = a.N;
     const double* yrow = a.y + (size_t)s * a.y_stride;
     double* orow = w.smooth + (size_t)s * N;
     const int nkb = (N + R + U - 1) / U;  // blocks of ticks per pass
     const int total = nkb + LAG * (P - 1);
-    double* my_ring = rings + p * RING;
+    double* my_ring = rings + (active ? p : 0) * RING;
     const double* in_ring = rings + (p > 0 ? p - 1 : 0) * RING;
     MAState<WS> st;
     st.sum = 0.0;
     st.div = 1.0;
 #pragma unroll
     for (int k = 0; k < WS; ++k) st.fifo[k] = 0.0;
-    if (p == 0)
-        for (int k = lane; k < U; k += 64) raw[k] = k < N ? yrow[k] : 0.0;
-    __syncthreads();
+
+    // Raw input of wave 0 arrives by LDS-DMA (global_load_lds, 4 bytes per lane,
+    // PIECES instructions per block) three blocks ahead, into slot j&3. No VGPR
+    // holds an in-flight load, so nothing makes the compiler drain the queue;
+    // the one wait is the counted vmcnt below. Past-the-end dwords are clamped to
+    // the row's last dword (never consumed: ticks >= N take no input).
+    const int last_dw = 2 * N - 1;
+    auto dma_block = [&](int j) {
+        const unsigned* src = (const unsigned*)yrow;
+        double* slot = raw + (j & 3) * RAWSLOT;
+#pragma unroll
+        for (int pc = 0; pc < PIECES; ++pc) {
+            const int dw = min(j * U * 2 + pc * 64 + lane, last_dw);
+            __builtin_amdgcn_global_load_lds((const void*)(src + dw),
+                                             (__attribute__((address_space(3))) void*)(slot + pc * 32),
+                                             4, 0, 0);
+        }
+    };
+    if (p == 0) {
+        dma_block(0);
+        dma_block(1);
+        dma_block(2);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    lds_barrier();
+    DIAG_DECL
     for (int gb = 0; gb < total; ++gb) {
         const int kb = gb - LAG * p;
-        // wave 0 prefetches raw block kb+1 into registers; stored to LDS after the work
-        double pre0 = 0.0, pre1 = 0.0;
-        const int nb = kb + 1;
-        if (p == 0 && nb < nkb) {
-            const int q0 = nb * U + lane, q1 = nb * U + 64 + lane;
-            pre0 = q0 < N ? yrow[q0] : 0.0;
-            if (64 + lane < U) pre1 = q1 < N ? yrow[q1] : 0.0;
-        }
-        if (lane == 0 && kb >= 0 && kb < nkb) {
+        if (p == 0) dma_block(kb + 3);  // j beyond nkb: harmless clamped copy
+        DIAG_STAMP(0);
+        // All 64 lanes run the recurrence redundantly (identical values): with one
+        // active lane, waves of a workgroup running concurrently on other SIMDs
+        // slowed every f64 op to 10-15 cycles; with full EXEC each sustains 4.6
+        // (tools/ubench, wave_chain). Only the ring write-back is lane 0's.
+        if (active && kb >= 0 && kb < nkb) {
             const int q0 = kb * U;
             double* out = my_ring + (kb & 3) * U;  // slot of tick q0 + k
-            // gather the whole block's inputs first: every LDS read is issued before
-            // the first write (the compiler cannot reorder reads past ring writes)
-            double in[U];
+            // gather the whole block's inputs first (broadcast LDS reads): every read
+            // is issued before any write (reads cannot be reordered past ring writes)
+            double v[U];
             if (p == 0) {
-                const double* src = raw + (kb & 1) * U;
+                const double* src = raw + (kb & 3) * RAWSLOT;
 #pragma unroll
-                for (int k = 0; k < U; ++k) in[k] = src[k];
+                for (int k = 0; k < U; ++k) v[k] = src[k];
             } else {
                 const double* in0 = in_ring + (kb & 3) * U + R;  // o_{p-1}[q] sits at tick q+R
                 const double* in1 = in_ring + ((kb + 1) & 3) * U + R - U;
 #pragma unroll
-                for (int k = 0; k < U; ++k) in[k] = k + R < U ? in0[k] : in1[k];
+                for (int k = 0; k < U; ++k) v[k] = k + R < U ? in0[k] : in1[k];
             }
+            DIAG_STAMP(1);
             if (q0 >= WS && q0 + U <= N) {
 #pragma unroll
-                for (int k = 0; k < U; ++k) out[k] = ma_tick_steady<WS>(st, k % WS, in[k]);
+                for (int k = 0; k < U; ++k) v[k] = ma_tick_steady<WS>(st, k % WS, v[k]);
             } else {
 #pragma unroll
                 for (int k = 0; k < U; ++k) {
                     const int q = q0 + k;
-                    out[k] = ma_tick_generic<WS>(st, k % WS, q, N, q < N ? in[k] : 0.0);
+                    v[k] = ma_tick_generic<WS>(st, k % WS, q, N, q < N ? v[k] : 0.0);
                 }
             }
+            if (lane == 0) {
+#pragma unroll
+                for (int k = 0; k < U; ++k) out[k] = v[k];
+            }
         }
-        if (p == 0 && nb < nkb) {
-            double* dst = raw + (nb & 1) * U;
-            dst[lane] = pre0;
-            if (64 + lane < U) dst[64 + lane] = pre1;
+        DIAG_STAMP(2);
+        if (p == 0) {
+            // block kb+1's DMA must have landed; only blocks kb+2, kb+3 may be in flight
+            // (wave 0 issues no other vector-memory op unless it is also the last pass)
+            if (P == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PIECES) : "memory");
         }
-        __syncthreads();
+        DIAG_STAMP(3);
+        lds_barrier();
+        DIAG_STAMP(4);
         // last pass: slot k of block kb holds o[kb*U + k - R]
         if (p == P - 1 && kb >= 0 && kb < nkb) {
             const double* blk = my_ring + (kb & 3) * U;
@@ -523,7 +594,9 @@ __global__ __launch_bounds__(512) void k_smooth_waves(BatchArgs a, Workspace w, 
                 if (i >= 0 && i < N) orow[i] = blk[k];
             }
         }
+        DIAG_STAMP(5);
     }
+    DIAG_FLUSH();
 }
 
 __global__ void k_smooth(BatchArgs a, Workspace w, int iters, int ws) {
@@ -935,7 +1008,7 @@ __global__ __launch_bounds__(BS) void k_fit_sup_split(BatchArgs a, Workspace w, 
                     pf[r][2] = ok ? params[3 * j + 2] : 0.0;
                 }
             }
-            __syncthreads();
+            lds_barrier();
             if (c > 0) {
                 const int cc = c - 1;
                 if (wv == cc % NW && lane < Q) {
@@ -1160,9 +1233,11 @@ void launch_prep(const BatchArgs& a, const Workspace& w, hipStream_t st) {
 }
 template <int WS>
 static void launch_waves(const BatchArgs& a, const Workspace& w, int iters, hipStream_t st) {
-    constexpr int U = WS * ((64 + WS - 1) / WS);
-    const size_t lds = sizeof(double) * (2 * U + (size_t)iters * 4 * U);
-    hipLaunchKernelGGL(k_smooth_waves<WS>, dim3(a.B), dim3(64 * iters), lds, st, a, w, iters);
+    constexpr int U = WS * ((32 + WS - 1) / WS);
+    constexpr int RAWSLOT = ((U * 8 + 255) / 256) * 32;
+    const size_t lds = sizeof(double) * (4 * RAWSLOT + (size_t)iters * 4 * U);
+    const int waves = (iters + 3) / 4 * 4;
+    hipLaunchKernelGGL(k_smooth_waves<WS>, dim3(a.B), dim3(64 * waves), lds, st, a, w, iters);
 }
 
 template <int WS>
@@ -1174,8 +1249,10 @@ static void launch_pipe(const BatchArgs& a, const Workspace& w, int iters, hipSt
 void launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int ws, hipStream_t st) {
     // lane-pipelined kernel whenever the window fits the register FIFO and the
     // spectrum is longer than the window; the one-lane-per-spectrum kernel otherwise
-    const bool waves = std::getenv("MDG_SMOOTH") ? std::string(std::getenv("MDG_SMOOTH")) == "waves"
-                                                 : a.B <= 512;
+    // measured (bench stages): lane-pipelined 3.05 ms vs wave-per-pass 3.3 ms at B = 1;
+    // at B = 256 wave-per-pass 3.0 ms vs 4.7 ms (21 spectra per lane-pipelined wave)
+    const char* force = std::getenv("MDG_SMOOTH");
+    const bool waves = force ? std::string(force) == "waves" : a.B > 21;
     if (waves && iters >= 1 && iters <= 8 && a.N > ws + 1) {
         switch (ws) {
             case 2: return launch_waves<2>(a, w, iters, st);
