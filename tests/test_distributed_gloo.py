@@ -1,0 +1,92 @@
+"""World-size-2 tests of the multi-GPU path on CPU (gloo backend).
+
+The per-rank compute is replaced by the oracle (test infrastructure) so the
+sharding, the padded all_gather of the Lorentzian tables and the fail-fast
+error order can be checked without a GPU. On the GPU box the same module runs
+with the nccl (RCCL) backend and the HIP engine as ``compute``.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from metabodecon.distributed import shard_range
+
+
+def test_shard_range_partitions():
+    for n in range(0, 40):
+        for world in range(1, 9):
+            ranges = [shard_range(n, r, world) for r in range(world)]
+            assert ranges[0][0] == 0 and ranges[-1][1] == n
+            assert all(ranges[i][1] == ranges[i + 1][0] for i in range(world - 1))
+            sizes = [hi - lo for lo, hi in ranges]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "metabodecon-rust_amd")]
+    import torch.distributed as dist
+    import oracle
+    from metabodecon.distributed import deconvolute_distributed
+    from tests.golden.cases import load_case
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        names = [f"sim_{i:02d}" for i in range(1, 8)]
+        spectra = [load_case(n) for n in names]
+        # inject one failing spectrum (flat -> NoPeaksDetected) and one more failure later
+        x, y, sb, st, ign = spectra[2]
+        spectra[2] = (x, np.full_like(y, 3.0), sb, st, ign)
+        spectra[5] = (x, np.full_like(y, 1.0), sb, st, ign)
+
+        def compute(block):
+            out = []
+            for (x, y, sb, st, ign) in block:
+                r = oracle.deconvolute(x, y, sb, st, ignore=ign)
+                out.append((r.status, r.params, r.mse))
+            return out
+
+        res = deconvolute_distributed(spectra, compute)
+        q.put((rank, [(s, p.tolist(), m) for s, p, m in res]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_gloo_world2_gather_matches_serial():
+    import oracle
+    from tests.golden.cases import load_case
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got[0] == got[1]  # every rank holds the full, identical result list
+    names = [f"sim_{i:02d}" for i in range(1, 8)]
+    for k, n in enumerate(names):
+        x, y, sb, st, ign = load_case(n)
+        if k in (2, 5):
+            y = np.full_like(y, 3.0 if k == 2 else 1.0)
+        r = oracle.deconvolute(x, y, sb, st, ignore=ign)
+        s, p, m = got[0][k]
+        assert s == r.status
+        if s == 0:
+            assert np.array_equal(np.array(p).reshape(-1, 3), r.params) and m == r.mse
+    first_err = next(s for s, _, _ in got[0] if s)
+    assert first_err == 1  # fail-fast reports the first failing spectrum in order

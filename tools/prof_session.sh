@@ -1,12 +1,19 @@
 #!/bin/bash
-# rocprofv3 kernel-trace/stats of bench.py (one config per call); outputs under gpurun_out/
+# rocprofv3 runs of bench.py; outputs under gpurun_out/prof_<tag>*/
+#   trace <tag> [bench args]   kernel trace + stats
+#   pmc <tag> <COUNTER> [bench args]  one PMC counter pass (never with sys/runtime traces)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-tag=$1; shift
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/gpurun_out/prof_$tag" -o run -- python3 "$ROOT/bench.py" --no-cpu-baseline "$@" > "gpurun_out/prof_$tag.log" 2>&1
+mode=$1; tag=$2; shift 2
+if [ "$mode" = trace ]; then
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/gpurun_out/prof_$tag" -o run -- python3 "$ROOT/bench.py" --no-cpu-baseline "$@" > "gpurun_out/prof_$tag.log" 2>&1
+else
+  ctr=$1; shift
+  timeout -k 10 600 rocprofv3 --pmc "$ctr" --output-format csv -d "$ROOT/gpurun_out/prof_${tag}_$ctr" -o run -- python3 "$ROOT/bench.py" --no-cpu-baseline --no-profile "$@" > "gpurun_out/prof_${tag}_$ctr.log" 2>&1
+fi
 rc=$?
-echo "prof $tag rc=$rc"
-tail -3 "gpurun_out/prof_$tag.log"
+echo "prof $mode $tag rc=$rc"
+tail -2 "gpurun_out/prof_$tag"*.log
 exit $rc
