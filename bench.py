@@ -42,7 +42,9 @@ def parse():
     ap.add_argument("--n", type=int, default=131072)
     ap.add_argument("--peaks", type=int, default=2048)
     ap.add_argument("--cap", type=int, default=4096)
-    ap.add_argument("--cpu-sample", type=int, default=16, help="spectra in the CPU sample")
+    ap.add_argument("--cpu-sample", type=int, default=64,
+                    help="spectra in the all-cores CPU sample (~10-15 core-seconds)")
+    ap.add_argument("--cpu-single", type=int, default=8, help="spectra in the 1-core sample")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="no per-stage HIP events")
@@ -54,6 +56,16 @@ def sbi_len(x0, step, sb0, sb1):
     a = max(0, math.floor((sb0 - x0) / step))
     b = max(0, math.ceil((sb1 - x0) / step))
     return b - a
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def cpu_baseline(args, threads):
@@ -71,11 +83,12 @@ def cpu_baseline(args, threads):
         nat.lib().mdg_synth_noise(s, n, 1.0e3, nat.ptr(noise))
         ys[s] = oracle.superposition_vec(x, p, threads=threads) + noise
     sb = np.array([[11.8, -2.2]] * S)
-    # single core: deconvolute_spectrum semantics on one spectrum
+    # single core: deconvolute_spectrum semantics, one spectrum after another
+    S1 = max(1, min(args.cpu_single, S))
     t = time.perf_counter()
-    r = oracle.deconvolute(x, ys[0], (11.8, -2.2), threads=1)
-    single = 1.0 / (time.perf_counter() - t)
-    assert r.status == 0
+    for s in range(S1):
+        assert oracle.deconvolute(x, ys[s], (11.8, -2.2), threads=1).status == 0
+    single = S1 / (time.perf_counter() - t)
     # all cores: par_deconvolute_spectra semantics (one spectrum per thread)
     t = time.perf_counter()
     status, counts, _, _ = oracle.deconvolute_batch(x, ys, sb, threads=threads, cap=args.cap)
@@ -85,7 +98,8 @@ def cpu_baseline(args, threads):
         "value": S / wall, "unit": "spectra/s", "cores": threads, "kind": "port",
         "sample": (f"{S} synthetic {n}-pt/{peaks}-peak spectra (seeds 0..{S - 1}), oracle "
                    f"C restatement -O3 -ffp-contract=off, {threads} threads over spectra "
-                   f"({wall:.2f} s wall); single core {single:.3f} spectra/s"),
+                   f"({wall:.2f} s wall, {wall * threads:.1f} core-s); single core {single:.3f} "
+                   f"spectra/s over {S1} spectra; host {_cpu_model()}"),
         "single_core_value": single,
     }
 
@@ -171,7 +185,7 @@ def main():
     L = sbi_len(xh0, xh1 - xh0, 11.8, -2.2)
     fit_flops = sum(FLOPS_PER_EVAL * 3 * p * p for p in P_sel)           # per launch (1 iteration)
     mse_flops = sum((FLOPS_PER_EVAL * int(k) + 3) * L for k in counts)     # per launch
-    smooth_bytes = B * settings.smooth_iterations * 16 * n                # per launch
+    smooth_bytes = B * 16 * n  # per launch: y read once, smoothed row written once (passes fused on chip)
     detect_bytes = B * (8 * n + 3 * ((n + 63) // 64) * 8)
     work = {
         "fit_superposition": ("fp64", fit_flops, "TFLOP/s", "k_fit_sup"),
@@ -192,15 +206,19 @@ def main():
         else:
             achieved = amount / avg_s / 1e9
             peak = HBM_PEAK_GBS
-        traffic = None
-        pmc = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
+        # HBM bytes per launch of this stage from the committed PMC passes of the same
+        # batch size (tools/pmc_summary.py; FETCH_SIZE doubled per the gfx950 note)
+        traffic, traffic_src = None, None
+        pmc = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_b{B}.json")))
         if pmc:
             try:
-                traffic = json.load(open(pmc[-1])).get(kname, {}).get("hbm_bytes_per_launch")
-            except Exception:
+                traffic = json.load(open(pmc[-1]))["stages"][dom]["hbm_bytes_per_launch"]
+                traffic_src = os.path.relpath(pmc[-1], ROOT)
+            except (OSError, KeyError, ValueError):
                 traffic = None
         roofline = {"bound": bound, "kernel": kname, "stage": dom, "achieved": achieved,
                     "peak": peak, "unit": unit, "frac": achieved / peak, "traffic": traffic,
+                    "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                     "avg_launch_ms": avg_s * 1e3, "algorithmic_per_launch": amount}
 
     total_spectra = world * B * args.steps

@@ -1,0 +1,91 @@
+"""Summarise rocprofv3 runs of bench.py into profiles/ (per round, per batch size).
+
+    python tools/pmc_summary.py r01 b1 [b256 ...]
+
+Reads gpurun_out/prof_<tag>/run_kernel_stats.csv (kernel trace + stats) and the
+separate PMC passes gpurun_out/prof_<tag>_FETCH_SIZE and _WRITE_SIZE, and writes
+  profiles/<round>_<tag>_kernel_stats.csv   (copy of the rocprofv3 --stats summary)
+  profiles/<round>_pmc_<tag>.json           (HBM bytes per launch, keyed by stage)
+FETCH_SIZE/WRITE_SIZE are in KiB. On gfx950 FETCH_SIZE counts half the bytes of a
+coalesced streaming read (MI355X_MICROARCH.md, HBM/rocprofv3 section), so it is
+doubled; WRITE_SIZE is taken as is.
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+STAGES = [  # stage -> kernel-name prefixes (after "mdg::")
+    ("smooth", ("k_smooth",)),
+    ("detect", ("k_flags", "k_peaks")),
+    ("select", ("k_select",)),
+    ("fit_init", ("k_fit_init",)),
+    ("fit_superposition", ("k_fit_sup",)),
+    ("fit_update", ("k_fit_update",)),
+    ("retain", ("k_retain",)),
+    ("mse_superposition", ("k_mse_partial",)),
+    ("mse_reduce", ("k_mse_final",)),
+]
+
+
+def short(name):
+    n = name.replace("void ", "")
+    n = n[5:] if n.startswith("mdg::") else n
+    return n.split("(")[0]
+
+
+def stage_of(kname):
+    for st, prefixes in STAGES:
+        if any(kname.startswith(p) for p in prefixes):
+            return st
+    return None
+
+
+def per_kernel(path, counter):
+    acc = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] == counter:
+            acc[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def main(rnd, tags):
+    os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
+    for tag in tags:
+        base = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+        stats = os.path.join(base, "run_kernel_stats.csv")
+        avg_ns = {}
+        if os.path.exists(stats):
+            shutil.copy(stats, os.path.join(ROOT, "profiles", f"{rnd}_{tag}_kernel_stats.csv"))
+            for r in csv.DictReader(open(stats)):
+                avg_ns[short(r["Name"])] = float(r["AverageNs"])
+        fetch = per_kernel(os.path.join(base + "_FETCH_SIZE", "run_counter_collection.csv"),
+                           "FETCH_SIZE")
+        write = per_kernel(os.path.join(base + "_WRITE_SIZE", "run_counter_collection.csv"),
+                           "WRITE_SIZE")
+        kernels = {}
+        for k in sorted(set(fetch) | set(write)):
+            f, w = fetch.get(k, 0.0), write.get(k, 0.0)
+            kernels[k] = {"fetch_size_kib_raw": f, "write_size_kib": w,
+                          "hbm_bytes_per_launch": (2 * f + w) * 1024,
+                          "avg_ns": avg_ns.get(k)}
+        stages = {}
+        for st, _ in STAGES:
+            ks = [k for k in kernels if stage_of(k) == st]
+            if ks:  # one launch of each member kernel per stage launch
+                stages[st] = {"kernels": ks,
+                              "hbm_bytes_per_launch": sum(kernels[k]["hbm_bytes_per_launch"]
+                                                          for k in ks)}
+        out = {"round": rnd, "tag": tag,
+               "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE half-count)",
+               "stages": stages, "kernels": kernels}
+        path = os.path.join(ROOT, "profiles", f"{rnd}_pmc_{tag}.json")
+        json.dump(out, open(path, "w"), indent=1)
+        print("wrote", path)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2:])
