@@ -157,6 +157,12 @@ int mdg_deconvolute_batch_device(mdg_ctx* ctx, size_t b, size_t n, const double*
 int mdg_ctx_last_peaks(mdg_ctx* ctx, size_t spectrum, int which, int32_t* left,
                        int32_t* center, int32_t* right, size_t cap, size_t* count);
 
+/* Diagnostics: the smoothed intensities (MovingAverage::smooth_values,
+ * moving_average.rs:53-83) of spectrum `spectrum` from the last batch run on this
+ * context; n must equal that run's point count, and the run must have used the
+ * moving-average smoother. */
+int mdg_ctx_last_smoothed(mdg_ctx* ctx, size_t spectrum, double* out, size_t n);
+
 /* Lorentzian::superposition_vec: out[i] = sum_j L[j](x[i]) in slice order. */
 int mdg_superposition_vec(mdg_ctx* ctx, const double* x, size_t n, const mdg_lorentzian* L,
                           size_t p, double* out);

@@ -11,6 +11,8 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <string>
+#include <cstdlib>
 #include <new>
 #include <vector>
 
@@ -48,7 +50,9 @@ struct mdg_ctx {
     // workspace arena
     Buffer arena;
     int ws_B = 0, ws_N = 0;
+    Buffer chain;  // k_smooth_chain buffers (allocated on first use)
     int last_B = 0, last_N = 0;  // shape of the last pipeline run
+    bool last_smoothed = false;  // the last run used the moving average
     Workspace w{};
     // staging for the host-pointer API
     Buffer st_x, st_y, st_sb, st_out, st_cnt, st_mse, st_status, st_L, st_sup, st_flag;
@@ -224,6 +228,7 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     c->last_N = a.N;
     hipStream_t st = c->stream;
     const bool ma = s->smoother == MDG_SMOOTH_MOVING_AVERAGE;
+    c->last_smoothed = ma;
     if (ma) {
         w.smooth_ptr = w.smooth;
         w.smooth_stride = a.N;
@@ -235,6 +240,25 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     const int gfit = std::max(1, std::min(64, 4096 / std::max(1, a.B)));
     const int gupd = std::max(1, std::min(16, 1024 / std::max(1, a.B)));
     const int nparts = std::max(1, std::min({1024, (a.N + 255) / 256, std::max(1, 4096 / a.B)}));
+    // chain smoother buffers: raw sums of every pass, scaled outputs of passes
+    // 0..P-2 and one 128-byte progress counter per (spectrum, pass)
+    w.chain_P = 0;
+    w.chain_raw = w.chain_tmp = nullptr;
+    w.chain_flags = nullptr;
+    if (ma) {
+        const char* force = std::getenv("MDG_SMOOTH");
+        const int P = (int)s->smooth_iterations, ws = (int)s->smooth_window;
+        if ((!force || std::string(force) == "chain") && chain_supported(a.B, a.N, P, ws) &&
+            ensure(c->chain, chain_bytes(a.B, a.N, ws, P)) == MDG_OK) {
+            const int64_t L = chain_stride_for(a.N, ws);
+            char* base = (char*)c->chain.p;
+            w.chain_stride = L;
+            w.chain_raw = (double*)base;
+            w.chain_tmp = w.chain_raw + (size_t)P * a.B * L;
+            w.chain_flags = (int32_t*)(base + (size_t)(2 * P - 1) * a.B * L * 8);
+            w.chain_P = P;
+        }
+    }
     {
         StageTimer t(c, ST_PREP);
         launch_prep(a, w, st);
@@ -477,7 +501,7 @@ int mdg_ctx_destroy(mdg_ctx* c) {
             (void)hipEventDestroy(p.b);
         }
         for (auto e : c->free_events) (void)hipEventDestroy(e);
-        for (Buffer* b : {&c->arena, &c->st_x, &c->st_y, &c->st_sb, &c->st_out, &c->st_cnt,
+        for (Buffer* b : {&c->arena, &c->chain, &c->st_x, &c->st_y, &c->st_sb, &c->st_out, &c->st_cnt,
                           &c->st_mse, &c->st_status, &c->st_L, &c->st_sup, &c->st_flag})
             if (b->p) (void)hipFree(b->p);
         if (c->own) (void)hipStreamDestroy(c->own);
@@ -553,6 +577,18 @@ int mdg_ctx_last_peaks(mdg_ctx* c, size_t spectrum, int which, int32_t* left, in
         if (center) HIPCHK(hipMemcpy(center, (which ? w.sel_c : w.det_c) + off, k * 4, hipMemcpyDeviceToHost));
         if (right) HIPCHK(hipMemcpy(right, (which ? w.sel_r : w.det_r) + off, k * 4, hipMemcpyDeviceToHost));
     }
+    return MDG_OK;
+}
+
+int mdg_ctx_last_smoothed(mdg_ctx* c, size_t spectrum, double* out, size_t n) {
+    if (!c || !out) return MDG_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (!c->arena.p || !c->last_smoothed || spectrum >= (size_t)c->last_B ||
+        n != (size_t)c->last_N)
+        return MDG_INVALID_ARGUMENT;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipMemcpy(out, c->w.smooth + spectrum * (size_t)c->last_N, n * 8, hipMemcpyDeviceToHost));
     return MDG_OK;
 }
 

@@ -13,6 +13,7 @@
 
 #include "mdg_common.hpp"
 #include "mdg_kernels.hpp"
+#include "mdg_chain_asm.inc"
 
 #include <cstdlib>
 #include <string>
@@ -268,6 +269,7 @@ __global__ void k_prep(BatchArgs a, Workspace w) {
     w.det_count[s] = 0;
     w.sel_count[s] = 0;
     w.kept_count[s] = 0;
+    for (int p = 0; p < w.chain_P; ++p) w.chain_flags[((size_t)s * w.chain_P + p) * 32] = 0;
 }
 
 // ----------------------------------------------------------------------------------
@@ -344,6 +346,13 @@ __device__ void ma_pass(const double* __restrict__ src, double* __restrict__ dst
 //   N <= q < N+R  : sum -= pop; div = 1/(N+WS-1-q); emit sum*div  (tail)
 // The popped value is always the one pushed WS ticks earlier, in the tail too.
 // ----------------------------------------------------------------------------------
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(unsigned)(b & 0xffffffffll), l);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
 __device__ __forceinline__ double dpp_shr1(double v) {
     const long long b = __double_as_longlong(v);
     int lo = (int)(unsigned)(b & 0xffffffffll), hi = (int)(b >> 32);
@@ -599,6 +608,412 @@ __global__ __launch_bounds__(512) void k_smooth_waves(BatchArgs a, Workspace w, 
     DIAG_FLUSH();
 }
 
+
+// ----------------------------------------------------------------------------------
+// K1d  chain moving average: one workgroup per (spectrum, pass), passes on
+// different CUs (the fast path for small and medium batches).
+//
+// Measured on gfx950 (tools/ubench/issue.hip): a dependent v_add_f64 costs ~4.8
+// cycles, any other instruction of the same wave 3-10 more, an s_load_dwordx16
+// plus its wait almost nothing when it feeds 8 ticks, and one CU issues one
+// 16-byte vector store per ~16 cycles across all its waves. So each pass runs
+// on its own CU as a "chain" wave that issues little besides the reference's two
+// dependent adds per tick (moving_average.rs:69-80, in j = i + R form below),
+// with SGPR operands and one 16-byte store of raw sums per two ticks. A second
+// "helper" wave per workgroup prefetches input blocks into the scalar cache,
+// multiplies the raw sums by the reference's 1/len (moving_average.rs:66-81:
+// 1/len while the buffer grows, 1/ws, then 1/len in the tail), and publishes
+// finished blocks to the next pass (sc1 stores, vmcnt(0), sc1 counter; the
+// consumer polls with sc1 loads -- MI355X_MICROARCH.md, cross-CU hand-offs).
+//
+// Per pass, in j = 0 .. N+R-1:  if j < N: sum += in[j];  if j >= WS: sum -= in[j-WS];
+//                               raw[j] = sum  (= the reference's sum after tick j-R)
+// out[i] = raw[i+R] * (1/len_i).  Blocks of CB ticks; the steady middle runs the
+// generated asm of mdg_chain_asm.inc, the first and last blocks the code below.
+// Every wait has a spin limit after which the spectrum reports MDG_ERR_HIP and
+// all its waves drain (never expected; it bounds a protocol bug).
+// ----------------------------------------------------------------------------------
+constexpr int kChainCB = MDG_CHAIN_CB;
+constexpr int kChainPrefetch = 6;        // input blocks touched into the scalar cache ahead
+constexpr int kChainL2Ahead = 64;        // pass-0 input blocks pulled into L2 ahead
+constexpr unsigned kChainSpins = 1u << 22;
+
+int64_t chain_stride_for(int N, int ws) {
+    const int64_t span = (int64_t)N + ws / 2 + 2 * kChainCB;
+    return (span + 63) / 64 * 64;
+}
+
+size_t chain_bytes(int B, int N, int ws, int passes) {
+    const size_t row = (size_t)chain_stride_for(N, ws) * 8;
+    return row * (size_t)B * (2 * (size_t)passes - 1) + (size_t)B * passes * 128 + 1024;
+}
+
+bool chain_supported(int B, int N, int iters, int ws) {
+    return ws >= 2 && ws <= 8 && iters >= 1 && iters <= 16 && B >= 1 && B * iters <= 2048 &&
+           N >= 4 * kChainCB + 16;
+}
+
+#ifdef MDG_DIAG
+#define DIAGC(k, v) \
+    if (lane == 0) g_diag[((size_t)s * P + p) * 32 + (k)] = (long long)(v)
+#define DIAGC_ADD(k, v) \
+    if (lane == 0) g_diag[((size_t)s * P + p) * 32 + (k)] += (long long)(v)
+#else
+#define DIAGC(k, v)
+#define DIAGC_ADD(k, v)
+#endif
+
+struct ChainCtl {
+    int in_ready;  // input blocks available in the scalar cache (helper -> chain)
+    int raw_done;  // j-blocks whose raw sums are stored (chain -> helper)
+    int abort;
+    int pad;
+};
+
+// wave-uniform copies for "s" asm operands (values computed under a branch the
+// compiler treats as divergent would otherwise land in VGPRs)
+template <typename T>
+__device__ __forceinline__ T* sgpr_ptr(T* p) {
+    const uint64_t v = (uint64_t)(uintptr_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (T*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ int sgpr_int(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+__device__ __forceinline__ unsigned lds_offset(const void* p) {
+    return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+__device__ __forceinline__ double ld_sc1(const double* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int WS>
+__device__ __forceinline__ int chain_steady(const double* in_grp, double* raw, int blk, int cnt,
+                                            int nib, unsigned lds, double& sum, int& stat);
+
+#define MDG_CHAIN_CLOBBERS                                                                  \
+    "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", \
+    "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", \
+    "s66", "s67", "s68", "s69", "s70", "s71", "s72", "s73", "s74", "s75", "s76", "s77", "s78", \
+    "s79", "s80", "s81", "s82", "s83", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", \
+    "s92", "s93", "s94", "s95", "s96", "s97", "s98", "s99", "v0", "v1", "v2", "v3", "v4", "v5",  \
+    "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "scc", \
+    "memory"
+
+#define MDG_CHAIN_STEADY(WSV)                                                                \
+    template <>                                                                              \
+    __device__ __forceinline__ int chain_steady<WSV>(const double* in_grp, double* raw,     \
+                                                     int blk, int cnt, int nib, unsigned lds, \
+                                                     double& sum, int& stat) {              \
+        int blk_out, st;                                                                     \
+        asm volatile(MDG_CHAIN_ASM_##WSV                                                     \
+                     : [sum] "+v"(sum), [blk_out] "=s"(blk_out), [stat] "=s"(st)             \
+                     : [in] "s"(sgpr_ptr(in_grp)), [raw] "s"(sgpr_ptr(raw)),                 \
+                       [blk] "s"(sgpr_int(blk)), [cnt] "s"(sgpr_int(cnt)),                  \
+                       [nib] "s"(sgpr_int(nib)), [lds] "v"(lds)                              \
+                     : MDG_CHAIN_CLOBBERS);                                                  \
+        stat = st;                                                                           \
+        return blk_out;                                                                      \
+    }
+MDG_CHAIN_STEADY(2)
+MDG_CHAIN_STEADY(3)
+MDG_CHAIN_STEADY(4)
+MDG_CHAIN_STEADY(5)
+MDG_CHAIN_STEADY(6)
+MDG_CHAIN_STEADY(7)
+MDG_CHAIN_STEADY(8)
+
+// touch the 64-byte lines of one input block (scalar cache prefetch for the chain)
+__device__ __forceinline__ void chain_touch(const double* p) {
+    asm volatile(
+        "s_load_dwordx16 s[40:55], %0, 0\n s_load_dwordx16 s[40:55], %0, 64\n"
+        "s_load_dwordx16 s[40:55], %0, 128\n s_load_dwordx16 s[40:55], %0, 192\n"
+        "s_load_dwordx16 s[40:55], %0, 256\n s_load_dwordx16 s[40:55], %0, 320\n"
+        "s_load_dwordx16 s[40:55], %0, 384\n s_load_dwordx16 s[40:55], %0, 448\n"
+        "s_load_dwordx16 s[40:55], %0, 512\n s_load_dwordx16 s[40:55], %0, 576\n"
+        "s_load_dwordx16 s[40:55], %0, 640\n s_load_dwordx16 s[40:55], %0, 704\n"
+        "s_waitcnt lgkmcnt(0)\n" ::"s"(sgpr_ptr(p))
+        : "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51",
+          "s52", "s53", "s54", "s55", "memory");
+}
+static_assert(kChainCB * 8 == 768, "chain_touch covers 12 lines of one block");
+
+// load cnt consecutive blocks (this lane's 16 bytes of each) into L2 and wait:
+// one asm statement, so no in-flight load can land in a register the compiler
+// has reused
+__device__ __forceinline__ void chain_l2_pull(const double* p, int cnt) {
+    asm volatile(
+        "v_mov_b64 v[24:25], %0\n"
+        "s_mov_b32 s40, %1\n"
+        "Lpull%=:\n"
+        "global_load_dwordx4 v[20:23], v[24:25], off\n"
+        "v_lshl_add_u64 v[24:25], v[24:25], 0, %2\n"
+        "s_sub_u32 s40, s40, 1\n"
+        "s_cmp_lg_u32 s40, 0\n"
+        "s_cbranch_scc1 Lpull%=\n"
+        "s_waitcnt vmcnt(0)\n" ::"v"(p),
+        "s"(sgpr_int(cnt)), "s"((unsigned long long)(kChainCB * 8))
+        : "v20", "v21", "v22", "v23", "v24", "v25", "s40", "scc", "memory");
+}
+
+template <int WS>
+__global__ __launch_bounds__(192) void k_smooth_chain(BatchArgs a, Workspace w, int P) {
+    // workgroup id -> (spectrum, pass): the P passes of a spectrum share id % 8
+    // (the XCD of round-robin dispatch), so their hand-offs stay in one L2
+    const int id = blockIdx.x;
+    const int x8 = id & 7, j8 = id >> 3;
+    const int p = j8 % P, s = (j8 / P) * 8 + x8;
+    if (s >= a.B) return;
+    if (w.status[s]) return;  // uniform per spectrum
+    constexpr int R = WS / 2;
+    constexpr int CB = kChainCB;
+    const int N = a.N;
+    const int nJ = N + R;
+    const int nJB = (nJ + CB - 1) / CB;     // j-blocks of the chain
+    const int nIB = (N + CB - 1) / CB;      // input blocks
+    const int nOB = nIB;                    // output blocks
+    const int64_t L = w.chain_stride;
+    const double* in = p == 0 ? a.y + (size_t)s * a.y_stride
+                              : w.chain_tmp + ((size_t)(p - 1) * a.B + s) * L;
+    double* out = p == P - 1 ? w.smooth + (size_t)s * N : w.chain_tmp + ((size_t)p * a.B + s) * L;
+    double* raw = w.chain_raw + ((size_t)p * a.B + s) * L;
+    int32_t* my_flag = w.chain_flags + ((size_t)s * w.chain_P + p) * 32;
+    const int32_t* up_flag = p > 0 ? w.chain_flags + ((size_t)s * w.chain_P + p - 1) * 32 : nullptr;
+
+    __shared__ ChainCtl ctl;
+    // scaler staging (one wave): inputs and raw sums of one batch of output blocks
+    __shared__ double sc_in[8 * kChainCB + 24];
+    __shared__ double sc_raw[8 * kChainCB + 24];
+    const int lane = threadIdx.x & 63;
+    if (threadIdx.x == 0) {
+        ctl.in_ready = 0;
+        ctl.raw_done = 0;
+        ctl.abort = 0;
+    }
+    __syncthreads();
+    asm volatile("s_dcache_inv" ::: "memory");
+    // LDS control words: workgroup-scope relaxed atomics lower to plain ds_ ops
+#define CTL_LD(f) __hip_atomic_load(&ctl.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+#define CTL_ST(f, v) __hip_atomic_store(&ctl.f, (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+
+    if (threadIdx.x < 64) {
+        // ---------------------------- chain wave ----------------------------
+        double sum = 0.0;  // T::zero()
+        // first steady block: 1; steady blocks k need CB*(k+1) + 8 <= N (group prefetch)
+        const int kA = 1;
+        const int kB = max(kA, (N - 8) / CB);
+        int avail = 0;
+        auto wait_in = [&](int need) -> bool {
+            unsigned spins = 0;
+            while (avail < need) {
+                avail = CTL_LD(in_ready);
+                if (avail >= need) break;
+                if (CTL_LD(abort)) return false;
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > kChainSpins) return false;
+            }
+            return true;
+        };
+        // generic block: inputs gathered lane-parallel (coherent sc1 loads), then the
+        // sequential ticks read them back with readlane
+        double prev_lo = 0.0, prev_hi = 0.0;  // previous block's inputs (for pops)
+        auto generic = [&](int k) -> bool {
+            if (!wait_in(min(k + 2, nIB))) return false;
+            const int j0 = k * CB;
+            const int ja = j0 + lane, jb = j0 + 64 + lane;
+            const double v_lo = ja < N ? ld_sc1(in + ja) : 0.0;
+            const double v_hi = (lane < CB - 64 && jb < N) ? ld_sc1(in + jb) : 0.0;
+            const int jend = min(j0 + CB, nJ);
+            for (int j = j0; j < jend; ++j) {
+                const int e = j - j0;
+                if (j < N) sum += readlane_f64(e < 64 ? v_lo : v_hi, e < 64 ? e : e - 64);
+                if (j >= WS) {
+                    const int q = e - WS;  // pop index relative to the block
+                    double pv;
+                    if (q >= 0) pv = readlane_f64(q < 64 ? v_lo : v_hi, q < 64 ? q : q - 64);
+                    else pv = readlane_f64(CB + q < 64 ? prev_lo : prev_hi,
+                                           CB + q < 64 ? CB + q : CB + q - 64);
+                    sum -= pv;
+                }
+                raw[j] = sum;
+            }
+            prev_lo = v_lo;
+            prev_hi = v_hi;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            CTL_ST(raw_done, k + 1);
+            return true;
+        };
+        bool ok = true;
+        DIAGC(0, __builtin_amdgcn_s_memtime());
+        for (int k = 0; ok && k < kA; ++k) ok = generic(k);
+        DIAGC(1, __builtin_amdgcn_s_memtime());
+        if (ok && kB > kA) {
+            int stat = 0;
+            const int done = chain_steady<WS>(in + (size_t)kA * CB - 8, raw + (size_t)kA * CB, kA,
+                                              kB - kA, nIB,
+                                              lds_offset(&ctl), sum, stat);
+            ok = stat == 0 && done == kB;
+            if (ok) {
+                CTL_ST(raw_done, kB);
+                // the generic tail pops from the last steady block: reload it
+                const int j0 = (kB - 1) * CB;
+                prev_lo = ld_sc1(in + j0 + lane);
+                prev_hi = lane < CB - 64 ? ld_sc1(in + j0 + 64 + lane) : 0.0;
+            }
+        }
+        DIAGC(2, __builtin_amdgcn_s_memtime());
+        DIAGC(4, kB - kA);
+        for (int k = kB; ok && k < nJB; ++k) ok = generic(k);
+        DIAGC(3, __builtin_amdgcn_s_memtime());
+        if (!ok) CTL_ST(abort, 1);
+    } else if (threadIdx.x < 128) {
+        // ---------------------------- feeder wave ----------------------------
+        // polls the upstream pass, touches newly available input blocks into the
+        // scalar cache (kChainPrefetch blocks ahead of the chain) and publishes them
+        int pf = 0;
+        int up = p == 0 ? nIB : 0;
+        int l2 = 0;  // next input block pulled into L2
+        unsigned idle = 0;
+        bool ok = true;
+        DIAGC(8, __builtin_amdgcn_s_memtime());
+        while (pf < nIB) {
+            if (CTL_LD(abort)) {
+                ok = false;
+                break;
+            }
+            const int rd = CTL_LD(raw_done);
+            // learn what the upstream pass has published (pass 0: everything)
+            if (p > 0 && up < min(nIB, rd + kChainL2Ahead))
+                up = __hip_atomic_load(const_cast<int32_t*>(up_flag), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            // pull published full input blocks into L2 (16 per wait), so the
+            // scalar-cache touches below hit L2 instead of HBM / the MALL
+            const int l2lim = min(min(N / CB, up), rd + kChainL2Ahead);
+            bool prog = false;
+            if (l2lim - l2 >= 16 || (l2lim > l2 && (l2lim == N / CB || l2 < pf + 4))) {
+                const int cnt = min(16, l2lim - l2);
+                if (lane < CB / 2) chain_l2_pull(in + (size_t)l2 * CB + 2 * lane, cnt);
+                l2 += cnt;
+                prog = true;
+            }
+            const int hi = min(min(up, nIB), rd + kChainPrefetch);
+            for (; pf < hi; ++pf) {
+                if ((pf + 1) * CB <= N) chain_touch(in + (size_t)pf * CB);
+                CTL_ST(in_ready, pf + 1);
+                prog = true;
+            }
+            if (prog) {
+                idle = 0;
+                DIAGC_ADD(10, 1);
+                continue;
+            }
+            DIAGC_ADD(11, 1);
+            __builtin_amdgcn_s_sleep(1);
+            if (++idle > kChainSpins) {
+                ok = false;
+                break;
+            }
+        }
+        DIAGC(9, __builtin_amdgcn_s_memtime());
+        if (!ok) CTL_ST(abort, 1);
+    } else {
+        // ---------------------------- scaler wave ----------------------------
+        // scales every finished raw block by 1/len and publishes them in one batch
+        // (sc1 stores, vmcnt(0), sc1 counter: the downstream pass polls it)
+        constexpr int MAXB = 8;                   // blocks per batch
+        const int kA = 1, kB = max(kA, (N - 8) / CB);  // steady j-blocks (as the chain)
+        int sc = 0;
+        unsigned idle = 0;
+        bool ok = true;
+        DIAGC(16, __builtin_amdgcn_s_memtime());
+        while (sc < nOB) {
+            if (CTL_LD(abort)) {
+                ok = false;
+                break;
+            }
+            const int rd = CTL_LD(raw_done);
+            // output block m needs raw j-blocks <= m+1: finished once raw_done >= m+2
+            const int ready = rd >= nJB ? nOB : min(nOB, max(0, rd - 1));
+            if (ready > sc) {
+                const int hi = min(ready, sc + MAXB);
+                const int i0 = sc * CB, i1 = min(hi * CB, N);
+                // raw sums j = i + R of the batch, staged in LDS: groups of 8 ticks in
+                // steady j-blocks [kA, kB) hold only their last sum (the checkpoint), so
+                // one lane per group replays it from the previous checkpoint with the
+                // chain's own two operations per tick; all HBM traffic is coalesced
+                const int g0 = (i0 + R) / 8, g1 = (i1 - 1 + R) / 8 + 1;
+                const int base = 8 * g0 - 8;               // LDS index = j - base
+                const int span = 8 * (g1 - g0) + 8;
+                {
+                    constexpr int SLOTS = (8 * kChainCB + 24 + 63) / 64;
+                    double vin[SLOTS], vraw[SLOTS];
+#pragma unroll
+                    for (int k = 0; k < SLOTS; ++k) {  // all loads in flight together
+                        const int e = 64 * k + lane, j = base + e;
+                        vin[k] = (e < span && j >= 0 && j < N) ? ld_sc1(in + j) : 0.0;
+                        vraw[k] = (e < span && j >= 0 && j < nJ) ? ld_sc1(raw + j) : 0.0;
+                    }
+#pragma unroll
+                    for (int k = 0; k < SLOTS; ++k) {
+                        const int e = 64 * k + lane;
+                        if (e < span) {
+                            sc_in[e] = vin[k];
+                            sc_raw[e] = vraw[k];
+                        }
+                    }
+                }
+                for (int g = g0 + lane; g < g1; g += 64) {
+                    const int blk = 8 * g / CB;
+                    if (blk >= kA && blk < kB) {
+                        const int e0 = 8 * g - base;
+                        double sum_g = sc_raw[e0 - 1];
+                        double rv[8];
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) {
+                            sum_g += sc_in[e0 + u];
+                            sum_g -= sc_in[e0 + u - WS];
+                            rv[u] = sum_g;
+                        }
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) sc_raw[e0 + u] = rv[u];
+                    }
+                }
+                for (int i = i0 + lane; i < i1; i += 64) {
+                    // len of the circular buffer after tick i (moving_average.rs:66-81)
+                    const int len = i < N - R ? min(i + R + 1, WS) : WS - 1 - (i - (N - R));
+                    __hip_atomic_store(out + i, sc_raw[i + R - base] * (1.0 / (double)len),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (lane == 0) __hip_atomic_store(my_flag, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                DIAGC_ADD(18, 1);
+                sc = hi;
+                idle = 0;
+                continue;
+            }
+            DIAGC_ADD(19, 1);
+            __builtin_amdgcn_s_sleep(1);
+            if (++idle > kChainSpins) {
+                ok = false;
+                break;
+            }
+        }
+        DIAGC(17, __builtin_amdgcn_s_memtime());
+        if (!ok) {
+            CTL_ST(abort, 1);
+            if (lane == 0) {
+                w.status[s] = MDG_ERR_HIP;
+                // release every downstream pass so all waves drain
+                __hip_atomic_store(my_flag, 1 << 30, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+#undef CTL_LD
+#undef CTL_ST
+}
+
 __global__ void k_smooth(BatchArgs a, Workspace w, int iters, int ws) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= a.B) return;
@@ -726,13 +1141,6 @@ __device__ __forceinline__ double score_min_sum(const double* __restrict__ sm, i
     for (int k = l; k <= c; ++k) left += fabs(dsd(sm, k));
     for (int k = c; k <= r; ++k) right += fabs(dsd(sm, k));
     return fmin(left, right);
-}
-
-__device__ __forceinline__ double readlane_f64(double v, int l) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readlane((int)(unsigned)(b & 0xffffffffll), l);
-    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
-    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
 }
 
 // Left fold over the signal-free-region scores peaks[..left] ++ peaks[right..P]
@@ -1246,12 +1654,30 @@ static void launch_pipe(const BatchArgs& a, const Workspace& w, int iters, hipSt
     hipLaunchKernelGGL(k_smooth_pipe<WS>, dim3(cdiv(a.B, spw)), dim3(64), 0, st, a, w, iters, spw);
 }
 
+template <int WS>
+static void launch_chain(const BatchArgs& a, const Workspace& w, int iters, hipStream_t st) {
+    const unsigned grid = 8u * (unsigned)iters * cdiv(a.B, 8);
+    hipLaunchKernelGGL(k_smooth_chain<WS>, dim3(grid), dim3(192), 0, st, a, w, iters);
+}
 void launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int ws, hipStream_t st) {
-    // lane-pipelined kernel whenever the window fits the register FIFO and the
-    // spectrum is longer than the window; the one-lane-per-spectrum kernel otherwise
-    // measured (bench stages): lane-pipelined 3.05 ms vs wave-per-pass 3.3 ms at B = 1;
-    // at B = 256 wave-per-pass 3.0 ms vs 4.7 ms (21 spectra per lane-pipelined wave)
+    // chain kernel (one CU per pass) for windows <= 8 and batches <= 512; then
+    // wave-per-pass (B > 21) or lane-pipelined (window fits the register FIFO);
+    // the one-lane-per-spectrum kernel otherwise. MDG_SMOOTH = chain | waves |
+    // pipe | generic forces one (tests); an unsupported shape falls through.
     const char* force = std::getenv("MDG_SMOOTH");
+    const bool chain = force ? std::string(force) == "chain" : true;
+    if (chain && w.chain_P >= iters && chain_supported(a.B, a.N, iters, ws)) {
+        switch (ws) {
+            case 2: return launch_chain<2>(a, w, iters, st);
+            case 3: return launch_chain<3>(a, w, iters, st);
+            case 4: return launch_chain<4>(a, w, iters, st);
+            case 5: return launch_chain<5>(a, w, iters, st);
+            case 6: return launch_chain<6>(a, w, iters, st);
+            case 7: return launch_chain<7>(a, w, iters, st);
+            case 8: return launch_chain<8>(a, w, iters, st);
+            default: break;
+        }
+    }
     const bool waves = force ? std::string(force) == "waves" : a.B > 21;
     if (waves && iters >= 1 && iters <= 8 && a.N > ws + 1) {
         switch (ws) {
@@ -1267,7 +1693,8 @@ void launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int ws, hi
             default: break;
         }
     }
-    if (iters >= 1 && iters <= 32 && a.N > ws + 1) {
+    const bool pipe = !force || std::string(force) == "pipe";
+    if (pipe && iters >= 1 && iters <= 32 && a.N > ws + 1) {
         switch (ws) {
             case 2: return launch_pipe<2>(a, w, iters, st);
             case 3: return launch_pipe<3>(a, w, iters, st);

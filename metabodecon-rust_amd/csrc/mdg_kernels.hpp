@@ -73,7 +73,18 @@ struct Workspace {
     int32_t* x_ok;            // B: axis inside the fast-division range
     int32_t* unsafe;          // B x 2: ping-pong count of fit params outside it
     int32_t* unsafe_kept;     // B: same for the retained Lorentzians
+    // k_smooth_chain (allocated on first use; null otherwise)
+    double* chain_raw;        // P x B x chain_stride: raw running sums of every pass
+    double* chain_tmp;        // (P-1) x B x chain_stride: scaled outputs of passes 0..P-2
+    int32_t* chain_flags;     // B x P x 32: published output blocks of (s, p) (own 128-B line)
+    int64_t chain_stride;
+    int chain_P;              // passes the chain buffers hold (0 = not allocated)
 };
+
+// Bytes of the k_smooth_chain buffers for (B, N, passes) and their row stride.
+int64_t chain_stride_for(int N, int ws);
+size_t chain_bytes(int B, int N, int ws, int passes);
+bool chain_supported(int B, int N, int iters, int ws);
 
 void launch_prep(const BatchArgs& a, const Workspace& w, hipStream_t st);
 void launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int ws, hipStream_t st);

@@ -43,7 +43,7 @@ EXPORTS = [
     "mdg_ctx_set_profiling", "mdg_ctx_stage_times", "mdg_ctx_reset_stage_times",
     "mdg_deconvolute", "mdg_deconvolute_batch", "mdg_deconvolute_batch_device",
     "mdg_superposition_vec", "mdg_superposition_vec_device", "mdg_synth_batch_device",
-    "mdg_ctx_last_peaks",
+    "mdg_ctx_last_peaks", "mdg_ctx_last_smoothed",
 ]
 
 
@@ -142,6 +142,7 @@ def _declare(L):
     L.mdg_superposition_vec.argtypes = [_vp, _dp, _sz, _dp, _sz, _dp]
     L.mdg_superposition_vec_device.argtypes = [_vp, _vp, _sz, _vp, _sz, _vp]
     L.mdg_ctx_last_peaks.argtypes = [_vp, _sz, ctypes.c_int, _i32p, _i32p, _i32p, _sz, _szp]
+    L.mdg_ctx_last_smoothed.argtypes = [_vp, _sz, _dp, _sz]
     L.mdg_synth_batch_device.argtypes = [_vp, _sz, _sz, ctypes.c_double, ctypes.c_double,
                                          ctypes.c_uint64, _sz, ctypes.c_double, ctypes.c_double,
                                          ctypes.c_double, _vp, _vp]
@@ -210,6 +211,14 @@ class Context:
         n = np.zeros(N_STAGES, dtype=np.uint64)
         lib().mdg_ctx_stage_times(self.handle, ptr(ms), ptr(n, _u64p), N_STAGES)
         return {STAGE_NAMES[i]: (float(ms[i]), int(n[i])) for i in range(N_STAGES)}
+
+    def last_smoothed(self, spectrum: int, n: int) -> np.ndarray:
+        """Smoothed intensities of `spectrum` from the last batch run (diagnostic)."""
+        out = np.empty(n, dtype=np.float64)
+        st = lib().mdg_ctx_last_smoothed(self.handle, spectrum, ptr(out), n)
+        if st:
+            raise RuntimeError(strerror(st))
+        return out
 
     def last_peaks(self, spectrum: int, which: str = "selected") -> np.ndarray:
         """(count, 3) int32 (left, center, right) of the last batch run."""

@@ -204,7 +204,7 @@ def test_small_and_odd_shapes(ctx):
             assert abs(mse[0] - o.mse) <= MSE_RTOL * abs(o.mse)
 
 
-@pytest.mark.parametrize("path", ["waves", "pipe"])
+@pytest.mark.parametrize("path", ["chain", "waves", "pipe"])
 @pytest.mark.parametrize("it,ws", [(1, 2), (2, 4), (3, 3), (5, 7), (8, 5), (10, 3), (3, 31),
                                    (4, 9), (2, 11)])
 def test_smoother_settings_sweep(ctx, it, ws, path, monkeypatch):
@@ -273,3 +273,48 @@ def test_stage_profiling(ctx):
     t = ctx.stage_times()
     ctx.set_profiling(False)
     assert t["fit_superposition"][1] == 10 and t["mse_superposition"][0] > 0
+
+
+def _smooth_rows(ctx, ys, it, ws):
+    """Run the batch (any final status) and read back every smoothed row."""
+    xs = np.linspace(14.8, -5.2, ys.shape[1])
+    st = oracle.make_settings(smooth_iterations=it, smooth_window=ws)
+    gpu_batch(ctx, xs, ys, [(11.8, -2.2)], st)
+    return [ctx.last_smoothed(s, ys.shape[1]) for s in range(ys.shape[0])]
+
+
+@pytest.mark.parametrize("path", ["chain", "pipe", "waves", "generic"])
+def test_smoothed_rows_bit_exact(ctx, path, monkeypatch):
+    """Smoothed intensities of every kernel equal the oracle's moving average bit for
+    bit (moving_average.rs:53-83), on real spectra and a synthetic 128k one."""
+    monkeypatch.setenv("MDG_SMOOTH", path)
+    ys = np.stack([load_case(f"blood_{i:02d}")[1] for i in (1, 7, 16)] + [synth_spectrum(0)[1]])
+    for s, row in enumerate(_smooth_rows(ctx, ys, 3, 3)):
+        assert np.array_equal(row, oracle.moving_average(ys[s], 3, 3)), s
+
+
+@pytest.mark.parametrize("ws", [2, 3, 4, 5, 6, 7, 8])
+def test_chain_smoother_shapes(ctx, ws, monkeypatch):
+    """k_smooth_chain at the edges of its range: short spectra (generic head/tail
+    blocks only), lengths off the block and group grids, up to 16 passes, batches
+    that do not fill the 8-spectrum placement groups."""
+    monkeypatch.setenv("MDG_SMOOTH", "chain")
+    rng = np.random.default_rng(ws)
+    for n, b, it in [(400, 1, 1), (401, 3, 2), (487, 2, 3), (577, 9, 5), (1000, 1, 16),
+                     (4101, 13, 3), (20000, 2, 4)]:
+        t = np.linspace(0, 1, n)
+        ys = rng.normal(0, 1, (b, n)) * 10.0 ** rng.integers(0, 6, (b, 1)) + 1e4 * np.sin(
+            40 * t)[None, :]
+        for s, row in enumerate(_smooth_rows(ctx, ys, it, ws)):
+            assert np.array_equal(row, oracle.moving_average(ys[s], it, ws)), (n, b, it, s)
+
+
+def test_chain_smoother_repeated_launches(ctx, monkeypatch):
+    """Back-to-back launches rewrite the chain's hand-off buffers: a stale line in
+    any cache would show as a mismatch in the second and third runs."""
+    monkeypatch.setenv("MDG_SMOOTH", "chain")
+    rng = np.random.default_rng(7)
+    for rep in range(3):
+        ys = rng.normal(0, 1, (5, 131072)) * 1e3 + rep
+        for s, row in enumerate(_smooth_rows(ctx, ys, 3, 3)):
+            assert np.array_equal(row, oracle.moving_average(ys[s], 3, 3)), (rep, s)

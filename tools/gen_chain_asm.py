@@ -1,0 +1,153 @@
+"""Generate metabodecon-rust_amd/csrc/mdg_chain_asm.inc (run after editing).
+
+The steady-state loop of the chain wave of k_smooth_chain (mdg_kernels.hip),
+one asm string per window size WS in 2..8. It runs the reference running sum
+(moving_average.rs:69-80: `sum += v[j]`, then `sum -= popped`) on wave-uniform
+SGPR operands, one block of CB = 96 ticks per trip:
+
+  * operands: groups of 8 doubles of the pass input, s_load_dwordx16 into three
+    rotating SGPR buffers (prev / cur / next); each group prefetches the next
+    and waits for it at its end (lgkmcnt(0): SMEM returns out of order);
+  * sums rotate through NV = 8 VGPR pairs v[0:15]; tick t writes pair t%NV; only
+    the last sum of each group of 8 ticks is stored (see block_body);
+  * per block: wait (LDS, cached) until the helper wave has published the input
+    block the prefetch reaches; after the block, s_waitcnt vmcnt(GROUPS) proves
+    the previous block's stores complete, then raw_done is published in LDS.
+
+Fixed registers: s[40:87] operand buffers, s[88:99] loop state, v[0:18].
+Operand %[in] is the address of the group before the first block (in + CB*k0 - 8).
+"""
+import os
+
+CB = 96              # ticks per block
+GROUPS = CB // 8     # 12 (multiple of 3: buffer rotation period)
+BUF = [40, 56, 72]   # SGPR base of the three 8-double buffers
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "metabodecon-rust_amd", "csrc", "mdg_chain_asm.inc")
+
+# loop state registers
+IN, RAW = "s[88:89]", "s[90:91]"
+IN_LO, IN_HI, RAW_LO, RAW_HI = "s88", "s89", "s90", "s91"
+BLK, AVAIL, NIB, GUARD, CNT, TMP, NEED, STAT = "s92", "s93", "s94", "s95", "s96", "s97", "s98", "s99"
+NV = int(os.environ.get("CHAIN_NV", "8"))          # rotating sum pairs (4 or 8)
+V = [f"v[{2 * k}:{2 * k + 1}]" for k in range(NV)]
+PAIR = {k: f"v[{2 * k}:{2 * k + 3}]" for k in range(0, NV, 2)}
+LDSA, VT, VZ = "v16", "v17", "v18"
+GUARD_SPINS = 1 << 22  # ~0.3 s of s_sleep 1 before the wave gives up (never expected)
+
+
+def sreg(buf, e):
+    b = BUF[buf] + 2 * e
+    return f"s[{b}:{b + 1}]"
+
+
+def block_body(ws):
+    """12 groups of 8 ticks; after each group only its LAST running sum (the
+    checkpoint raw[8G+7]) is stored, one 8-byte store placed after the first add
+    of the next group's second tick. The scaler wave recomputes the other seven
+    sums of the group from the previous checkpoint with the same two operations
+    per tick, so the stored data is 1/8 of the ticks."""
+    L = []
+    for q in range(GROUPS):
+        prev, cur, nxt = q % 3, (q + 1) % 3, (q + 2) % 3
+        # IN points one group (64 B) before the block: group q+1 starts at 64*(q+2)
+        if not os.environ.get("CHAIN_NOLOAD"):  # diagnostic variants only (wrong results)
+            L.append(f"s_load_dwordx16 s[{BUF[nxt]}:{BUF[nxt] + 15}], {IN}, {64 * (q + 2)}")
+        for u in range(8):
+            t = 8 * q + u
+            dst, src = V[t % NV], V[(t - 1) % NV]
+            L.append(f"v_add_f64 {dst}, {src}, {sreg(cur, u)}")
+            if u == 1 and q >= 1 and not os.environ.get("CHAIN_NOSTORE"):
+                c = 8 * q - 1  # checkpoint of the previous group, still in its register
+                L.append(f"global_store_dwordx2 {VZ}, {V[c % NV]}, {RAW} offset:{8 * c}")
+            pop = sreg(cur, u - ws) if u >= ws else sreg(prev, 8 + u - ws)
+            L.append(f"v_add_f64 {dst}, {dst}, -{pop}")
+        L.append("s_waitcnt lgkmcnt(0)")
+    if not os.environ.get("CHAIN_NOSTORE"):
+        L.append(f"global_store_dwordx2 {VZ}, {V[(CB - 1) % NV]}, {RAW} offset:{8 * (CB - 1)}")
+    return L
+
+
+def program(ws):
+    L = []
+    # entry: copy operands into the fixed registers, load prev/cur of the first group
+    L += [
+        "s_mov_b64 s[88:89], %[in]",
+        "s_mov_b64 s[90:91], %[raw]",
+        "s_mov_b32 s92, %[blk]",
+        "s_mov_b32 s96, %[cnt]",
+        "s_mov_b32 s94, %[nib]",
+        "s_mov_b32 s93, 0",
+        "s_mov_b32 s99, 0",
+        f"v_mov_b32 {LDSA}, %[lds]",
+        f"v_mov_b32 {VZ}, 0",
+        f"v_mov_b64 {V[NV - 1]}, %[sum]",
+        f"s_load_dwordx16 s[{BUF[0]}:{BUF[0] + 15}], {IN}, 0",
+        f"s_load_dwordx16 s[{BUF[1]}:{BUF[1] + 15}], {IN}, 64",
+        "s_waitcnt lgkmcnt(0)",
+        "Lblk%=:",
+        # need = min(blk + 2, nib); re-read the helper's in_ready only when the cached value is short
+        f"s_add_u32 {NEED}, {BLK}, 2",
+        f"s_min_i32 {NEED}, {NEED}, {NIB}",
+        f"s_cmp_ge_i32 {AVAIL}, {NEED}",
+        "s_cbranch_scc1 Lgo%=",
+        f"s_mov_b32 {GUARD}, {GUARD_SPINS}",
+        "Lwait%=:",
+        f"ds_read_b32 {VT}, {LDSA}",
+        "s_waitcnt lgkmcnt(0)",
+        f"v_readfirstlane_b32 {AVAIL}, {VT}",
+        f"s_cmp_ge_i32 {AVAIL}, {NEED}",
+        "s_cbranch_scc1 Lgo%=",
+        f"ds_read_b32 {VT}, {LDSA} offset:8",   # abort flag set by the helper
+        "s_waitcnt lgkmcnt(0)",
+        f"v_readfirstlane_b32 {TMP}, {VT}",
+        f"s_cmp_lg_u32 {TMP}, 0",
+        "s_cbranch_scc1 Lto%=",
+        "s_sleep 1",
+        f"s_sub_u32 {GUARD}, {GUARD}, 1",
+        f"s_cmp_lg_u32 {GUARD}, 0",
+        "s_cbranch_scc1 Lwait%=",
+        "Lto%=:",
+        f"s_mov_b32 {STAT}, 1",
+        "s_branch Ldone%=",
+        "Lgo%=:",
+    ]
+    L += block_body(ws)
+    L += [
+        f"s_add_u32 {IN_LO}, {IN_LO}, {8 * CB}",
+        f"s_addc_u32 {IN_HI}, {IN_HI}, 0",
+        f"s_add_u32 {RAW_LO}, {RAW_LO}, {8 * CB}",
+        f"s_addc_u32 {RAW_HI}, {RAW_HI}, 0",
+        f"s_waitcnt vmcnt({GROUPS})",
+        f"v_mov_b32 {VT}, {BLK}",
+        f"ds_write_b32 {LDSA}, {VT} offset:4",   # raw_done = blocks < blk complete
+        f"s_add_u32 {BLK}, {BLK}, 1",
+        f"s_sub_u32 {CNT}, {CNT}, 1",
+        f"s_cmp_lg_u32 {CNT}, 0",
+        "s_cbranch_scc1 Lblk%=",
+        "Ldone%=:",
+        "s_waitcnt vmcnt(0)",
+        f"v_mov_b64 %[sum], {V[(CB - 1) % NV]}",
+        "s_mov_b32 %[blk_out], s92",
+        "s_mov_b32 %[stat], s99",
+    ]
+    return L
+
+
+def main():
+    lines = ["// Generated by tools/gen_chain_asm.py -- do not edit.",
+             f"// Steady loop of the k_smooth_chain chain wave, CB = {CB} ticks per block.",
+             f"#define MDG_CHAIN_CB {CB}", ""]
+    for ws in range(2, 9):
+        body = program(ws)
+        lines.append(f"#define MDG_CHAIN_ASM_{ws} \\")
+        for ins in body:
+            lines.append(f'    "{ins}\\n" \\')
+        lines.append("")
+    with open(OUT, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    print("wrote", OUT, "lines per WS:", len(program(3)))
+
+
+if __name__ == "__main__":
+    main()
