@@ -281,6 +281,7 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     }
     {
         StageTimer t(c, ST_SELECT);
+        if (!det_only) launch_scores(a, w, st);
         launch_select(a, w, det_only, s->threshold, st);
     }
     {

@@ -71,24 +71,51 @@ __device__ __forceinline__ double lorentz_t(double x, double sfhw, double hw2, d
 typedef const __attribute__((address_space(4))) double* const_f64_ptr;
 
 template <bool FAST>
+__device__ __forceinline__ void sup_group(double x, double& acc, const double (&c)[12], double (&n)[12],
+                                          const_f64_ptr next, bool load_next) {
+    const double e0 = lorentz_t<FAST>(x, c[0], c[1], c[2]);
+    // the wait for c precedes e0; the next group's loads go out only after it
+    __builtin_amdgcn_sched_barrier(0);
+    if (load_next) {
+#pragma unroll
+        for (int k = 0; k < 12; ++k) n[k] = next[k];
+    }
+    const double e1 = lorentz_t<FAST>(x, c[3], c[4], c[5]);
+    const double e2 = lorentz_t<FAST>(x, c[6], c[7], c[8]);
+    const double e3 = lorentz_t<FAST>(x, c[9], c[10], c[11]);
+    acc += e0;
+    acc += e1;
+    acc += e2;
+    acc += e3;
+}
+
+template <bool FAST>
 __device__ __forceinline__ double superpose_t(double x, const double* __restrict__ params_g, int P) {
     // Parameters are read-only for the whole launch: address space 4 (constant)
     // lets the backend issue s_load_dwordx* and feed SGPR operands to the VALU.
+    // Groups of 4 Lorentzians alternate between two SGPR buffers (A, B): each
+    // group's loads for the group after it are issued behind the group's first
+    // evaluation, so their latency hides behind the rest of the group.
     const const_f64_ptr params = (const_f64_ptr)(params_g);
     double acc = -0.0;
-    int j = 0;
-    for (; j + 4 <= P; j += 4) {
-        const_f64_ptr L = params + 3 * j;
-        const double e0 = lorentz_t<FAST>(x, L[0], L[1], L[2]);
-        const double e1 = lorentz_t<FAST>(x, L[3], L[4], L[5]);
-        const double e2 = lorentz_t<FAST>(x, L[6], L[7], L[8]);
-        const double e3 = lorentz_t<FAST>(x, L[9], L[10], L[11]);
-        acc += e0;
-        acc += e1;
-        acc += e2;
-        acc += e3;
+    const int G = P / 4;  // full groups
+    int g = 0;
+    if (G > 0) {
+        double A[12], B[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) A[k] = params[k];
+        for (; g + 2 < G; g += 2) {
+            sup_group<FAST>(x, acc, A, B, params + 12 * (g + 1), true);
+            sup_group<FAST>(x, acc, B, A, params + 12 * (g + 2), true);
+        }
+        if (g + 1 < G) {
+            sup_group<FAST>(x, acc, A, B, params + 12 * (g + 1), true);
+            sup_group<FAST>(x, acc, B, A, params, false);
+        } else {
+            sup_group<FAST>(x, acc, A, B, params, false);
+        }
     }
-    for (; j < P; ++j) {
+    for (int j = 4 * G; j < P; ++j) {
         const_f64_ptr L = params + 3 * j;
         acc += lorentz_t<FAST>(x, L[0], L[1], L[2]);
     }
@@ -104,6 +131,9 @@ __device__ __forceinline__ double superpose(double x, const double* __restrict__
 // cycle sums of kernel phases, written to a side buffer only. Empty otherwise.
 #ifdef MDG_DIAG
 __device__ long long* g_diag = nullptr;
+#define KSTAMP(slot)                                                           \
+    if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0 && g_diag)      \
+        g_diag[512 + (slot)] = (long long)__builtin_amdgcn_s_memtime()
 #define DIAG_DECL unsigned long long _d_t = __builtin_amdgcn_s_memtime(); unsigned long long _d_acc[8] = {0};
 #define DIAG_STAMP(i)                                                       \
     do {                                                                    \
@@ -120,6 +150,7 @@ __device__ long long* g_diag = nullptr;
                 g_diag[(blockIdx.x * 16 + (threadIdx.x >> 6)) * 8 + _i] = (long long)_d_acc[_i]; \
     } while (0)
 #else
+#define KSTAMP(slot)
 #define DIAG_DECL
 #define DIAG_STAMP(i)
 #define DIAG_FLUSH()
@@ -1136,45 +1167,330 @@ __global__ __launch_bounds__(BS) void k_peaks(BatchArgs a, Workspace w, int dete
 // ----------------------------------------------------------------------------------
 // K4  noise-score selection (noise_score_filter.rs:91-138, scorer.rs:65-75, common.rs:26-40)
 // ----------------------------------------------------------------------------------
-__device__ __forceinline__ double score_min_sum(const double* __restrict__ sm, int l, int c, int r) {
-    double left = -0.0, right = -0.0;
-    for (int k = l; k <= c; ++k) left += fabs(dsd(sm, k));
-    for (int k = c; k <= r; ++k) right += fabs(dsd(sm, k));
-    return fmin(left, right);
+
+// ScorerMinimumSum::score_peak (scorer.rs:65-75) for every detected peak, one
+// thread per peak over many workgroups: min(sum |D[l..=c]|, sum |D[c..=r]|) with
+// D[k] = (y[k-1] - 2 y[k]) + y[k+1], both sums left folds in k order. The
+// smoothed values of a chunk of 8 ticks are loaded together (clamped addresses),
+// so a peak costs one memory latency per 8 ticks instead of one per tick.
+__global__ void k_scores(BatchArgs a, Workspace w) {
+    const int s = blockIdx.y;
+    if (w.status[s]) return;
+    const int P = w.det_count[s];
+    const size_t base = (size_t)s * w.capD;
+    const double* __restrict__ sm = w.smooth_ptr + (size_t)s * w.smooth_stride;
+    const int N = a.N;
+    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
+        const int l = w.det_l[base + p], c = w.det_c[base + p], r = w.det_r[base + p];
+        double left = -0.0, right = -0.0;
+        for (int k0 = l; k0 <= r; k0 += 8) {
+            double y[10];  // y[k0-1 .. k0+8]
+#pragma unroll
+            for (int u = 0; u < 10; ++u) y[u] = sm[min(max(k0 - 1 + u, 0), N - 1)];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int k = k0 + u;
+                if (k <= r) {
+                    const double d = fabs((y[u] - 2.0 * y[u + 1]) + y[u + 2]);
+                    if (k <= c) left += d;
+                    if (k >= c) right += d;
+                }
+            }
+        }
+        w.scores[base + p] = fmin(left, right);
+    }
 }
 
 // Left fold over the signal-free-region scores peaks[..left] ++ peaks[right..P]
-// in the reference's order (noise_score_filter.rs:129-138), by ONE wave: lanes
-// load 64 consecutive terms (coalesced, one block ahead), then the running sum
-// consumes them lane by lane through readlane -> SGPR operands. The only serial
-// part is the chain of dependent adds the reference itself performs.
-template <bool SQUARE>
-__device__ double sfr_fold(const double* __restrict__ scores, int left, int right, int P,
-                           double mean) {
-    const int lane = threadIdx.x & 63;
-    const int n = left + (P - right);
-    auto term = [&](int k) -> double {
-        if (k >= n) return 0.0;
-        const int idx = k < left ? k : right + (k - left);
-        const double v = scores[idx];
-        if (SQUARE) {
-            const double d = v - mean;
-            return d * d;
-        }
-        return v;
-    };
-    double acc = -0.0;
-    double cur = term(lane);
-    for (int base = 0; base < n; base += 64) {
-        const double nxt = term(base + 64 + lane);  // prefetch the next block
-        const int cnt = min(64, n - base);
-        if (cnt == 64) {
-#pragma unroll
-            for (int l = 0; l < 64; ++l) acc += readlane_f64(cur, l);
-        } else {
-            for (int l = 0; l < cnt; ++l) acc += readlane_f64(cur, l);
-        }
-        cur = nxt;
+// in the reference's order (noise_score_filter.rs:129-138), by ONE wave. Terms
+// come 16 at a time, lane l holding term l & 15 (each 16-lane row a copy), and
+// every term is added with one v_fmac_f64 acc, term, 1.0 whose DPP row_newbcast:k
+// hands row lane k to the whole row: fma(t, 1, acc) rounds exactly like acc + t
+// (t*1 is exact), so the chain is the reference's adds, one instruction per
+// term, no readlane. Four groups of loads stay in flight (in-order vmcnt).
+#define MDG_FMAC_BCAST(k) "v_fmac_f64_dpp %0, %1, %2 row_newbcast:" #k " row_mask:0xf bank_mask:0xf\n"
+__device__ __forceinline__ void fold16(double& acc, double t, double one) {
+    // s_nop 1: a VALU write of t may precede this DPP read of it
+    asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) MDG_FMAC_BCAST(1) MDG_FMAC_BCAST(2)
+                 MDG_FMAC_BCAST(3) MDG_FMAC_BCAST(4) MDG_FMAC_BCAST(5) MDG_FMAC_BCAST(6)
+                 MDG_FMAC_BCAST(7) MDG_FMAC_BCAST(8) MDG_FMAC_BCAST(9) MDG_FMAC_BCAST(10)
+                 MDG_FMAC_BCAST(11) MDG_FMAC_BCAST(12) MDG_FMAC_BCAST(13) MDG_FMAC_BCAST(14)
+                 MDG_FMAC_BCAST(15)
+                 : "+v"(acc)
+                 : "v"(t), "v"(one));
+}
+
+// acc + t[0] + ... + t[n-1] (left to right) by one wave: groups of 16 terms loaded
+// with lane l holding t[16g + (l & 15)], fold16-style DPP adds. The steady part is
+// one asm loop with 12 load buffers: each group waits vmcnt(11) and, after its 16
+// adds, reloads its buffer with the group 12 ahead -- loads never cross the loop's
+// back-edge in a compiler-visible register (which forces vmcnt(0) there).
+constexpr int kFoldD = 12;
+__device__ __forceinline__ double dpp_fold_steady(double acc, const double* t, int iters) {
+    const double one = 1.0;
+    asm volatile(
+        "v_mov_b64 v[44:45], %[addr]\n"
+        "v_mov_b64 v[46:47], %[acc]\n"
+        "v_mov_b64 v[48:49], %[one]\n"
+        "s_mov_b32 s40, %[it]\n"
+        "s_mov_b64 s[42:43], 1536\n"
+        "global_load_dwordx2 v[20:21], v[44:45], off offset:0\n"
+        "global_load_dwordx2 v[22:23], v[44:45], off offset:128\n"
+        "global_load_dwordx2 v[24:25], v[44:45], off offset:256\n"
+        "global_load_dwordx2 v[26:27], v[44:45], off offset:384\n"
+        "global_load_dwordx2 v[28:29], v[44:45], off offset:512\n"
+        "global_load_dwordx2 v[30:31], v[44:45], off offset:640\n"
+        "global_load_dwordx2 v[32:33], v[44:45], off offset:768\n"
+        "global_load_dwordx2 v[34:35], v[44:45], off offset:896\n"
+        "global_load_dwordx2 v[36:37], v[44:45], off offset:1024\n"
+        "global_load_dwordx2 v[38:39], v[44:45], off offset:1152\n"
+        "global_load_dwordx2 v[40:41], v[44:45], off offset:1280\n"
+        "global_load_dwordx2 v[42:43], v[44:45], off offset:1408\n"
+        "Lfold%=:\n"
+        "s_waitcnt vmcnt(11)\n"
+        "v_fmac_f64_dpp v[46:47], v[20:21], v[48:49] row_newbcast:0 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[20:21], v[48:49] row_newbcast:1 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[20:21], v[48:49] row_newbcast:2 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[20:21], v[48:49] row_newbcast:3 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[20:21], v[48:49] row_newbcast:4 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[20:21], v[48:49] row_newbcast:5 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[20:21], v[48:49] row_newbcast:6 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[20:21], v[48:49] row_newbcast:7 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[20:21], v[48:49] row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[20:21], v[48:49] row_newbcast:9 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[20:21], v[48:49] row_newbcast:10 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[20:21], v[48:49] row_newbcast:11 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[20:21], v[48:49] row_newbcast:12 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[20:21], v[48:49] row_newbcast:13 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[20:21], v[48:49] row_newbcast:14 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[20:21], v[48:49] row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+        "global_load_dwordx2 v[20:21], v[44:45], off offset:1536\n"
+        "s_waitcnt vmcnt(11)\n"
+        "v_fmac_f64_dpp v[46:47], v[22:23], v[48:49] row_newbcast:0 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[22:23], v[48:49] row_newbcast:1 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[22:23], v[48:49] row_newbcast:2 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[22:23], v[48:49] row_newbcast:3 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[22:23], v[48:49] row_newbcast:4 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[22:23], v[48:49] row_newbcast:5 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[22:23], v[48:49] row_newbcast:6 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[22:23], v[48:49] row_newbcast:7 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[22:23], v[48:49] row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[22:23], v[48:49] row_newbcast:9 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[22:23], v[48:49] row_newbcast:10 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[22:23], v[48:49] row_newbcast:11 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[22:23], v[48:49] row_newbcast:12 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[22:23], v[48:49] row_newbcast:13 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[22:23], v[48:49] row_newbcast:14 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[22:23], v[48:49] row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+        "global_load_dwordx2 v[22:23], v[44:45], off offset:1664\n"
+        "s_waitcnt vmcnt(11)\n"
+        "v_fmac_f64_dpp v[46:47], v[24:25], v[48:49] row_newbcast:0 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[24:25], v[48:49] row_newbcast:1 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[24:25], v[48:49] row_newbcast:2 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[24:25], v[48:49] row_newbcast:3 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[24:25], v[48:49] row_newbcast:4 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[24:25], v[48:49] row_newbcast:5 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[24:25], v[48:49] row_newbcast:6 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[24:25], v[48:49] row_newbcast:7 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[24:25], v[48:49] row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[24:25], v[48:49] row_newbcast:9 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[24:25], v[48:49] row_newbcast:10 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[24:25], v[48:49] row_newbcast:11 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[24:25], v[48:49] row_newbcast:12 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[24:25], v[48:49] row_newbcast:13 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[24:25], v[48:49] row_newbcast:14 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[24:25], v[48:49] row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+        "global_load_dwordx2 v[24:25], v[44:45], off offset:1792\n"
+        "s_waitcnt vmcnt(11)\n"
+        "v_fmac_f64_dpp v[46:47], v[26:27], v[48:49] row_newbcast:0 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[26:27], v[48:49] row_newbcast:1 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[26:27], v[48:49] row_newbcast:2 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[26:27], v[48:49] row_newbcast:3 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[26:27], v[48:49] row_newbcast:4 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[26:27], v[48:49] row_newbcast:5 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[26:27], v[48:49] row_newbcast:6 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[26:27], v[48:49] row_newbcast:7 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[26:27], v[48:49] row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[26:27], v[48:49] row_newbcast:9 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[26:27], v[48:49] row_newbcast:10 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[26:27], v[48:49] row_newbcast:11 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[26:27], v[48:49] row_newbcast:12 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[26:27], v[48:49] row_newbcast:13 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[26:27], v[48:49] row_newbcast:14 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[26:27], v[48:49] row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+        "global_load_dwordx2 v[26:27], v[44:45], off offset:1920\n"
+        "s_waitcnt vmcnt(11)\n"
+        "v_fmac_f64_dpp v[46:47], v[28:29], v[48:49] row_newbcast:0 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[28:29], v[48:49] row_newbcast:1 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[28:29], v[48:49] row_newbcast:2 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[28:29], v[48:49] row_newbcast:3 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[28:29], v[48:49] row_newbcast:4 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[28:29], v[48:49] row_newbcast:5 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[28:29], v[48:49] row_newbcast:6 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[28:29], v[48:49] row_newbcast:7 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[28:29], v[48:49] row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[28:29], v[48:49] row_newbcast:9 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[28:29], v[48:49] row_newbcast:10 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[28:29], v[48:49] row_newbcast:11 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[28:29], v[48:49] row_newbcast:12 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[28:29], v[48:49] row_newbcast:13 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[28:29], v[48:49] row_newbcast:14 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[28:29], v[48:49] row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+        "global_load_dwordx2 v[28:29], v[44:45], off offset:2048\n"
+        "s_waitcnt vmcnt(11)\n"
+        "v_fmac_f64_dpp v[46:47], v[30:31], v[48:49] row_newbcast:0 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[30:31], v[48:49] row_newbcast:1 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[30:31], v[48:49] row_newbcast:2 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[30:31], v[48:49] row_newbcast:3 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[30:31], v[48:49] row_newbcast:4 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[30:31], v[48:49] row_newbcast:5 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[30:31], v[48:49] row_newbcast:6 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[30:31], v[48:49] row_newbcast:7 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[30:31], v[48:49] row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[30:31], v[48:49] row_newbcast:9 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[30:31], v[48:49] row_newbcast:10 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[30:31], v[48:49] row_newbcast:11 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[30:31], v[48:49] row_newbcast:12 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[30:31], v[48:49] row_newbcast:13 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[30:31], v[48:49] row_newbcast:14 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[30:31], v[48:49] row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+        "global_load_dwordx2 v[30:31], v[44:45], off offset:2176\n"
+        "s_waitcnt vmcnt(11)\n"
+        "v_fmac_f64_dpp v[46:47], v[32:33], v[48:49] row_newbcast:0 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[32:33], v[48:49] row_newbcast:1 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[32:33], v[48:49] row_newbcast:2 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[32:33], v[48:49] row_newbcast:3 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[32:33], v[48:49] row_newbcast:4 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[32:33], v[48:49] row_newbcast:5 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[32:33], v[48:49] row_newbcast:6 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[32:33], v[48:49] row_newbcast:7 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[32:33], v[48:49] row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[32:33], v[48:49] row_newbcast:9 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[32:33], v[48:49] row_newbcast:10 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[32:33], v[48:49] row_newbcast:11 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[32:33], v[48:49] row_newbcast:12 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[32:33], v[48:49] row_newbcast:13 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[32:33], v[48:49] row_newbcast:14 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[32:33], v[48:49] row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+        "global_load_dwordx2 v[32:33], v[44:45], off offset:2304\n"
+        "s_waitcnt vmcnt(11)\n"
+        "v_fmac_f64_dpp v[46:47], v[34:35], v[48:49] row_newbcast:0 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[34:35], v[48:49] row_newbcast:1 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[34:35], v[48:49] row_newbcast:2 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[34:35], v[48:49] row_newbcast:3 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[34:35], v[48:49] row_newbcast:4 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[34:35], v[48:49] row_newbcast:5 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[34:35], v[48:49] row_newbcast:6 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[34:35], v[48:49] row_newbcast:7 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[34:35], v[48:49] row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[34:35], v[48:49] row_newbcast:9 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[34:35], v[48:49] row_newbcast:10 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[34:35], v[48:49] row_newbcast:11 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[34:35], v[48:49] row_newbcast:12 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[34:35], v[48:49] row_newbcast:13 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[34:35], v[48:49] row_newbcast:14 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[34:35], v[48:49] row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+        "global_load_dwordx2 v[34:35], v[44:45], off offset:2432\n"
+        "s_waitcnt vmcnt(11)\n"
+        "v_fmac_f64_dpp v[46:47], v[36:37], v[48:49] row_newbcast:0 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[36:37], v[48:49] row_newbcast:1 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[36:37], v[48:49] row_newbcast:2 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[36:37], v[48:49] row_newbcast:3 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[36:37], v[48:49] row_newbcast:4 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[36:37], v[48:49] row_newbcast:5 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[36:37], v[48:49] row_newbcast:6 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[36:37], v[48:49] row_newbcast:7 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[36:37], v[48:49] row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[36:37], v[48:49] row_newbcast:9 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[36:37], v[48:49] row_newbcast:10 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[36:37], v[48:49] row_newbcast:11 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[36:37], v[48:49] row_newbcast:12 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[36:37], v[48:49] row_newbcast:13 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[36:37], v[48:49] row_newbcast:14 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[36:37], v[48:49] row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+        "global_load_dwordx2 v[36:37], v[44:45], off offset:2560\n"
+        "s_waitcnt vmcnt(11)\n"
+        "v_fmac_f64_dpp v[46:47], v[38:39], v[48:49] row_newbcast:0 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[38:39], v[48:49] row_newbcast:1 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[38:39], v[48:49] row_newbcast:2 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[38:39], v[48:49] row_newbcast:3 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[38:39], v[48:49] row_newbcast:4 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[38:39], v[48:49] row_newbcast:5 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[38:39], v[48:49] row_newbcast:6 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[38:39], v[48:49] row_newbcast:7 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[38:39], v[48:49] row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[38:39], v[48:49] row_newbcast:9 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[38:39], v[48:49] row_newbcast:10 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[38:39], v[48:49] row_newbcast:11 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[38:39], v[48:49] row_newbcast:12 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[38:39], v[48:49] row_newbcast:13 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[38:39], v[48:49] row_newbcast:14 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[38:39], v[48:49] row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+        "global_load_dwordx2 v[38:39], v[44:45], off offset:2688\n"
+        "s_waitcnt vmcnt(11)\n"
+        "v_fmac_f64_dpp v[46:47], v[40:41], v[48:49] row_newbcast:0 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[40:41], v[48:49] row_newbcast:1 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[40:41], v[48:49] row_newbcast:2 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[40:41], v[48:49] row_newbcast:3 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[40:41], v[48:49] row_newbcast:4 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[40:41], v[48:49] row_newbcast:5 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[40:41], v[48:49] row_newbcast:6 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[40:41], v[48:49] row_newbcast:7 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[40:41], v[48:49] row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[40:41], v[48:49] row_newbcast:9 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[40:41], v[48:49] row_newbcast:10 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[40:41], v[48:49] row_newbcast:11 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[40:41], v[48:49] row_newbcast:12 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[40:41], v[48:49] row_newbcast:13 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[40:41], v[48:49] row_newbcast:14 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[40:41], v[48:49] row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+        "global_load_dwordx2 v[40:41], v[44:45], off offset:2816\n"
+        "s_waitcnt vmcnt(11)\n"
+        "v_fmac_f64_dpp v[46:47], v[42:43], v[48:49] row_newbcast:0 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[42:43], v[48:49] row_newbcast:1 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[42:43], v[48:49] row_newbcast:2 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[42:43], v[48:49] row_newbcast:3 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[42:43], v[48:49] row_newbcast:4 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[42:43], v[48:49] row_newbcast:5 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[42:43], v[48:49] row_newbcast:6 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[42:43], v[48:49] row_newbcast:7 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[42:43], v[48:49] row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[42:43], v[48:49] row_newbcast:9 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[42:43], v[48:49] row_newbcast:10 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[42:43], v[48:49] row_newbcast:11 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[42:43], v[48:49] row_newbcast:12 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[42:43], v[48:49] row_newbcast:13 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[42:43], v[48:49] row_newbcast:14 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp v[46:47], v[42:43], v[48:49] row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+        "global_load_dwordx2 v[42:43], v[44:45], off offset:2944\n"
+        "v_lshl_add_u64 v[44:45], v[44:45], 0, s[42:43]\n"
+        "s_sub_u32 s40, s40, 1\n"
+        "s_cmp_lg_u32 s40, 0\n"
+        "s_cbranch_scc1 Lfold%=\n"
+        "s_waitcnt vmcnt(0)\n"
+        "v_mov_b64 %[acc], v[46:47]\n"
+        : [acc] "+v"(acc)
+        : [addr] "v"(t + (threadIdx.x & 15)), [one] "v"(one), [it] "s"(sgpr_int(iters))
+        : "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", "s40", "s42", "s43", "scc", "memory");
+    return acc;
+}
+
+__device__ double dpp_fold(double acc, const double* __restrict__ t, int n) {
+    const int sub = threadIdx.x & 15;
+    const double one = 1.0;
+    const int G = n / 16;
+    // steady asm loop: iterations of kFoldD groups whose prefetch stays below G
+    const int it = G / kFoldD - 1;
+    int g = 0;
+    if (it > 0) {
+        acc = dpp_fold_steady(acc, t, it);
+        g = it * kFoldD;
+    }
+    for (; g < G; ++g) fold16(acc, t[16 * g + sub], one);
+    const int r = n - 16 * G;
+    if (r > 0) {
+        const double v = t[min(16 * G + sub, n - 1)];
+        for (int k = 0; k < r; ++k) acc += readlane_f64(v, k);
     }
     return acc;
 }
@@ -1196,14 +1512,13 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
     const int* pc = w.det_c + base;
     const int* pr = w.det_r + base;
     const int64_t sbi0 = w.sbi[2 * s], sbi1 = w.sbi[2 * s + 1];
-    const double* sm = w.smooth_ptr + (size_t)s * w.smooth_stride;
     double* scores = w.scores + base;
+    KSTAMP(10);
     long long c0 = 0, c1 = 0;
-    for (int p = threadIdx.x; p < P; p += BS) {
+    for (int p = threadIdx.x; p < P; p += BS) {  // scores: k_scores
         const int64_t c = pc[p];
         c0 += c <= sbi0;
         c1 += c <= sbi1;
-        scores[p] = score_min_sum(sm, pl[p], pc[p], pr[p]);
     }
     const long long cnt0 = block_sum_ll<BS>(c0, lds_l);
     const long long cnt1 = block_sum_ll<BS>(c1, lds_l);
@@ -1220,11 +1535,32 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
         return;
     }
     __syncthreads();  // scores visible to the whole block
+    KSTAMP(11);
+    // mean_sd_scores (noise_score_filter.rs:129-138): left folds over the SFR =
+    // peaks[..left] ++ peaks[right..], staged contiguously (all threads) and folded
+    // by wave 0; then the squared deviations, staged in place, folded the same way
+    const int n_sfr = left + (P - right);
+    double* sfr = w.tmp0 + (size_t)s * a.N;
+    for (int k = threadIdx.x; k < n_sfr; k += BS) sfr[k] = scores[k < left ? k : right + (k - left)];
+    __syncthreads();
     if (threadIdx.x < 64) {
-        // mean_sd_scores: sequential left folds over SFR = peaks[..left] ++ peaks[right..]
-        const int n = left + (P - right);
-        const double mean = sfr_fold<false>(scores, left, right, P, 0.0) / (double)n;
-        const double var = sfr_fold<true>(scores, left, right, P, mean) / (double)n;
+        KSTAMP(15);
+        const double mean = dpp_fold(-0.0, sfr, n_sfr) / (double)n_sfr;
+        KSTAMP(16);
+        if (threadIdx.x == 0) thr_sh = mean;
+    }
+    __syncthreads();
+    KSTAMP(12);
+    const double mean = thr_sh;
+    for (int k = threadIdx.x; k < n_sfr; k += BS) {
+        const double d = sfr[k] - mean;
+        sfr[k] = d * d;
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        KSTAMP(17);
+        const double var = dpp_fold(-0.0, sfr, n_sfr) / (double)n_sfr;
+        KSTAMP(18);
         const double sd = __builtin_sqrt(var);
         if (threadIdx.x == 0) {
             thr_sh = mean + threshold * sd;
@@ -1232,6 +1568,7 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
             w.sfr_stats[2 * s + 1] = sd;
         }
     }
+    KSTAMP(13);
     __syncthreads();
     const double thr = thr_sh;
     // ordered compaction of peaks[left..right] with score >= thr
@@ -1256,6 +1593,7 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
         w.sel_count[s] = total;
         if (total == 0) w.status[s] = MDG_EMPTY_SIGNAL_REGION;
     }
+    KSTAMP(14);
 }
 
 // DetectorOnly: the detector output is the selection (detector_only.rs:17-39)
@@ -1716,6 +2054,10 @@ void launch_flags(const BatchArgs& a, const Workspace& w, hipStream_t st) {
 void launch_peaks(const BatchArgs& a, const Workspace& w, int detector_only, hipStream_t st) {
     hipLaunchKernelGGL(k_peaks<1024>, dim3(a.B), dim3(1024), 0, st, a, w, detector_only);
 }
+void launch_scores(const BatchArgs& a, const Workspace& w, hipStream_t st) {
+    const int gx = std::max(1, std::min(64, 4096 / std::max(1, a.B)));
+    hipLaunchKernelGGL(k_scores, dim3(gx, a.B), dim3(256), 0, st, a, w);
+}
 void launch_select(const BatchArgs& a, const Workspace& w, int detector_only, double threshold,
                    hipStream_t st) {
     if (detector_only)
@@ -1765,3 +2107,11 @@ void launch_synth(double* x, double* y, int64_t n, int B, double xmax, double wi
 }
 
 }  // namespace mdg
+
+#ifdef MDG_DIAG
+// diagnostic builds only (make diag): device buffer for kernel phase stamps
+extern "C" int mdg_debug_set_diag(void* dev_ptr) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(mdg::g_diag), &dev_ptr, sizeof(dev_ptr)) == hipSuccess ? 0
+                                                                                                : 100;
+}
+#endif

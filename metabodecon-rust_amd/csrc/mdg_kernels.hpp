@@ -90,6 +90,7 @@ void launch_prep(const BatchArgs& a, const Workspace& w, hipStream_t st);
 void launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int ws, hipStream_t st);
 void launch_flags(const BatchArgs& a, const Workspace& w, hipStream_t st);
 void launch_peaks(const BatchArgs& a, const Workspace& w, int detector_only, hipStream_t st);
+void launch_scores(const BatchArgs& a, const Workspace& w, hipStream_t st);
 void launch_select(const BatchArgs& a, const Workspace& w, int detector_only, double threshold,
                    hipStream_t st);
 void launch_fit_init(const BatchArgs& a, const Workspace& w, int gx, hipStream_t st);

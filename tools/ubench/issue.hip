@@ -122,6 +122,13 @@ DEFK(t_oct, "s_load_dwordx16 s[40:55], s[56:57], 0x0\n"
             "global_store_dwordx4 v8, v[0:3], s[56:57] offset:112\n"
             "s_waitcnt lgkmcnt(0)\n", 0)
 
+DEFK(t_fmac, "v_fmac_f64 v[0:1], v[2:3], v[4:5]\n", 0)
+DEFK(t_fmac_dpp, "v_fmac_f64_dpp v[0:1], v[2:3], v[4:5] row_newbcast:3 row_mask:0xf bank_mask:0xf\n", 0)
+DEFK(t_fmac_dpp_x2, "v_fmac_f64_dpp v[0:1], v[2:3], v[4:5] row_newbcast:3 row_mask:0xf bank_mask:0xf\n"
+                    "v_fmac_f64_dpp v[6:7], v[2:3], v[4:5] row_newbcast:5 row_mask:0xf bank_mask:0xf\n", 0)
+DEFK(t_add_s, "v_add_f64 v[0:1], v[0:1], s[64:65]\n", 0)
+DEFK(t_rl2_add, "v_readlane_b32 s68, v2, 5\n v_readlane_b32 s69, v3, 5\n v_add_f64 v[0:1], v[0:1], s[68:69]\n", 0)
+
 struct Test { const char* name; void (*k)(long long*, int*, const double*); int ticks_per_body; };
 
 int main() {
@@ -148,6 +155,11 @@ int main() {
         {"pair: 4 adds + b128 w/r", t_pair_b128, 2},
         {"8 tick2 + s_load x16", t_sload, 8},
         {"pair (2 ticks) alone", t_pair, 2},
+        {"tick dep v_fmac_f64", t_fmac, 1},
+        {"tick dep v_fmac_f64_dpp bcast", t_fmac_dpp, 1},
+        {"tick 2 chains fmac_dpp (per instr)", t_fmac_dpp_x2, 2},
+        {"tick dep add SGPR", t_add_s, 1},
+        {"tick 2 readlane + add", t_rl2_add, 1},
         {"pair + gstore x4 same addr", t_pair_gst_same, 2},
         {"pair + gstore x4 lane addr", t_pair_gst_lane, 2},
         {"pair + gstore x4 EXEC=1", t_pair_gst_1lane, 2},
@@ -158,7 +170,7 @@ int main() {
     };
     const int waves_list[] = {1, 4};
     for (const Test& t : tests) {
-        if (getenv("ONLY_NEW") && strncmp(t.name, "pair", 4) && strncmp(t.name, "quad", 4) && strncmp(t.name, "oct", 3) && strncmp(t.name, "tick2 add", 9)) continue;
+        if (getenv("ONLY_NEW") && strncmp(t.name, "pair", 4) && strncmp(t.name, "quad", 4) && strncmp(t.name, "oct", 3) && strncmp(t.name, "tick", 4)) continue;
         for (int W : waves_list) {
             hipLaunchKernelGGL(t.k, dim3(1), dim3(64 * W), 0, 0, cyc, ids, src);
             CHECK(hipDeviceSynchronize());
