@@ -1678,6 +1678,267 @@ __device__ __forceinline__ bool fit_fast(const Workspace& w, int s, int it) {
     return w.x_ok[s] && w.unsafe[2 * s + (it & 1)] == 0;
 }
 
+// fold the first r < 16 terms of a row-replicated group (see fold16)
+__device__ __forceinline__ void fold_partial(double& acc, double t, double one, int r) {
+    switch (r) {
+        case 1:
+            asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) : "+v"(acc) : "v"(t), "v"(one));
+            break;
+        case 2:
+            asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) MDG_FMAC_BCAST(1) : "+v"(acc) : "v"(t), "v"(one));
+            break;
+        case 3:
+            asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) MDG_FMAC_BCAST(1) MDG_FMAC_BCAST(2) : "+v"(acc) : "v"(t), "v"(one));
+            break;
+        case 4:
+            asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) MDG_FMAC_BCAST(1) MDG_FMAC_BCAST(2) MDG_FMAC_BCAST(3) : "+v"(acc) : "v"(t), "v"(one));
+            break;
+        case 5:
+            asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) MDG_FMAC_BCAST(1) MDG_FMAC_BCAST(2) MDG_FMAC_BCAST(3) MDG_FMAC_BCAST(4) : "+v"(acc) : "v"(t), "v"(one));
+            break;
+        case 6:
+            asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) MDG_FMAC_BCAST(1) MDG_FMAC_BCAST(2) MDG_FMAC_BCAST(3) MDG_FMAC_BCAST(4) MDG_FMAC_BCAST(5) : "+v"(acc) : "v"(t), "v"(one));
+            break;
+        case 7:
+            asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) MDG_FMAC_BCAST(1) MDG_FMAC_BCAST(2) MDG_FMAC_BCAST(3) MDG_FMAC_BCAST(4) MDG_FMAC_BCAST(5) MDG_FMAC_BCAST(6) : "+v"(acc) : "v"(t), "v"(one));
+            break;
+        case 8:
+            asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) MDG_FMAC_BCAST(1) MDG_FMAC_BCAST(2) MDG_FMAC_BCAST(3) MDG_FMAC_BCAST(4) MDG_FMAC_BCAST(5) MDG_FMAC_BCAST(6) MDG_FMAC_BCAST(7) : "+v"(acc) : "v"(t), "v"(one));
+            break;
+        case 9:
+            asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) MDG_FMAC_BCAST(1) MDG_FMAC_BCAST(2) MDG_FMAC_BCAST(3) MDG_FMAC_BCAST(4) MDG_FMAC_BCAST(5) MDG_FMAC_BCAST(6) MDG_FMAC_BCAST(7) MDG_FMAC_BCAST(8) : "+v"(acc) : "v"(t), "v"(one));
+            break;
+        case 10:
+            asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) MDG_FMAC_BCAST(1) MDG_FMAC_BCAST(2) MDG_FMAC_BCAST(3) MDG_FMAC_BCAST(4) MDG_FMAC_BCAST(5) MDG_FMAC_BCAST(6) MDG_FMAC_BCAST(7) MDG_FMAC_BCAST(8) MDG_FMAC_BCAST(9) : "+v"(acc) : "v"(t), "v"(one));
+            break;
+        case 11:
+            asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) MDG_FMAC_BCAST(1) MDG_FMAC_BCAST(2) MDG_FMAC_BCAST(3) MDG_FMAC_BCAST(4) MDG_FMAC_BCAST(5) MDG_FMAC_BCAST(6) MDG_FMAC_BCAST(7) MDG_FMAC_BCAST(8) MDG_FMAC_BCAST(9) MDG_FMAC_BCAST(10) : "+v"(acc) : "v"(t), "v"(one));
+            break;
+        case 12:
+            asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) MDG_FMAC_BCAST(1) MDG_FMAC_BCAST(2) MDG_FMAC_BCAST(3) MDG_FMAC_BCAST(4) MDG_FMAC_BCAST(5) MDG_FMAC_BCAST(6) MDG_FMAC_BCAST(7) MDG_FMAC_BCAST(8) MDG_FMAC_BCAST(9) MDG_FMAC_BCAST(10) MDG_FMAC_BCAST(11) : "+v"(acc) : "v"(t), "v"(one));
+            break;
+        case 13:
+            asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) MDG_FMAC_BCAST(1) MDG_FMAC_BCAST(2) MDG_FMAC_BCAST(3) MDG_FMAC_BCAST(4) MDG_FMAC_BCAST(5) MDG_FMAC_BCAST(6) MDG_FMAC_BCAST(7) MDG_FMAC_BCAST(8) MDG_FMAC_BCAST(9) MDG_FMAC_BCAST(10) MDG_FMAC_BCAST(11) MDG_FMAC_BCAST(12) : "+v"(acc) : "v"(t), "v"(one));
+            break;
+        case 14:
+            asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) MDG_FMAC_BCAST(1) MDG_FMAC_BCAST(2) MDG_FMAC_BCAST(3) MDG_FMAC_BCAST(4) MDG_FMAC_BCAST(5) MDG_FMAC_BCAST(6) MDG_FMAC_BCAST(7) MDG_FMAC_BCAST(8) MDG_FMAC_BCAST(9) MDG_FMAC_BCAST(10) MDG_FMAC_BCAST(11) MDG_FMAC_BCAST(12) MDG_FMAC_BCAST(13) : "+v"(acc) : "v"(t), "v"(one));
+            break;
+        case 15:
+            asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) MDG_FMAC_BCAST(1) MDG_FMAC_BCAST(2) MDG_FMAC_BCAST(3) MDG_FMAC_BCAST(4) MDG_FMAC_BCAST(5) MDG_FMAC_BCAST(6) MDG_FMAC_BCAST(7) MDG_FMAC_BCAST(8) MDG_FMAC_BCAST(9) MDG_FMAC_BCAST(10) MDG_FMAC_BCAST(11) MDG_FMAC_BCAST(12) MDG_FMAC_BCAST(13) MDG_FMAC_BCAST(14) : "+v"(acc) : "v"(t), "v"(one));
+            break;
+        default:
+            break;
+    }
+}
+
+// fold16 of ei into acc, interleaved with the FAST evaluation (lorentz_t<true>:
+// (x - mp)^2 + hw, then div_rn_fast's exact sequence) of the next group, returned:
+// two independent dependency chains share the issue slots
+__device__ __forceinline__ double fold16_eval_fast(double& acc, double ei, double one, double x,
+                                                   double sf, double hw, double mp) {
+    double eo, d, den, r, t, q;
+    asm volatile(
+        "s_nop 1\n"
+        "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:0 row_mask:0xf bank_mask:0xf\n"
+        "v_add_f64 %[d], %[x], -%[mp]\n"
+        "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:1 row_mask:0xf bank_mask:0xf\n"
+        "v_mul_f64 %[d], %[d], %[d]\n"
+        "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:2 row_mask:0xf bank_mask:0xf\n"
+        "v_add_f64 %[den], %[hw], %[d]\n"
+        "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:3 row_mask:0xf bank_mask:0xf\n"
+        "v_rcp_f64 %[r], %[den]\n"
+        "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:4 row_mask:0xf bank_mask:0xf\n"
+        "v_fma_f64 %[t], -%[den], %[r], 1.0\n"
+        "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:5 row_mask:0xf bank_mask:0xf\n"
+        "v_fma_f64 %[r], %[r], %[t], %[r]\n"
+        "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:6 row_mask:0xf bank_mask:0xf\n"
+        "v_fma_f64 %[t], -%[den], %[r], 1.0\n"
+        "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:7 row_mask:0xf bank_mask:0xf\n"
+        "v_fma_f64 %[r], %[r], %[t], %[r]\n"
+        "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
+        "v_mul_f64 %[q], %[sf], %[r]\n"
+        "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:9 row_mask:0xf bank_mask:0xf\n"
+        "v_fma_f64 %[t], -%[den], %[q], %[sf]\n"
+        "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:10 row_mask:0xf bank_mask:0xf\n"
+        "v_fma_f64 %[eo], %[t], %[r], %[q]\n"
+        "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:11 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:12 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:13 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:14 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+        : [acc] "+v"(acc), [eo] "=&v"(eo), [d] "=&v"(d), [den] "=&v"(den), [r] "=&v"(r),
+          [t] "=&v"(t), [q] "=&v"(q)
+        : [ei] "v"(ei), [one] "v"(one), [x] "v"(x), [sf] "v"(sf), [hw] "v"(hw), [mp] "v"(mp));
+    return eo;
+}
+
+// Two independent 4-point sets (A, B) per wave: fold16 of both into their sums,
+// interleaved with the FAST evaluation of the next group for both (same peaks,
+// different x) -- four dependency chains share the issue slots.
+__device__ __forceinline__ void fold2_eval_fast(double& accA, double& accB, double& eA, double& eB,
+                                                double one, double xA, double xB, double sf,
+                                                double hw, double mp) {
+    double eoA, dA, denA, rA, tA, qA; double eoB, dB, denB, rB, tB, qB;
+    asm volatile(
+        "s_nop 1\n"
+        "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:0 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:0 row_mask:0xf bank_mask:0xf\n"
+        "v_add_f64 %[dA], %[xA], -%[mp]\n"
+        "v_add_f64 %[dB], %[xB], -%[mp]\n"
+        "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:1 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:1 row_mask:0xf bank_mask:0xf\n"
+        "v_mul_f64 %[dA], %[dA], %[dA]\n"
+        "v_mul_f64 %[dB], %[dB], %[dB]\n"
+        "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:2 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:2 row_mask:0xf bank_mask:0xf\n"
+        "v_add_f64 %[denA], %[hw], %[dA]\n"
+        "v_add_f64 %[denB], %[hw], %[dB]\n"
+        "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:3 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:3 row_mask:0xf bank_mask:0xf\n"
+        "v_rcp_f64 %[rA], %[denA]\n"
+        "v_rcp_f64 %[rB], %[denB]\n"
+        "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:4 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:4 row_mask:0xf bank_mask:0xf\n"
+        "v_fma_f64 %[tA], -%[denA], %[rA], 1.0\n"
+        "v_fma_f64 %[tB], -%[denB], %[rB], 1.0\n"
+        "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:5 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:5 row_mask:0xf bank_mask:0xf\n"
+        "v_fma_f64 %[rA], %[rA], %[tA], %[rA]\n"
+        "v_fma_f64 %[rB], %[rB], %[tB], %[rB]\n"
+        "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:6 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:6 row_mask:0xf bank_mask:0xf\n"
+        "v_fma_f64 %[tA], -%[denA], %[rA], 1.0\n"
+        "v_fma_f64 %[tB], -%[denB], %[rB], 1.0\n"
+        "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:7 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:7 row_mask:0xf bank_mask:0xf\n"
+        "v_fma_f64 %[rA], %[rA], %[tA], %[rA]\n"
+        "v_fma_f64 %[rB], %[rB], %[tB], %[rB]\n"
+        "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
+        "v_mul_f64 %[qA], %[sf], %[rA]\n"
+        "v_mul_f64 %[qB], %[sf], %[rB]\n"
+        "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:9 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:9 row_mask:0xf bank_mask:0xf\n"
+        "v_fma_f64 %[tA], -%[denA], %[qA], %[sf]\n"
+        "v_fma_f64 %[tB], -%[denB], %[qB], %[sf]\n"
+        "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:10 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:10 row_mask:0xf bank_mask:0xf\n"
+        "v_fma_f64 %[eoA], %[tA], %[rA], %[qA]\n"
+        "v_fma_f64 %[eoB], %[tB], %[rB], %[qB]\n"
+        "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:11 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:11 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:12 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:12 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:13 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:13 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:14 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:14 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+        : [accA] "+v"(accA), [accB] "+v"(accB), [eoA] "=&v"(eoA), [dA] "=&v"(dA), [denA] "=&v"(denA), [rA] "=&v"(rA), [tA] "=&v"(tA), [qA] "=&v"(qA), [eoB] "=&v"(eoB), [dB] "=&v"(dB), [denB] "=&v"(denB), [rB] "=&v"(rB), [tB] "=&v"(tB), [qB] "=&v"(qB)
+        : [eiA] "v"(eA), [eiB] "v"(eB), [one] "v"(one), [xA] "v"(xA), [xB] "v"(xB), [sf] "v"(sf),
+          [hw] "v"(hw), [mp] "v"(mp));
+    eA = eoA;
+    eB = eoB;
+}
+
+// K6c  fit superposition for the smallest batches (B <= 4): a wave evaluates 4
+// reduced points x 16 Lorentzians per instruction (16-lane row = one point) and
+// folds each 16-peak group into its row's running sum with row_newbcast DPP adds
+// (fold16), in peak order -- the reference's summation (lorentzian.rs:606-611),
+// bit-identical to K6. 3P/4 waves instead of 3P/64, so a single spectrum spreads
+// over the whole chip; peak parameters are staged in LDS in chunks of kFitChunk.
+constexpr int kFitChunk = 2048;
+template <bool FAST>
+__device__ __forceinline__ void fit_dpp_body(const BatchArgs& a, const Workspace& w, int s, int P,
+                                             double* lds_p) {
+    const size_t base = (size_t)s * w.capD;
+    const double* __restrict__ params = w.params + 3 * base;
+    const int lane = threadIdx.x & 63, sub = lane & 15;
+    const int n_pts = 3 * P;
+    const int tiles = (n_pts + 31) / 32;  // 32 points per 256-thread workgroup, 8 per wave
+    const double one = 1.0;
+    KSTAMP(20);
+    for (int tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+        const int iA = tile * 32 + (threadIdx.x >> 6) * 8 + (lane >> 4), iB = iA + 4;
+        const double xA = w.rx[3 * base + min(iA, n_pts - 1)];
+        const double xB = w.rx[3 * base + min(iB, n_pts - 1)];
+        double accA = -0.0, accB = -0.0;
+        for (int c0 = 0; c0 < P; c0 += kFitChunk) {
+            const int cn = min(kFitChunk, P - c0);
+            __syncthreads();
+            {
+                // coalesced copy of the chunk's {sfhw, hw2, maxp} triples, all loads in
+                // flight (fixed trip count, clamped addresses, predicated LDS writes)
+                constexpr int PER = 3 * kFitChunk / 256;
+                const double* src = params + 3 * (size_t)c0;
+                const int nd = 3 * cn;
+                double v[PER];
+#pragma unroll
+                for (int u = 0; u < PER; ++u) v[u] = src[min(u * 256 + (int)threadIdx.x, nd - 1)];
+#pragma unroll
+                for (int u = 0; u < PER; ++u)
+                    if (u * 256 + (int)threadIdx.x < nd) lds_p[u * 256 + threadIdx.x] = v[u];
+            }
+            __syncthreads();
+            KSTAMP(21);
+            const int G = cn / 16;
+            if constexpr (FAST) {
+                // software-pipelined: fold group k-1 while evaluating group k, the
+                // parameters of group k+1 read from LDS one step ahead (sets P / Q)
+                if (G > 0) {
+                    auto ld = [&](int grp, double& f, double& h, double& m) {
+                        const int j = 16 * min(grp, G - 1) + sub;  // clamped: never divergent
+                        f = lds_p[3 * j];
+                        h = lds_p[3 * j + 1];
+                        m = lds_p[3 * j + 2];
+                    };
+                    const double f0 = lds_p[3 * sub], h0 = lds_p[3 * sub + 1], m0 = lds_p[3 * sub + 2];
+                    double eA = lorentz_t<true>(xA, f0, h0, m0), eB = lorentz_t<true>(xB, f0, h0, m0);
+                    double fP, hP, mP, fQ, hQ, mQ;
+                    ld(1, fP, hP, mP);
+                    int k = 1;  // next group to evaluate
+                    for (; k + 2 <= G; k += 2) {
+                        ld(k + 1, fQ, hQ, mQ);
+                        fold2_eval_fast(accA, accB, eA, eB, one, xA, xB, fP, hP, mP);
+                        ld(k + 2, fP, hP, mP);
+                        fold2_eval_fast(accA, accB, eA, eB, one, xA, xB, fQ, hQ, mQ);
+                    }
+                    if (k < G) fold2_eval_fast(accA, accB, eA, eB, one, xA, xB, fP, hP, mP);
+                    fold16(accA, eA, one);
+                    fold16(accB, eB, one);
+                }
+            } else {
+                for (int g = 0; g < G; ++g) {
+                    const int j = 16 * g + sub;
+                    const double f = lds_p[3 * j], h = lds_p[3 * j + 1], m = lds_p[3 * j + 2];
+                    fold16(accA, lorentz_t<false>(xA, f, h, m), one);
+                    fold16(accB, lorentz_t<false>(xB, f, h, m), one);
+                }
+            }
+            if (16 * G < cn) {
+                const int jj = min(16 * G + sub, cn - 1);
+                const double f = lds_p[3 * jj], h = lds_p[3 * jj + 1], m = lds_p[3 * jj + 2];
+                fold_partial(accA, lorentz_t<FAST>(xA, f, h, m), one, cn - 16 * G);
+                fold_partial(accB, lorentz_t<FAST>(xB, f, h, m), one, cn - 16 * G);
+            }
+        }
+        KSTAMP(22);
+        if (sub == 0 && iA < n_pts) w.ratio[3 * base + iA] = w.ry[3 * base + iA] / accA;
+        if (sub == 0 && iB < n_pts) w.ratio[3 * base + iB] = w.ry[3 * base + iB] / accB;
+    }
+    KSTAMP(23);
+}
+
+__global__ __launch_bounds__(256) void k_fit_sup_dpp(BatchArgs a, Workspace w, int it) {
+    __shared__ double lds_p[3 * kFitChunk];  // {sfhw, hw2, maxp} of one chunk of peaks
+    const int s = blockIdx.y;
+    if (w.status[s]) return;
+    const int P = w.sel_count[s];
+    if (fit_fast(w, s, it)) fit_dpp_body<true>(a, w, s, P, lds_p);
+    else fit_dpp_body<false>(a, w, s, P, lds_p);
+}
+
 __global__ void k_fit_sup(BatchArgs a, Workspace w, int it) {
     const int s = blockIdx.y;
     if (w.status[s]) return;
@@ -2069,7 +2330,15 @@ void launch_fit_init(const BatchArgs& a, const Workspace& w, int gx, hipStream_t
     hipLaunchKernelGGL(k_fit_init, dim3(gx, a.B), dim3(256), 0, st, a, w);
 }
 void launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st) {
-    if (a.B <= 16) {
+    const char* force = std::getenv("MDG_FITSUP");
+    const std::string f = force ? force : "";
+    if ((!force && a.B <= 4) || f == "dpp") {
+        // 32 points per workgroup: 192 workgroups at P = 2048, grid-stride beyond
+        const int g = std::max(64, std::min(512, 1024 / a.B));
+        hipLaunchKernelGGL(k_fit_sup_dpp, dim3(g, a.B), dim3(256), 0, st, a, w, it);
+        return;
+    }
+    if ((!force && a.B <= 16) || f == "split") {
         // 16 points per 1024-thread workgroup: 3P/16 workgroups per spectrum (384 at
         // P = 2048) keep every CU busy; grid-stride beyond that
         const int g = std::max(64, std::min(1024, 2048 / a.B));

@@ -318,3 +318,19 @@ def test_chain_smoother_repeated_launches(ctx, monkeypatch):
         ys = rng.normal(0, 1, (5, 131072)) * 1e3 + rep
         for s, row in enumerate(_smooth_rows(ctx, ys, 3, 3)):
             assert np.array_equal(row, oracle.moving_average(ys[s], 3, 3)), (rep, s)
+
+
+@pytest.mark.parametrize("path", ["dpp", "split", "plain"])
+def test_fit_superposition_kernels(ctx, path, monkeypatch):
+    """Every fit-superposition kernel (row-broadcast DPP fold, LDS split fold, one
+    thread per point; chosen by MDG_FITSUP) gives the oracle's Lorentzians bit for
+    bit, including peak counts that are not multiples of the 16-peak groups."""
+    monkeypatch.setenv("MDG_FITSUP", path)
+    names = ["sim_03", "blood_03", "synth_128k_2k_s1"]
+    for name in names:
+        x, y, sb, st, ign = load_case(name)
+        o = oracle.deconvolute(x, y, sb, st, ignore=ign)
+        status, counts, out, mse = gpu_batch(ctx, x, y[None, :], [sb], st, ignore=ign)
+        assert status[0] == o.status, name
+        assert np.array_equal(out[0, : counts[0]], o.params), name
+        assert abs(mse[0] - o.mse) <= MSE_RTOL * abs(o.mse), name

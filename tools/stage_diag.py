@@ -39,7 +39,7 @@ for _ in range(3):
     assert rc == 0
     torch.cuda.synchronize()
 d = diag.cpu().tolist()[512:]
-groups = {"select": range(10, 19), "peaks": range(0, 5), "fit_split": range(20, 26),
+groups = {"select": range(10, 19), "peaks": range(0, 5), "fit_dpp": range(20, 24),
           "mse": range(30, 34)}
 for name, r in groups.items():
     v = [d[k] for k in r]
