@@ -116,6 +116,8 @@ int mdg_ctx_synchronize(mdg_ctx* ctx);
  * 6 fit_update, 7 retain, 8 mse_superposition, 9 mse_reduce, 10 superposition_vec,
  * 11 synth. times_ms/launches receive accumulated values (arrays of n_stages). */
 int mdg_ctx_set_profiling(mdg_ctx* ctx, int enable);
+/* Same, for the stages whose bit (1 << stage) is set in mask only. */
+int mdg_ctx_set_profiling_mask(mdg_ctx* ctx, uint32_t mask);
 int mdg_ctx_stage_times(mdg_ctx* ctx, double* times_ms, uint64_t* launches, int n_stages);
 int mdg_ctx_reset_stage_times(mdg_ctx* ctx);
 

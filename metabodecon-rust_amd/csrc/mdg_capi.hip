@@ -51,13 +51,15 @@ struct mdg_ctx {
     Buffer arena;
     int ws_B = 0, ws_N = 0;
     Buffer chain;  // k_smooth_chain buffers (allocated on first use)
+    // replayable pipelines of mdg_deconvolute_batch_device, keyed by every argument
+    std::vector<std::pair<std::vector<unsigned char>, hipGraphExec_t>> graphs;
     int last_B = 0, last_N = 0;  // shape of the last pipeline run
     bool last_smoothed = false;  // the last run used the moving average
     Workspace w{};
     // staging for the host-pointer API
     Buffer st_x, st_y, st_sb, st_out, st_cnt, st_mse, st_status, st_L, st_sup, st_flag;
     // profiling
-    bool profiling = false;
+    uint32_t profile_mask = 0;  // stages timed with hipEvents (bit = stage)
     std::vector<Pending> pending;
     std::vector<hipEvent_t> free_events;
     double stage_ms[kStages] = {0};
@@ -105,13 +107,13 @@ struct StageTimer {
     int stage;
     hipEvent_t a = nullptr;
     StageTimer(mdg_ctx* c_, int s) : c(c_), stage(s) {
-        if (c->profiling) {
+        if ((c->profile_mask >> stage) & 1u) {
             a = get_event(c);
             if (a) (void)hipEventRecord(a, c->stream);
         }
     }
     ~StageTimer() {
-        if (c->profiling && a) {
+        if (a) {
             hipEvent_t b = get_event(c);
             if (b) {
                 (void)hipEventRecord(b, c->stream);
@@ -317,6 +319,7 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
 void fill_args(BatchArgs& a, size_t b, size_t n, const double* x, size_t xs, const double* y,
                size_t ys, const double* sb, const double* ignore, size_t n_ignore, double* out,
                size_t cap, int32_t* cnt, double* mse, int32_t* status) {
+    std::memset(&a, 0, sizeof(a));  // padding too: graph keys compare the bytes
     a.B = (int)b;
     a.N = (int)n;
     a.x = x;
@@ -502,6 +505,8 @@ int mdg_ctx_destroy(mdg_ctx* c) {
             (void)hipEventDestroy(p.b);
         }
         for (auto e : c->free_events) (void)hipEventDestroy(e);
+        for (auto& ge : c->graphs) (void)hipGraphExecDestroy(ge.second);
+        c->graphs.clear();
         for (Buffer* b : {&c->arena, &c->chain, &c->st_x, &c->st_y, &c->st_sb, &c->st_out, &c->st_cnt,
                           &c->st_mse, &c->st_status, &c->st_L, &c->st_sup, &c->st_flag})
             if (b->p) (void)hipFree(b->p);
@@ -532,7 +537,15 @@ int mdg_ctx_set_profiling(mdg_ctx* c, int enable) {
     if (!c) return MDG_INVALID_ARGUMENT;
     std::lock_guard<std::mutex> g(c->mu);
     drain_timers(c);
-    c->profiling = enable != 0;
+    c->profile_mask = enable ? 0xffffffffu : 0u;
+    return MDG_OK;
+}
+
+int mdg_ctx_set_profiling_mask(mdg_ctx* c, uint32_t mask) {
+    if (!c) return MDG_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> g(c->mu);
+    drain_timers(c);
+    c->profile_mask = mask;
     return MDG_OK;
 }
 
@@ -593,6 +606,70 @@ int mdg_ctx_last_smoothed(mdg_ctx* c, size_t spectrum, double* out, size_t n) {
     return MDG_OK;
 }
 
+// run_pipeline through a cached hipGraph: the whole launch sequence (about 26
+// kernels at the default settings) replays as one graph launch. Captured on the
+// context's own stream, launched on the current one; keyed by the bytes of every
+// argument, the settings and the workspace addresses (a reallocation re-keys).
+// Not used while stages are being timed, or for the reference-panic shape
+// (host-synchronous path); MDG_GRAPHS=0 disables it.
+int run_pipeline_graphed(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
+    const char* env = std::getenv("MDG_GRAPHS");
+    const bool ma = s->smoother == MDG_SMOOTH_MOVING_AVERAGE;
+    if ((env && std::string(env) == "0") || c->profile_mask ||
+        (ma && (int64_t)(s->smooth_window / 2) > a.N))
+        return run_pipeline(c, a, s);
+    // size every buffer first: the capture must not allocate, and the key needs the
+    // final addresses
+    int rc = ensure_workspace(c, a.B, a.N);
+    if (rc) return rc;
+    if (ma && chain_supported(a.B, a.N, (int)s->smooth_iterations, (int)s->smooth_window) &&
+        !(std::getenv("MDG_SMOOTH") && std::string(std::getenv("MDG_SMOOTH")) != "chain"))
+        (void)ensure(c->chain, chain_bytes(a.B, a.N, (int)s->smooth_window, (int)s->smooth_iterations));
+    std::vector<unsigned char> key(sizeof(BatchArgs) + sizeof(mdg_settings) + 2 * sizeof(void*) +
+                                   sizeof(size_t));
+    unsigned char* k = key.data();
+    std::memcpy(k, &a, sizeof(BatchArgs));
+    k += sizeof(BatchArgs);
+    std::memcpy(k, s, sizeof(mdg_settings));
+    k += sizeof(mdg_settings);
+    std::memcpy(k, &c->arena.p, sizeof(void*));
+    k += sizeof(void*);
+    std::memcpy(k, &c->chain.p, sizeof(void*));
+    k += sizeof(void*);
+    std::memcpy(k, &c->chain.bytes, sizeof(size_t));
+    hipGraphExec_t exec = nullptr;
+    for (auto& ge : c->graphs)
+        if (ge.first == key) exec = ge.second;
+    if (!exec) {
+        hipStream_t user = c->stream;
+        c->stream = c->own;
+        HIPCHK(hipStreamBeginCapture(c->own, hipStreamCaptureModeRelaxed));
+        rc = run_pipeline(c, a, s);
+        hipGraph_t graph = nullptr;
+        const hipError_t e = hipStreamEndCapture(c->own, &graph);
+        c->stream = user;
+        if (rc || e != hipSuccess) {
+            if (graph) (void)hipGraphDestroy(graph);
+            return rc ? rc : hip_fail(e);
+        }
+        const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(graph);
+        if (ei != hipSuccess) return hip_fail(ei);
+        if (c->graphs.size() >= 8) {
+            (void)hipGraphExecDestroy(c->graphs.front().second);
+            c->graphs.erase(c->graphs.begin());
+        }
+        c->graphs.emplace_back(std::move(key), exec);
+    } else {
+        // host-side state run_pipeline would have set
+        c->last_B = a.B;
+        c->last_N = a.N;
+        c->last_smoothed = ma;
+    }
+    HIPCHK(hipGraphLaunch(exec, c->stream));
+    return MDG_OK;
+}
+
 int mdg_deconvolute_batch_device(mdg_ctx* c, size_t b, size_t n, const double* d_x,
                                  size_t x_stride, const double* d_y, size_t y_stride,
                                  const double* d_sb, const mdg_settings* s, const double* ignore,
@@ -609,7 +686,7 @@ int mdg_deconvolute_batch_device(mdg_ctx* c, size_t b, size_t n, const double* d
     BatchArgs a;
     fill_args(a, b, n, d_x, x_stride, d_y, y_stride, d_sb, ignore, n_ignore, (double*)d_out, cap,
               d_counts, d_mse, d_status);
-    return run_pipeline(c, a, s);
+    return run_pipeline_graphed(c, a, s);
 }
 
 int mdg_deconvolute_batch(mdg_ctx* c, size_t b, size_t n, const double* x, size_t x_stride,

@@ -384,6 +384,40 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
     return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
 }
 
+#define MDG_FMAC_BCAST(k) "v_fmac_f64_dpp %0, %1, %2 row_newbcast:" #k " row_mask:0xf bank_mask:0xf\n"
+__device__ __forceinline__ void fold16(double& acc, double t, double one) {
+    // s_nop 1: a VALU write of t may precede this DPP read of it
+    asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) MDG_FMAC_BCAST(1) MDG_FMAC_BCAST(2)
+                 MDG_FMAC_BCAST(3) MDG_FMAC_BCAST(4) MDG_FMAC_BCAST(5) MDG_FMAC_BCAST(6)
+                 MDG_FMAC_BCAST(7) MDG_FMAC_BCAST(8) MDG_FMAC_BCAST(9) MDG_FMAC_BCAST(10)
+                 MDG_FMAC_BCAST(11) MDG_FMAC_BCAST(12) MDG_FMAC_BCAST(13) MDG_FMAC_BCAST(14)
+                 MDG_FMAC_BCAST(15)
+                 : "+v"(acc)
+                 : "v"(t), "v"(one));
+}
+
+// eight moving-average ticks k0..k0+7 of a row-replicated operand group: for each
+// tick, acc += A[k] then acc -= P[k] (fma(+-t, 1, acc) rounds as the add / sub)
+#define MDG_TICK(k)                                                                        \
+    "v_fmac_f64_dpp %0, %1, %3 row_newbcast:" #k " row_mask:0xf bank_mask:0xf\n"           \
+    "v_fmac_f64_dpp %0, -%2, %3 row_newbcast:" #k " row_mask:0xf bank_mask:0xf\n"
+template <int K0>
+__device__ __forceinline__ void fold8_ticks(double& acc, double A, double P, double one);
+template <>
+__device__ __forceinline__ void fold8_ticks<0>(double& acc, double A, double P, double one) {
+    asm volatile("s_nop 1\n" MDG_TICK(0) MDG_TICK(1) MDG_TICK(2) MDG_TICK(3) MDG_TICK(4)
+                 MDG_TICK(5) MDG_TICK(6) MDG_TICK(7)
+                 : "+v"(acc)
+                 : "v"(A), "v"(P), "v"(one));
+}
+template <>
+__device__ __forceinline__ void fold8_ticks<8>(double& acc, double A, double P, double one) {
+    asm volatile("s_nop 1\n" MDG_TICK(8) MDG_TICK(9) MDG_TICK(10) MDG_TICK(11) MDG_TICK(12)
+                 MDG_TICK(13) MDG_TICK(14) MDG_TICK(15)
+                 : "+v"(acc)
+                 : "v"(A), "v"(P), "v"(one));
+}
+
 __device__ __forceinline__ double dpp_shr1(double v) {
     const long long b = __double_as_longlong(v);
     int lo = (int)(unsigned)(b & 0xffffffffll), hi = (int)(b >> 32);
@@ -847,31 +881,27 @@ __global__ __launch_bounds__(192) void k_smooth_chain(BatchArgs a, Workspace w, 
             }
             return true;
         };
-        // generic block: inputs gathered lane-parallel (coherent sc1 loads), then the
-        // sequential ticks read them back with readlane
-        double prev_lo = 0.0, prev_hi = 0.0;  // previous block's inputs (for pops)
+        // generic block (first and last blocks): the ticks as DPP row-broadcast fmacs
+        // (fold8_ticks), operands zero-padded: the running sum starts at +0.0 and can
+        // never become -0.0 (x + y is -0 only for -0 + -0, x - y only for -0 - +0),
+        // so adding or subtracting +0.0 is exactly the reference's skipped term.
+        // Only the per-8-tick checkpoints are stored, as in the steady loop.
+        const double one = 1.0;
         auto generic = [&](int k) -> bool {
             if (!wait_in(min(k + 2, nIB))) return false;
             const int j0 = k * CB;
-            const int ja = j0 + lane, jb = j0 + 64 + lane;
-            const double v_lo = ja < N ? ld_sc1(in + ja) : 0.0;
-            const double v_hi = (lane < CB - 64 && jb < N) ? ld_sc1(in + jb) : 0.0;
-            const int jend = min(j0 + CB, nJ);
-            for (int j = j0; j < jend; ++j) {
-                const int e = j - j0;
-                if (j < N) sum += readlane_f64(e < 64 ? v_lo : v_hi, e < 64 ? e : e - 64);
-                if (j >= WS) {
-                    const int q = e - WS;  // pop index relative to the block
-                    double pv;
-                    if (q >= 0) pv = readlane_f64(q < 64 ? v_lo : v_hi, q < 64 ? q : q - 64);
-                    else pv = readlane_f64(CB + q < 64 ? prev_lo : prev_hi,
-                                           CB + q < 64 ? CB + q : CB + q - 64);
-                    sum -= pv;
-                }
-                raw[j] = sum;
+#pragma unroll 1
+            for (int g16 = 0; g16 < CB / 16; ++g16) {
+                const int j = j0 + 16 * g16 + (lane & 15);
+                const double av = ld_sc1(in + min(j, N - 1));
+                const double pv = ld_sc1(in + max(min(j - WS, N - 1), 0));
+                const double A = j < N ? av : 0.0;
+                const double Pm = j >= WS ? pv : 0.0;
+                fold8_ticks<0>(sum, A, Pm, one);
+                raw[j0 + 16 * g16 + 7] = sum;
+                fold8_ticks<8>(sum, A, Pm, one);
+                raw[j0 + 16 * g16 + 15] = sum;
             }
-            prev_lo = v_lo;
-            prev_hi = v_hi;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             CTL_ST(raw_done, k + 1);
             return true;
@@ -886,13 +916,7 @@ __global__ __launch_bounds__(192) void k_smooth_chain(BatchArgs a, Workspace w, 
                                               kB - kA, nIB,
                                               lds_offset(&ctl), sum, stat);
             ok = stat == 0 && done == kB;
-            if (ok) {
-                CTL_ST(raw_done, kB);
-                // the generic tail pops from the last steady block: reload it
-                const int j0 = (kB - 1) * CB;
-                prev_lo = ld_sc1(in + j0 + lane);
-                prev_hi = lane < CB - 64 ? ld_sc1(in + j0 + 64 + lane) : 0.0;
-            }
+            if (ok) CTL_ST(raw_done, kB);
         }
         DIAGC(2, __builtin_amdgcn_s_memtime());
         DIAGC(4, kB - kA);
@@ -954,7 +978,6 @@ __global__ __launch_bounds__(192) void k_smooth_chain(BatchArgs a, Workspace w, 
         // scales every finished raw block by 1/len and publishes them in one batch
         // (sc1 stores, vmcnt(0), sc1 counter: the downstream pass polls it)
         constexpr int MAXB = 8;                   // blocks per batch
-        const int kA = 1, kB = max(kA, (N - 8) / CB);  // steady j-blocks (as the chain)
         int sc = 0;
         unsigned idle = 0;
         bool ok = true;
@@ -996,20 +1019,19 @@ __global__ __launch_bounds__(192) void k_smooth_chain(BatchArgs a, Workspace w, 
                     }
                 }
                 for (int g = g0 + lane; g < g1; g += 64) {
-                    const int blk = 8 * g / CB;
-                    if (blk >= kA && blk < kB) {
-                        const int e0 = 8 * g - base;
-                        double sum_g = sc_raw[e0 - 1];
-                        double rv[8];
+                    // every group holds only its checkpoint; replay from the previous one
+                    // (group 0 from T::zero()) with the zero-padded operands of the chain
+                    const int e0 = 8 * g - base;
+                    double sum_g = g == 0 ? 0.0 : sc_raw[e0 - 1];
+                    double rv[8];
 #pragma unroll
-                        for (int u = 0; u < 8; ++u) {
-                            sum_g += sc_in[e0 + u];
-                            sum_g -= sc_in[e0 + u - WS];
-                            rv[u] = sum_g;
-                        }
-#pragma unroll
-                        for (int u = 0; u < 8; ++u) sc_raw[e0 + u] = rv[u];
+                    for (int u = 0; u < 8; ++u) {
+                        sum_g += sc_in[e0 + u];
+                        sum_g -= sc_in[e0 + u - WS];
+                        rv[u] = sum_g;
                     }
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) sc_raw[e0 + u] = rv[u];
                 }
                 for (int i = i0 + lane; i < i1; i += 64) {
                     // len of the circular buffer after tick i (moving_average.rs:66-81)
@@ -1208,17 +1230,7 @@ __global__ void k_scores(BatchArgs a, Workspace w) {
 // hands row lane k to the whole row: fma(t, 1, acc) rounds exactly like acc + t
 // (t*1 is exact), so the chain is the reference's adds, one instruction per
 // term, no readlane. Four groups of loads stay in flight (in-order vmcnt).
-#define MDG_FMAC_BCAST(k) "v_fmac_f64_dpp %0, %1, %2 row_newbcast:" #k " row_mask:0xf bank_mask:0xf\n"
-__device__ __forceinline__ void fold16(double& acc, double t, double one) {
-    // s_nop 1: a VALU write of t may precede this DPP read of it
-    asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) MDG_FMAC_BCAST(1) MDG_FMAC_BCAST(2)
-                 MDG_FMAC_BCAST(3) MDG_FMAC_BCAST(4) MDG_FMAC_BCAST(5) MDG_FMAC_BCAST(6)
-                 MDG_FMAC_BCAST(7) MDG_FMAC_BCAST(8) MDG_FMAC_BCAST(9) MDG_FMAC_BCAST(10)
-                 MDG_FMAC_BCAST(11) MDG_FMAC_BCAST(12) MDG_FMAC_BCAST(13) MDG_FMAC_BCAST(14)
-                 MDG_FMAC_BCAST(15)
-                 : "+v"(acc)
-                 : "v"(t), "v"(one));
-}
+
 
 // acc + t[0] + ... + t[n-1] (left to right) by one wave: groups of 16 terms loaded
 // with lane l holding t[16g + (l & 15)], fold16-style DPP adds. The steady part is

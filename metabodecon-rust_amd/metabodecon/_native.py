@@ -43,7 +43,7 @@ EXPORTS = [
     "mdg_ctx_set_profiling", "mdg_ctx_stage_times", "mdg_ctx_reset_stage_times",
     "mdg_deconvolute", "mdg_deconvolute_batch", "mdg_deconvolute_batch_device",
     "mdg_superposition_vec", "mdg_superposition_vec_device", "mdg_synth_batch_device",
-    "mdg_ctx_last_peaks", "mdg_ctx_last_smoothed",
+    "mdg_ctx_last_peaks", "mdg_ctx_last_smoothed", "mdg_ctx_set_profiling_mask",
 ]
 
 
@@ -131,6 +131,7 @@ def _declare(L):
     L.mdg_ctx_set_stream.argtypes = [_vp, _vp]
     L.mdg_ctx_synchronize.argtypes = [_vp]
     L.mdg_ctx_set_profiling.argtypes = [_vp, ctypes.c_int]
+    L.mdg_ctx_set_profiling_mask.argtypes = [_vp, ctypes.c_uint32]
     L.mdg_ctx_stage_times.argtypes = [_vp, _dp, _u64p, ctypes.c_int]
     L.mdg_ctx_reset_stage_times.argtypes = [_vp]
     L.mdg_deconvolute.argtypes = [_vp, _dp, _dp, _sz, ctypes.c_double, ctypes.c_double, sp, _dp,
@@ -205,6 +206,13 @@ class Context:
 
     def set_profiling(self, on: bool):
         lib().mdg_ctx_set_profiling(self.handle, 1 if on else 0)
+
+    def set_profiling_stages(self, names):
+        """Time only the named stages (STAGE_NAMES) with hipEvents."""
+        mask = 0
+        for n in names:
+            mask |= 1 << STAGE_NAMES.index(n)
+        lib().mdg_ctx_set_profiling_mask(self.handle, mask)
 
     def stage_times(self) -> dict:
         ms = np.zeros(N_STAGES)

@@ -334,3 +334,52 @@ def test_fit_superposition_kernels(ctx, path, monkeypatch):
         assert status[0] == o.status, name
         assert np.array_equal(out[0, : counts[0]], o.params), name
         assert abs(mse[0] - o.mse) <= MSE_RTOL * abs(o.mse), name
+
+
+def test_device_graph_replay(ctx, monkeypatch):
+    """mdg_deconvolute_batch_device replays a cached hipGraph for repeated argument
+    sets: refilling the same device buffers with other spectra must still give the
+    oracle's results on the replayed launch, and the same bits as the uncaptured
+    pipeline (MDG_GRAPHS=0)."""
+    torch = pytest.importorskip("torch")
+    names = [["blood_02", "blood_04"], ["blood_09", "blood_11"], ["blood_02", "blood_04"]]
+    n = load_case("blood_02")[1].size
+    b = 2
+    dev = "cuda"
+    x = torch.empty((b, n), dtype=torch.float64, device=dev)
+    y = torch.empty((b, n), dtype=torch.float64, device=dev)
+    sb = torch.empty((b, 2), dtype=torch.float64, device=dev)
+    cap = n // 2 + 2
+    out = torch.zeros((b, cap, 3), dtype=torch.float64, device=dev)
+    cnt = torch.zeros(b, dtype=torch.int32, device=dev)
+    mse = torch.zeros(b, dtype=torch.float64, device=dev)
+    status = torch.zeros(b, dtype=torch.int32, device=dev)
+    s = nat.default_settings()
+
+    def run():
+        rc = nat.lib().mdg_deconvolute_batch_device(
+            ctx.handle, b, n, x.data_ptr(), n, y.data_ptr(), n, sb.data_ptr(), ctypes.byref(s),
+            None, 0, out.data_ptr(), cap, cnt.data_ptr(), mse.data_ptr(), status.data_ptr())
+        assert rc == 0
+        ctx.synchronize()
+        return [(int(status[k]), out[k, : int(cnt[k])].cpu().numpy().copy(), float(mse[k]))
+                for k in range(b)]
+
+    results = []
+    for batch in names:
+        cases = [load_case(nm) for nm in batch]
+        for k, (cx, cy, csb, _, _) in enumerate(cases):
+            x[k] = torch.from_numpy(cx)
+            y[k] = torch.from_numpy(cy)
+            sb[k] = torch.tensor(csb, dtype=torch.float64)
+        torch.cuda.synchronize()
+        got = run()
+        for (cx, cy, csb, cst, _), (st_, p, m) in zip(cases, got):
+            o = oracle.deconvolute(cx, cy, csb, cst)
+            assert st_ == o.status and np.array_equal(p, o.params)
+            assert abs(m - o.mse) <= MSE_RTOL * abs(o.mse)
+        results.append(got)
+    monkeypatch.setenv("MDG_GRAPHS", "0")
+    plain = run()  # last batch again, uncaptured
+    for (s1, p1, m1), (s2, p2, m2) in zip(results[-1], plain):
+        assert s1 == s2 and np.array_equal(p1, p2) and m1 == m2
