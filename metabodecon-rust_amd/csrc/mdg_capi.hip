@@ -239,7 +239,8 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
         w.smooth_stride = a.y_stride;
     }
     const int det_only = s->selector == MDG_SELECT_DETECTOR_ONLY;
-    const int gfit = std::max(1, std::min(64, 4096 / std::max(1, a.B)));
+    int gfit = 24;  // k_fit_sup workgroups per spectrum (3 * 2048 / 256)
+    if (const char* e = std::getenv("MDG_GFIT")) gfit = std::max(1, std::atoi(e));  // tuning
     const int gupd = std::max(1, std::min(16, 1024 / std::max(1, a.B)));
     const int nparts = std::max(1, std::min({1024, (a.N + 255) / 256, std::max(1, 4096 / a.B)}));
     // chain smoother buffers: raw sums of every pass, scaled outputs of passes

@@ -2134,8 +2134,11 @@ __device__ __forceinline__ void mse_region(const Workspace& w, int s, int r, int
 }
 
 template <int BS>
-__global__ __launch_bounds__(BS) void k_mse_partial(BatchArgs a, Workspace w) {
-    const int s = blockIdx.y;
+__global__ __launch_bounds__(BS) void k_mse_partial(BatchArgs a, Workspace w, int nparts) {
+    // 1-D grid, spectrum = block % B: round-robin dispatch puts blocks w and w+256 on
+    // the same CU, so the workgroups resident on a CU share one spectrum's
+    // Lorentzians in the scalar cache (B dividing 256) instead of streaming several
+    const int s = blockIdx.x % a.B, part = blockIdx.x / a.B;
     __shared__ double red[BS / 64];
     if (w.status[s] || w.mse_panic[s]) return;
     const int P = w.kept_count[s];
@@ -2151,8 +2154,7 @@ __global__ __launch_bounds__(BS) void k_mse_partial(BatchArgs a, Workspace w) {
     }
     const bool fast = w.x_ok[s] && w.unsafe_kept[s] == 0;
     double acc = 0.0;
-    for (int64_t v = (int64_t)blockIdx.x * BS + threadIdx.x; v < total;
-         v += (int64_t)gridDim.x * BS) {
+    for (int64_t v = (int64_t)part * BS + threadIdx.x; v < total; v += (int64_t)nparts * BS) {
         int64_t rem = v, idx = 0;
         for (int r = 0; r <= nig; ++r) {
             int64_t lo, hi;
@@ -2174,7 +2176,7 @@ __global__ __launch_bounds__(BS) void k_mse_partial(BatchArgs a, Workspace w) {
     if (threadIdx.x == 0) {
         double t = 0.0;
         for (int k = 0; k < BS / 64; ++k) t += red[k];
-        w.mse_part[(size_t)s * gridDim.x + blockIdx.x] = t;
+        w.mse_part[(size_t)s * nparts + part] = t;
     }
 }
 
@@ -2342,20 +2344,24 @@ void launch_fit_init(const BatchArgs& a, const Workspace& w, int gx, hipStream_t
     hipLaunchKernelGGL(k_fit_init, dim3(gx, a.B), dim3(256), 0, st, a, w);
 }
 void launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st) {
+    // measured (bench, P = 2048, ms per 10 launches): B=2 dpp 0.43 / plain 1.65;
+    // B=8 dpp 1.49 / plain 2.50; B=16 dpp 2.76 / plain 2.67; the split kernel lost
+    // everywhere (kept for MDG_FITSUP=split)
     const char* force = std::getenv("MDG_FITSUP");
     const std::string f = force ? force : "";
-    if ((!force && a.B <= 4) || f == "dpp") {
+    if ((!force && a.B <= 12) || f == "dpp") {
         // 32 points per workgroup: 192 workgroups at P = 2048, grid-stride beyond
         const int g = std::max(64, std::min(512, 1024 / a.B));
         hipLaunchKernelGGL(k_fit_sup_dpp, dim3(g, a.B), dim3(256), 0, st, a, w, it);
         return;
     }
-    if ((!force && a.B <= 16) || f == "split") {
+    if (f == "split") {
         // 16 points per 1024-thread workgroup: 3P/16 workgroups per spectrum (384 at
         // P = 2048) keep every CU busy; grid-stride beyond that
         const int g = std::max(64, std::min(1024, 2048 / a.B));
         hipLaunchKernelGGL((k_fit_sup_split<16, 128, 1024>), dim3(g, a.B), dim3(1024), 0, st, a, w, it);
     } else {
+        // gx 256-thread workgroups per spectrum (24: one point per thread at P = 2048)
         hipLaunchKernelGGL(k_fit_sup, dim3(gx, a.B), dim3(256), 0, st, a, w, it);
     }
 }
@@ -2366,7 +2372,7 @@ void launch_retain(const BatchArgs& a, const Workspace& w, hipStream_t st) {
     hipLaunchKernelGGL(k_retain<1024>, dim3(a.B), dim3(1024), 0, st, a, w);
 }
 void launch_mse(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st) {
-    hipLaunchKernelGGL(k_mse_partial<256>, dim3(nparts, a.B), dim3(256), 0, st, a, w);
+    hipLaunchKernelGGL(k_mse_partial<256>, dim3(nparts * a.B), dim3(256), 0, st, a, w, nparts);
 }
 void launch_mse_final(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st) {
     hipLaunchKernelGGL(k_mse_final, dim3(cdiv(a.B, 64)), dim3(64), 0, st, a, w, nparts);

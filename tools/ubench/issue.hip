@@ -26,7 +26,11 @@ constexpr int ITERS = 4096;
     "v_mov_b32 v10, 0\n v_mov_b32 v11, 0\n"                                   \
     "s_mov_b32 s64, 0\n s_mov_b32 s65, 0x3ff00000\n"                          \
     "s_mov_b32 s66, 0\n s_mov_b32 s67, 0x3fe00000\n"                          \
-    "s_mov_b32 s60, 0\n"
+    "s_mov_b32 s60, 0\n"                                                     \
+    "s_mov_b64 s[40:41], 0\n s_mov_b64 s[42:43], 0\n s_mov_b64 s[44:45], 0\n s_mov_b64 s[46:47], 0\n" \
+    "s_mov_b64 s[48:49], 0\n s_mov_b64 s[50:51], 0\n s_mov_b64 s[52:53], 0\n s_mov_b64 s[54:55], 0\n" \
+    "s_mov_b64 s[56:57], 0\n s_mov_b64 s[58:59], 0\n s_mov_b64 s[60:61], 0\n s_mov_b64 s[62:63], 0\n" \
+    "s_mov_b64 s[68:69], 0\n s_mov_b64 s[70:71], 0\n"
 
 #define LOOP(body)                                     \
     "s_mov_b32 s78, %[iters]\n"                        \
@@ -129,6 +133,9 @@ DEFK(t_fmac_dpp_x2, "v_fmac_f64_dpp v[0:1], v[2:3], v[4:5] row_newbcast:3 row_ma
 DEFK(t_add_s, "v_add_f64 v[0:1], v[0:1], s[64:65]\n", 0)
 DEFK(t_rl2_add, "v_readlane_b32 s68, v2, 5\n v_readlane_b32 s69, v3, 5\n v_add_f64 v[0:1], v[0:1], s[68:69]\n", 0)
 
+DEFK(t_grp_rot, "v_add_f64 v[0:1], v[14:15], s[40:41]\n v_add_f64 v[0:1], v[0:1], -s[50:51]\nv_add_f64 v[2:3], v[0:1], s[42:43]\n v_add_f64 v[2:3], v[2:3], -s[52:53]\nv_add_f64 v[4:5], v[2:3], s[44:45]\n v_add_f64 v[4:5], v[4:5], -s[54:55]\nv_add_f64 v[6:7], v[4:5], s[46:47]\n v_add_f64 v[6:7], v[6:7], -s[40:41]\nv_add_f64 v[8:9], v[6:7], s[48:49]\n v_add_f64 v[8:9], v[8:9], -s[42:43]\nv_add_f64 v[10:11], v[8:9], s[50:51]\n v_add_f64 v[10:11], v[10:11], -s[44:45]\nv_add_f64 v[12:13], v[10:11], s[52:53]\n v_add_f64 v[12:13], v[12:13], -s[46:47]\nv_add_f64 v[14:15], v[12:13], s[54:55]\n v_add_f64 v[14:15], v[14:15], -s[48:49]\n", 0)
+DEFK(t_grp_fix, "v_add_f64 v[0:1], v[0:1], s[40:41]\n v_add_f64 v[0:1], v[0:1], -s[50:51]\nv_add_f64 v[0:1], v[0:1], s[42:43]\n v_add_f64 v[0:1], v[0:1], -s[52:53]\nv_add_f64 v[0:1], v[0:1], s[44:45]\n v_add_f64 v[0:1], v[0:1], -s[54:55]\nv_add_f64 v[0:1], v[0:1], s[46:47]\n v_add_f64 v[0:1], v[0:1], -s[40:41]\nv_add_f64 v[0:1], v[0:1], s[48:49]\n v_add_f64 v[0:1], v[0:1], -s[42:43]\nv_add_f64 v[0:1], v[0:1], s[50:51]\n v_add_f64 v[0:1], v[0:1], -s[44:45]\nv_add_f64 v[0:1], v[0:1], s[52:53]\n v_add_f64 v[0:1], v[0:1], -s[46:47]\nv_add_f64 v[0:1], v[0:1], s[54:55]\n v_add_f64 v[0:1], v[0:1], -s[48:49]\n", 0)
+
 struct Test { const char* name; void (*k)(long long*, int*, const double*); int ticks_per_body; };
 
 int main() {
@@ -159,6 +166,8 @@ int main() {
         {"tick dep v_fmac_f64_dpp bcast", t_fmac_dpp, 1},
         {"tick 2 chains fmac_dpp (per instr)", t_fmac_dpp_x2, 2},
         {"tick dep add SGPR", t_add_s, 1},
+        {"tick grp8 rotating v+s", t_grp_rot, 8},
+        {"tick grp8 fixed v, rot s", t_grp_fix, 8},
         {"tick 2 readlane + add", t_rl2_add, 1},
         {"pair + gstore x4 same addr", t_pair_gst_same, 2},
         {"pair + gstore x4 lane addr", t_pair_gst_lane, 2},
