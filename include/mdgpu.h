@@ -165,6 +165,16 @@ int mdg_ctx_last_peaks(mdg_ctx* ctx, size_t spectrum, int which, int32_t* left,
  * moving-average smoother. */
 int mdg_ctx_last_smoothed(mdg_ctx* ctx, size_t spectrum, double* out, size_t n);
 
+/* Deconvoluter::optimize_settings (deconvoluter.rs:762-825): grid search over 27
+ * moving-average x 10 noise-score x 3 analytical-fit settings on the reference
+ * spectrum (x, y: n host values; sb0/sb1 and ignore as for mdg_deconvolute).
+ * *best receives the first setting of minimum MSE in the reference's order and
+ * *best_mse its MSE, summed in the reference's order. A failing combination
+ * returns its status (the reference's `?`). */
+int mdg_optimize_settings(mdg_ctx* ctx, const double* x, const double* y, size_t n, double sb0,
+                          double sb1, const double* ignore, size_t n_ignore, mdg_settings* best,
+                          double* best_mse);
+
 /* Lorentzian::superposition_vec: out[i] = sum_j L[j](x[i]) in slice order. */
 int mdg_superposition_vec(mdg_ctx* ctx, const double* x, size_t n, const mdg_lorentzian* L,
                           size_t p, double* out);

@@ -1575,7 +1575,7 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
         KSTAMP(18);
         const double sd = __builtin_sqrt(var);
         if (threadIdx.x == 0) {
-            thr_sh = mean + threshold * sd;
+            thr_sh = mean + (w.thr_s ? w.thr_s[s] : threshold) * sd;
             w.sfr_stats[2 * s] = mean;
             w.sfr_stats[2 * s + 1] = sd;
         }
@@ -1685,6 +1685,12 @@ __global__ void k_fit_init(BatchArgs a, Workspace w) {
 // K6  fit superposition at the 3P reduced points + ratio (fitter_analytical.rs:40-47)
 // Ping-pong range flags: iteration `it` reads unsafe[it&1] (written by the
 // producer of its parameters) and clears unsafe[(it+1)&1] for k_fit_update(it).
+// per-spectrum fit iteration counts (optimize_settings batches): a spectrum whose
+// count is reached skips the remaining superposition/update launches
+__device__ __forceinline__ bool fit_done(const Workspace& w, int s, int it) {
+    return w.fit_iters_s && it >= w.fit_iters_s[s];
+}
+
 __device__ __forceinline__ bool fit_fast(const Workspace& w, int s, int it) {
     if (blockIdx.x == 0 && threadIdx.x == 0) w.unsafe[2 * s + ((it + 1) & 1)] = 0;
     return w.x_ok[s] && w.unsafe[2 * s + (it & 1)] == 0;
@@ -1945,7 +1951,7 @@ __device__ __forceinline__ void fit_dpp_body(const BatchArgs& a, const Workspace
 __global__ __launch_bounds__(256) void k_fit_sup_dpp(BatchArgs a, Workspace w, int it) {
     __shared__ double lds_p[3 * kFitChunk];  // {sfhw, hw2, maxp} of one chunk of peaks
     const int s = blockIdx.y;
-    if (w.status[s]) return;
+    if (w.status[s] || fit_done(w, s, it)) return;
     const int P = w.sel_count[s];
     if (fit_fast(w, s, it)) fit_dpp_body<true>(a, w, s, P, lds_p);
     else fit_dpp_body<false>(a, w, s, P, lds_p);
@@ -1953,7 +1959,7 @@ __global__ __launch_bounds__(256) void k_fit_sup_dpp(BatchArgs a, Workspace w, i
 
 __global__ void k_fit_sup(BatchArgs a, Workspace w, int it) {
     const int s = blockIdx.y;
-    if (w.status[s]) return;
+    if (w.status[s] || fit_done(w, s, it)) return;
     const int P = w.sel_count[s];
     const size_t base = (size_t)s * w.capD;
     const double* __restrict__ params = w.params + 3 * base;
@@ -1982,7 +1988,7 @@ __global__ __launch_bounds__(BS) void k_fit_sup_split(BatchArgs a, Workspace w, 
     const int s = blockIdx.y;
     __shared__ double ev[3][J][Q];
     __shared__ double accs[Q];
-    if (w.status[s]) return;
+    if (w.status[s] || fit_done(w, s, it)) return;
     const int P = w.sel_count[s];
     const size_t base = (size_t)s * w.capD;
     const double* __restrict__ params = w.params + 3 * base;
@@ -2056,7 +2062,7 @@ __global__ __launch_bounds__(BS) void k_fit_sup_split(BatchArgs a, Workspace w, 
 // K7  stencil update + re-solve (fitter_analytical.rs:48-65)
 __global__ void k_fit_update(BatchArgs a, Workspace w, int it) {
     const int s = blockIdx.y;
-    if (w.status[s]) return;
+    if (w.status[s] || fit_done(w, s, it)) return;
     const int P = w.sel_count[s];
     const size_t base = (size_t)s * w.capD;
     for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
@@ -2206,6 +2212,32 @@ __global__ void k_mse_final(BatchArgs a, Workspace w, int nparts) {
 // standalone Lorentzian::superposition_vec (lorentzian.rs:631-663)
 // ----------------------------------------------------------------------------------
 // range pre-pass: flag[0] = number of Lorentzians / x values outside the fast ranges
+// ----------------------------------------------------------------------------------
+// Exact MSE (deconvoluter.rs:846-861 in the reference's order): squared residuals,
+// then one wave folds each region left to right (dpp_fold) and the region sums in
+// region order. Used by optimize_settings to settle near-ties of the tree MSE.
+// ----------------------------------------------------------------------------------
+__global__ void k_sq_residuals(const double* __restrict__ sup, const double* __restrict__ y,
+                               int64_t n, double* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        const double d = sup[i] - y[i];
+        out[i] = d * d;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_exact_fold(const double* __restrict__ t, ExactRegions r,
+                                                   double* __restrict__ out) {
+    double total = -0.0;
+    int64_t len = 0;
+    for (int k = 0; k < r.n; ++k) {
+        const int64_t lo = r.lo[k], hi = r.hi[k];
+        total += dpp_fold(-0.0, t + lo, (int)(hi - lo));
+        len += hi - lo;
+    }
+    if (threadIdx.x == 0) out[0] = total / (double)len;
+}
+
 __global__ void k_range_check(const double* __restrict__ x, int64_t n,
                               const double* __restrict__ params, int P, int* flag) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < P;
@@ -2376,6 +2408,11 @@ void launch_mse(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t 
 }
 void launch_mse_final(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st) {
     hipLaunchKernelGGL(k_mse_final, dim3(cdiv(a.B, 64)), dim3(64), 0, st, a, w, nparts);
+}
+void launch_mse_exact(const double* sup, const double* y, int64_t n, const ExactRegions& r,
+                      double* scratch, double* out, hipStream_t st) {
+    hipLaunchKernelGGL(k_sq_residuals, dim3(cdiv(n, 256)), dim3(256), 0, st, sup, y, n, scratch);
+    hipLaunchKernelGGL(k_exact_fold, dim3(1), dim3(64), 0, st, scratch, r, out);
 }
 void launch_superposition_vec(const double* x, int64_t n, const double* params, int P,
                               double* out, int* flag, hipStream_t st) {

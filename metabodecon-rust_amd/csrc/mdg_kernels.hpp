@@ -79,12 +79,24 @@ struct Workspace {
     int32_t* chain_flags;     // B x P x 32: published output blocks of (s, p) (own 128-B line)
     int64_t chain_stride;
     int chain_P;              // passes the chain buffers hold (0 = not allocated)
+    // per-spectrum overrides (optimize_settings batches; null = the batch settings)
+    const double* thr_s;      // B noise-score thresholds
+    const int32_t* fit_iters_s;  // B fit iteration counts (<= the launched count)
 };
 
 // Bytes of the k_smooth_chain buffers for (B, N, passes) and their row stride.
 int64_t chain_stride_for(int N, int ws);
 size_t chain_bytes(int B, int N, int ws, int passes);
 bool chain_supported(int B, int N, int iters, int ws);
+
+// MSE regions (start, end) of one spectrum for the exact MSE
+struct ExactRegions {
+    int n;
+    int64_t lo[kMaxIgnore + 1];
+    int64_t hi[kMaxIgnore + 1];
+};
+void launch_mse_exact(const double* sup, const double* y, int64_t n, const ExactRegions& r,
+                      double* scratch, double* out, hipStream_t st);
 
 void launch_prep(const BatchArgs& a, const Workspace& w, hipStream_t st);
 void launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int ws, hipStream_t st);

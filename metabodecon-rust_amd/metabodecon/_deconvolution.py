@@ -368,26 +368,29 @@ class Deconvoluter:
         return self.deconvolute_spectra(spectra)
 
     def optimize_settings(self, reference: Spectrum) -> float:
-        """deconvoluter.rs:762-825: grid of 27 smoothing x 10 selection x 3 fitting
-        settings, keep the first minimum MSE. Each combination runs on the GPU."""
-        smoothing = [(it, ws) for it in range(2, 11) for ws in (3, 5, 7)]
-        selection = [5.0 + (c * (8.0 - 5.0)) / 9.0 for c in range(10)]
-        fitting = [5, 10, 15]
-        best = None
-        for it, ws in smoothing:
-            for thr in selection:
-                for fit in fitting:
-                    d = Deconvoluter()
-                    d._ignore = self._ignore
-                    d.device = self.device
-                    d.set_moving_average_smoother(it, ws)
-                    d.set_noise_score_selector(thr)
-                    d.set_analytical_fitter(fit)
-                    res = d.deconvolute_spectrum(reference)
-                    if best is None or res.mse < best[0]:
-                        best = (res.mse, it, ws, thr, fit)
-        mse, it, ws, thr, fit = best
-        self.set_moving_average_smoother(it, ws)
-        self.set_noise_score_selector(thr)
-        self.set_analytical_fitter(fit)
-        return mse
+        """Deconvoluter::optimize_settings (deconvoluter.rs:762-825): grid of 27
+        smoothing x 10 noise-score x 3 analytical-fit settings on ``reference``;
+        keeps the first setting of minimum MSE and returns that MSE. Runs as 27
+        batched GPU pipelines (mdg_optimize_settings); near-ties of the batched
+        MSE are settled with the reference's exact summation order."""
+        if not isinstance(reference, Spectrum):
+            raise TypeError("expected metabodecon.Spectrum")
+        ign = self._ignore_array()
+        ctx = nat.context(self.device)
+        best = nat.Settings()
+        mse = ctypes.c_double(0.0)
+        sb0, sb1 = reference.signal_boundaries
+        with ctx.lock:
+            rc = nat.lib().mdg_optimize_settings(
+                ctx.handle, nat.ptr(np.ascontiguousarray(reference.chemical_shifts)),
+                nat.ptr(np.ascontiguousarray(reference.intensities)), len(reference), sb0, sb1,
+                nat.ptr(ign) if ign.size else None, ign.size // 2, ctypes.byref(best),
+                ctypes.byref(mse))
+        if rc >= 100 or rc == nat.INVALID_ARGUMENT:
+            raise exc.UnexpectedError(f"GPU engine failure: {nat.strerror(rc)}")
+        if rc:
+            raise exc.from_status(rc)
+        self.set_moving_average_smoother(int(best.smooth_iterations), int(best.smooth_window))
+        self.set_noise_score_selector(float(best.threshold))
+        self.set_analytical_fitter(int(best.fit_iterations))
+        return float(mse.value)

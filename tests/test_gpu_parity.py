@@ -383,3 +383,38 @@ def test_device_graph_replay(ctx, monkeypatch):
     plain = run()  # last batch again, uncaptured
     for (s1, p1, m1), (s2, p2, m2) in zip(results[-1], plain):
         assert s1 == s2 and np.array_equal(p1, p2) and m1 == m2
+
+
+@pytest.mark.parametrize("name", ["sim_01", "sim_07"])
+def test_optimize_settings_matches_exhaustive_oracle(name):
+    """Deconvoluter.optimize_settings (GPU: 27 batched pipelines + exact tie
+    check) picks the same setting as an exhaustive oracle search over the
+    reference's 810 combinations (first minimum, deconvoluter.rs:762-825) and
+    returns that setting's MSE bit for bit (summed in the reference's order)."""
+    import metabodecon as md
+    from metabodecon import exceptions as mexc
+    x, y, sb, _, ign = load_case(name)
+    best, first_err = None, None
+    for it in range(2, 11):
+        for ws in (3, 5, 7):
+            for c in range(10):
+                thr = 5.0 + (c * (8.0 - 5.0)) / 9.0
+                for fit in (5, 10, 15):
+                    st = oracle.make_settings(smooth_iterations=it, smooth_window=ws, threshold=thr,
+                                              fit_iterations=fit)
+                    r = oracle.deconvolute(x, y, sb, st, ignore=ign)
+                    if r.status and first_err is None:
+                        first_err = r.status
+                    if r.status == 0 and (best is None or r.mse < best[0]):
+                        best = (r.mse, it, ws, thr, fit)
+    d = md.Deconvoluter()
+    spec = md.Spectrum(x, y, sb)
+    if first_err is not None:
+        with pytest.raises(mexc.DeconvolutionError):
+            d.optimize_settings(spec)
+        return
+    mse = d.optimize_settings(spec)
+    assert mse == best[0]
+    s = d.settings
+    assert (s.smooth_iterations, s.smooth_window, s.fit_iterations) == (best[1], best[2], best[4])
+    assert s.threshold == best[3]
