@@ -9,12 +9,12 @@ the same operation order as lorentzian.rs:546-611.
 from __future__ import annotations
 
 import ctypes
-import json
 import math
 
 import numpy as np
 
 from . import _native as nat
+from . import _serde as serde
 from . import exceptions as exc
 from ._spectrum import Spectrum
 
@@ -123,34 +123,68 @@ def superposition_vec(x, params: np.ndarray, device: int | None = None) -> np.nd
 
 
 # =====================================================================================
-# settings serialisation (serde forms, smoother.rs/selector.rs/fitter.rs)
+# settings serialisation (serde forms of smoother.rs:21-56, selector.rs:26-58,
+# scorer.rs:15-29, fitter.rs:28-57: internally tagged on "method", camelCase fields)
 # =====================================================================================
-def _settings_json(s: nat.Settings) -> tuple[dict, dict, dict]:
+_U32_MAX = (1 << 32) - 1
+
+
+def _settings_serde(s: nat.Settings, as_array: bool) -> list:
+    if as_array:  # rmp_serde: [tag, fields...]
+        sm = (["MovingAverage", s.smooth_iterations, s.smooth_window] if s.smoother == 1
+              else ["Identity"])
+        se = (["NoiseScoreFilter", ["MinimumSum"], s.threshold] if s.selector == 1
+              else ["DetectorOnly"])
+        return [sm, se, ["Analytical", s.fit_iterations]]
     sm = ({"method": "MovingAverage", "iterations": s.smooth_iterations,
            "windowSize": s.smooth_window} if s.smoother == 1 else {"method": "Identity"})
     se = ({"method": "NoiseScoreFilter", "scoringMethod": {"method": "MinimumSum"},
            "threshold": s.threshold} if s.selector == 1 else {"method": "DetectorOnly"})
-    fi = {"method": "Analytical", "iterations": s.fit_iterations}
-    return sm, se, fi
+    return [sm, se, {"method": "Analytical", "iterations": s.fit_iterations}]
 
 
-def _settings_from_json(sm: dict, se: dict, fi: dict) -> nat.Settings:
+def _engine_u32(v: int, what: str) -> int:
+    if v > _U32_MAX:
+        raise serde.SerdeError(f"{what} = {v} exceeds the engine's u32 settings field")
+    return v
+
+
+def _settings_from_serde(sm, se, fi) -> nat.Settings:
     s = nat.default_settings()
-    if sm["method"] == "Identity":
+    tag, rest = serde.tagged(sm, "SmoothingSettings")
+    if tag == "Identity":
         s.smoother = 0
-    else:
+    elif tag == "MovingAverage":
+        f = serde.fields(rest, ("iterations", "windowSize"), "SmoothingSettings::MovingAverage")
         s.smoother = 1
-        s.smooth_iterations = int(sm["iterations"])
-        s.smooth_window = int(sm["windowSize"])
-    if se["method"] == "DetectorOnly":
-        s.selector = 0
+        s.smooth_iterations = _engine_u32(serde.usize(f["iterations"], "iterations"),
+                                          "iterations")
+        s.smooth_window = _engine_u32(serde.usize(f["windowSize"], "windowSize"), "windowSize")
     else:
+        raise serde.SerdeError(f"unknown variant `{tag}`, expected `Identity` or `MovingAverage`")
+    tag, rest = serde.tagged(se, "SelectionSettings")
+    if tag == "DetectorOnly":
+        s.selector = 0
+    elif tag == "NoiseScoreFilter":
+        f = serde.fields(rest, ("scoringMethod", "threshold"),
+                         "SelectionSettings::NoiseScoreFilter")
+        stag, _ = serde.tagged(f["scoringMethod"], "ScoringMethod")
+        if stag != "MinimumSum":
+            raise serde.SerdeError(f"unknown variant `{stag}`, expected `MinimumSum`")
         s.selector = 1
-        s.threshold = float(se["threshold"])
-    s.fit_iterations = int(fi["iterations"])
+        s.threshold = serde.f64(f["threshold"], "threshold")
+    else:
+        raise serde.SerdeError(
+            f"unknown variant `{tag}`, expected `DetectorOnly` or `NoiseScoreFilter`")
+    tag, rest = serde.tagged(fi, "FittingSettings")
+    if tag != "Analytical":
+        raise serde.SerdeError(f"unknown variant `{tag}`, expected `Analytical`")
+    f = serde.fields(rest, ("iterations",), "FittingSettings::Analytical")
+    s.fit_iterations = _engine_u32(serde.usize(f["iterations"], "iterations"), "iterations")
+    # TryFrom<SerializedDeconvolution> validates (serialized_deconvolution.rs:34-49)
     st = nat.validate(s)
     if st:
-        raise exc.from_status(st)
+        raise serde.SerdeError(str(exc.from_status(st)))
     return s
 
 
@@ -190,32 +224,72 @@ class Deconvolution:
     def par_superposition_vec(self, x) -> np.ndarray:
         return superposition_vec(x, self._params)
 
-    # serde JSON form of serialized_deconvolution.rs:18-31 / serialized_lorentzian.rs:16-43
-    def to_json_dict(self) -> dict:
-        sm, se, fi = _settings_json(self._settings)
+    # ---- serialisation (bindings/deconvolution.rs:77-116) ------------------------------
+    def _serialized(self, as_array: bool):
+        """SerializedDeconvolution (serialized_deconvolution.rs:9-31) with
+        SerializedLorentzian {sf, hw, maxp} = (sfhw / sqrt(hw2), sqrt(hw2), maxp)
+        (serialized_lorentzian.rs:5-21, lorentzian.rs:406-430)."""
+        sm, se, fi = _settings_serde(self._settings, as_array)
         lz = []
         for sfhw, hw2, maxp in self._params.tolist():
             hw = math.sqrt(hw2)
-            lz.append({"sf": sfhw / hw, "hw": hw, "maxp": maxp})
+            sf = sfhw / hw
+            lz.append([sf, hw, maxp] if as_array else {"sf": sf, "hw": hw, "maxp": maxp})
+        if as_array:
+            return [sm, se, fi, self._mse, lz]
         return {"smoothingSettings": sm, "selectionSettings": se, "fittingSettings": fi,
                 "mse": self._mse, "lorentzians": lz}
 
+    def to_json_dict(self) -> dict:
+        return self._serialized(as_array=False)
+
+    @staticmethod
+    def _from_serialized(v) -> "Deconvolution":
+        d = serde.fields(v, ("smoothingSettings", "selectionSettings", "fittingSettings", "mse",
+                             "lorentzians"), "Deconvolution")
+        s = _settings_from_serde(d["smoothingSettings"], d["selectionSettings"],
+                                 d["fittingSettings"])
+        mse = serde.f64(d["mse"], "mse")
+        if not isinstance(d["lorentzians"], list):
+            raise serde.SerdeError("invalid type for lorentzians: expected a sequence")
+        rows = []
+        for l in d["lorentzians"]:
+            f = serde.fields(l, ("sf", "hw", "maxp"), "Lorentzian")
+            sf, hw, maxp = (serde.f64(f[k], k) for k in ("sf", "hw", "maxp"))
+            # Lorentzian::new(sf * hw, hw.powi(2), maxp) (serialized_lorentzian.rs:23-27)
+            rows.append((sf * hw, hw * hw, maxp))
+        return Deconvolution(np.array(rows, dtype=np.float64).reshape(-1, 3), mse, s)
+
     def write_json(self, path: str) -> None:
-        with open(path, "w") as f:
-            json.dump(self.to_json_dict(), f, indent=2)
+        text = serde.to_string_pretty(self._serialized(as_array=False))
+        with open(path, "wb") as f:
+            f.write(text.encode("utf-8"))
 
     @staticmethod
     def read_json(path: str) -> "Deconvolution":
+        with open(path, "rb") as f:
+            raw = f.read()
         try:
-            with open(path) as f:
-                d = json.load(f)
-            s = _settings_from_json(d["smoothingSettings"], d["selectionSettings"],
-                                    d["fittingSettings"])
-            p = np.array([[l["sf"] * l["hw"], l["hw"] * l["hw"], l["maxp"]]
-                          for l in d["lorentzians"]], dtype=np.float64).reshape(-1, 3)
-            return Deconvolution(p, d["mse"], s)
-        except (KeyError, TypeError, ValueError) as e:
-            raise exc.SerializationError(str(e)) from None
+            text = raw.decode("utf-8")
+        except UnicodeDecodeError as e:
+            raise OSError("stream did not contain valid UTF-8") from e
+        try:
+            return Deconvolution._from_serialized(serde.from_str(text))
+        except serde.SerdeError as e:
+            raise serde.serialization_error(e) from None
+
+    def write_bin(self, path: str) -> None:
+        with open(path, "wb") as f:
+            f.write(serde.to_msgpack(self._serialized(as_array=True)))
+
+    @staticmethod
+    def read_bin(path: str) -> "Deconvolution":
+        with open(path, "rb") as f:
+            raw = f.read()
+        try:
+            return Deconvolution._from_serialized(serde.from_msgpack(raw))
+        except serde.SerdeError as e:
+            raise serde.serialization_error(e) from None
 
     def __repr__(self) -> str:
         return f"Deconvolution(lorentzians={self._params.shape[0]}, mse={self._mse!r})"

@@ -3,16 +3,24 @@
 Construction enforces the invariants of spectrum/spectrum.rs:120-150 and
 :779-890 (lengths, uniform spacing, finite intensities, boundaries ordered per
 monotonicity and inside the axis), so every spectrum handed to the GPU engine
-is one the reference would also accept.
+is one the reference would also accept. Metadata follows spectrum/meta/
+(nucleus.rs, reference.rs): the nucleus is normalised through ``Nucleus::from``
+and shown with its ``Display`` string; the reference compound is validated as
+the binding's setter does (bindings/spectrum.rs:155-191). Serialisation is the
+reference's ``SerializedSpectrum`` (serialized_spectrum.rs:7-55) through
+``_serde``.
 """
 from __future__ import annotations
 
 import math
+import operator
 
 import numpy as np
 
+from . import _serde as serde
 from . import exceptions as exc
 from ._bruker import MetadataError, bruker_set_paths, read_bruker_arrays
+from ._jcampdx import RUST_WS, JcampError, jcampdx_set_paths, read_jcampdx_arrays
 
 CHECK_PRECISION = 1.0e3 * 2.220446049250313e-16  # lib.rs:277
 
@@ -27,6 +35,66 @@ def _monotonicity(first: float, second: float) -> str | None:
     if first > second:
         return "decreasing"
     return None
+
+
+# spectrum/meta/nucleus.rs:20-73: accepted spellings -> Display string
+_NUCLEI = {
+    "1H": "1H", "PROTON": "1H", "HYDROGEN1": "1H",
+    "11B": "11B", "BORON11": "11B",
+    "13C": "13C", "CARBON13": "13C",
+    "15N": "15N", "NITROGEN15": "15N",
+    "19F": "19F", "FLUORINE19": "19F",
+    "29SI": "29Si", "SILICON29": "29Si",
+    "31P": "31P", "PHOSPHORUS31": "31P",
+}
+_RUST_WS = RUST_WS  # char::is_whitespace, for str::trim
+
+
+def nucleus_display(value: str) -> str:
+    """``Nucleus::from(value).to_string()`` (nucleus.rs:22-46, :57-72)."""
+    key = value.strip(_RUST_WS)
+    for ch in " ^-_":
+        key = key.replace(ch, "")
+    return _NUCLEI.get(key.upper(), value)
+
+
+def referencing_method(value: str) -> str | None:
+    """``ReferencingMethod::from_str`` (reference.rs:15-35) as its Display string."""
+    return {"INTERNAL": "internal", "EXTERNAL": "external"}.get(value.strip(_RUST_WS).upper())
+
+
+def _extract_f64(v, what: str) -> float:
+    # pyo3 f64 extraction: floats and ints (anything with __float__/__index__), not str
+    if isinstance(v, (str, bytes)):
+        raise TypeError(f"'{type(v).__name__}' object cannot be converted to 'PyFloat' ({what})")
+    return float(v)
+
+
+def _extract_usize(v, what: str) -> int:
+    i = operator.index(v)  # TypeError for floats / str, as pyo3
+    if i < 0:
+        raise OverflowError(f"can't convert negative int to unsigned ({what})")
+    if i >= 1 << 64:
+        raise OverflowError(f"int too big to convert ({what})")
+    return i
+
+
+def _validate_boundaries(sb, cs: np.ndarray, mono: str) -> tuple[float, float]:
+    """validate_boundaries (spectrum.rs:840-890): ordered per monotonicity, inside the axis."""
+    sb = (float(sb[0]), float(sb[1]))
+    width = sb[0] - sb[1]
+    rng = (float(cs[0]), float(cs[-1]))
+    if abs(width) < CHECK_PRECISION or not math.isfinite(width):
+        raise exc.InvalidSignalBoundaries(f"signal boundaries {sb} invalid for range {rng}")
+    if mono == "increasing":
+        sb = (min(sb), max(sb))
+        if sb[0] < rng[0] or sb[1] > rng[1]:
+            raise exc.InvalidSignalBoundaries(f"signal boundaries {sb} outside range {rng}")
+    else:
+        sb = (max(sb), min(sb))
+        if sb[0] > rng[0] or sb[1] < rng[1]:
+            raise exc.InvalidSignalBoundaries(f"signal boundaries {sb} outside range {rng}")
+    return sb
 
 
 class Spectrum:
@@ -59,29 +127,17 @@ class Spectrum:
         if mono is None:  # pragma: no cover - excluded by validate_spacing
             raise exc.NonUniformSpacing("chemical shifts are not monotonic")
         # validate_boundaries (spectrum.rs:840-890)
-        sb = (float(signal_boundaries[0]), float(signal_boundaries[1]))
-        width = sb[0] - sb[1]
-        rng = (float(cs[0]), float(cs[-1]))
-        if abs(width) < CHECK_PRECISION or not math.isfinite(width):
-            raise exc.InvalidSignalBoundaries(f"signal boundaries {sb} invalid for range {rng}")
-        if mono == "increasing":
-            sb = (min(sb), max(sb))
-            if sb[0] < rng[0] or sb[1] > rng[1]:
-                raise exc.InvalidSignalBoundaries(f"signal boundaries {sb} outside range {rng}")
-        else:
-            sb = (max(sb), min(sb))
-            if sb[0] > rng[0] or sb[1] < rng[1]:
-                raise exc.InvalidSignalBoundaries(f"signal boundaries {sb} outside range {rng}")
+        sb = _validate_boundaries(signal_boundaries, cs, mono)
         cs.setflags(write=False)
         it.setflags(write=False)
         self._cs = cs
         self._it = it
         self._sb = sb
         self._mono = mono
-        self.nucleus = "1H"
-        self.frequency = 1.0
-        self.reference_compound = {"chemical_shift": float(cs[0]), "index": 0, "name": None,
-                                   "method": None}
+        # defaults of Spectrum::new (spectrum.rs:140-150): 1H, 1.0, (x_0, index 0)
+        self._nucleus = "1H"
+        self._frequency = 1.0
+        self._reference = (float(cs[0]), 0, None, None)
 
     # ---- accessors (spectrum.rs:225-260, :633-635, :741-746) ------------------------
     @property
@@ -95,6 +151,58 @@ class Spectrum:
     @property
     def signal_boundaries(self) -> tuple[float, float]:
         return self._sb
+
+    @signal_boundaries.setter
+    def signal_boundaries(self, signal_boundaries) -> None:
+        # bindings/spectrum.rs:134-143 -> Spectrum::set_signal_boundaries
+        self._sb = _validate_boundaries(signal_boundaries, self._cs, self._mono)
+
+    @property
+    def nucleus(self) -> str:
+        return self._nucleus
+
+    @nucleus.setter
+    def nucleus(self, nucleus: str) -> None:
+        if not isinstance(nucleus, str):
+            raise TypeError(f"'{type(nucleus).__name__}' object cannot be converted to 'PyString'")
+        self._nucleus = nucleus_display(nucleus)
+
+    @property
+    def frequency(self) -> float:
+        return self._frequency
+
+    @frequency.setter
+    def frequency(self, frequency: float) -> None:
+        self._frequency = _extract_f64(frequency, "frequency")
+
+    @property
+    def reference_compound(self) -> dict:
+        cs, index, name, method = self._reference
+        return {"chemical_shift": cs, "index": index, "name": name, "method": method}
+
+    @reference_compound.setter
+    def reference_compound(self, reference: dict) -> None:
+        # bindings/spectrum.rs:155-191
+        if not isinstance(reference, dict):
+            raise TypeError(f"'{type(reference).__name__}' object cannot be converted to 'PyDict'")
+        cs = _extract_f64(reference["chemical_shift"], "chemical_shift")
+        index = _extract_usize(reference["index"], "index")
+        name = reference.get("name")
+        if name is not None and not isinstance(name, str):
+            raise TypeError("reference compound name must be a string")
+        method = reference.get("method")
+        if method is not None:
+            if not isinstance(method, str):
+                raise TypeError("referencing method must be a string")
+            parsed = referencing_method(method)
+            if parsed is None:
+                raise ValueError("referencing method must be either 'external' or 'internal'")
+            method = parsed
+        self._reference = (cs, index, name, method)
+
+    def range(self) -> tuple[float, float]:
+        """(first, last) chemical shift (spectrum.rs:633-635)."""
+        return (float(self._cs[0]), float(self._cs[-1]))
 
     @property
     def monotonicity(self) -> str:
@@ -132,6 +240,120 @@ class Spectrum:
                         signal_boundaries) -> list["Spectrum"]:
         return [Spectrum.read_bruker(p, experiment, processing, signal_boundaries)
                 for p in bruker_set_paths(path)]
+
+
+    @staticmethod
+    def read_jcampdx(path: str, signal_boundaries) -> "Spectrum":
+        """bindings/spectrum.rs:69-75 -> JcampDx::read_spectrum (jcampdx.rs:555-590)."""
+        try:
+            cs, it, header = read_jcampdx_arrays(path)
+        except JcampError as e:
+            if e.kind == "UnsupportedJcampDxFile":  # not mapped by error.rs
+                raise exc.UnexpectedError(f"unexpected error: {e}") from None
+            raise getattr(exc, e.kind, exc.SpectrumError)(str(e)) from None
+        except UnicodeDecodeError as e:  # read_to_string -> io::Error -> PyIOError
+            raise OSError(f"stream did not contain valid UTF-8: {path}") from e
+        s = Spectrum(cs, it, signal_boundaries)
+        s.nucleus = header["nucleus"]
+        s.frequency = header["frequency"]
+        ref = header["reference"]
+        if ref is not None:
+            s._reference = (ref["chemical_shift"], ref["index"], ref["name"], ref["method"])
+        return s
+
+    @staticmethod
+    def read_jcampdx_set(path: str, signal_boundaries) -> list["Spectrum"]:
+        return [Spectrum.read_jcampdx(p, signal_boundaries) for p in jcampdx_set_paths(path)]
+
+    # ---- serialisation (bindings/spectrum.rs:193-232, serialized_spectrum.rs) --------
+    def _serialized(self, as_array: bool):
+        cs, index, name, method = self._reference
+        if as_array:  # rmp_serde: structs as arrays, skipped Options omitted
+            ref = [cs, index] + ([name] if name is not None else []) \
+                + ([method] if method is not None else [])
+            return [list(self.range()), list(self._sb), int(self._cs.size), self._nucleus,
+                    self._frequency, ref, self._it.tolist()]
+        ref = {"chemicalShift": cs, "index": index}
+        if name is not None:
+            ref["name"] = name
+        if method is not None:
+            ref["method"] = method
+        return {"spectrumBoundaries": list(self.range()), "signalBoundaries": list(self._sb),
+                "size": int(self._cs.size), "nucleus": self._nucleus,
+                "frequency": self._frequency, "referenceCompound": ref,
+                "intensities": self._it.tolist()}
+
+    @staticmethod
+    def _from_serialized(v) -> "Spectrum":
+        d = serde.fields(v, ("spectrumBoundaries", "signalBoundaries", "size", "nucleus",
+                             "frequency", "referenceCompound", "intensities"), "Spectrum")
+
+        def pair(x, what):
+            if not isinstance(x, list) or len(x) != 2:
+                raise serde.SerdeError(f"invalid value for {what}: expected a tuple of size 2")
+            return (serde.f64(x[0], what), serde.f64(x[1], what))
+
+        start, end = pair(d["spectrumBoundaries"], "spectrumBoundaries")
+        sb = pair(d["signalBoundaries"], "signalBoundaries")
+        size = serde.usize(d["size"], "size")
+        nucleus = serde.string(d["nucleus"], "nucleus")
+        frequency = serde.f64(d["frequency"], "frequency")
+        r = serde.fields(d["referenceCompound"], ("chemicalShift", "index", "name", "method"),
+                         "ReferenceCompound", optional=("name", "method"))
+        ref_cs = serde.f64(r["chemicalShift"], "chemicalShift")
+        ref_index = serde.usize(r["index"], "index")
+        name = None if r["name"] is None else serde.string(r["name"], "name")
+        method = None
+        if r["method"] is not None:
+            method = serde.string(r["method"], "method")
+            if method not in ("internal", "external"):  # rename_all = "camelCase"
+                raise serde.SerdeError(f"unknown variant `{method}`, expected `internal` or "
+                                       "`external`")
+        if not isinstance(d["intensities"], list):
+            raise serde.SerdeError("invalid type for intensities: expected a sequence")
+        it = [serde.f64(x, "intensities") for x in d["intensities"]]
+        # TryFrom<SerializedSpectrum> (serialized_spectrum.rs:35-55)
+        step = (end - start) / (float(size) - 1.0)
+        cs = start + np.arange(size, dtype=np.float64) * step
+        try:
+            s = Spectrum(cs, it, sb)
+        except exc.SpectrumError as e:
+            raise serde.SerdeError(str(e)) from None
+        s._nucleus = nucleus_display(nucleus)
+        s._frequency = frequency
+        s._reference = (ref_cs, ref_index, name, method)
+        return s
+
+    def write_json(self, path: str) -> None:
+        text = serde.to_string_pretty(self._serialized(as_array=False))
+        with open(path, "wb") as f:
+            f.write(text.encode("utf-8"))
+
+    @staticmethod
+    def read_json(path: str) -> "Spectrum":
+        with open(path, "rb") as f:
+            raw = f.read()
+        try:
+            text = raw.decode("utf-8")
+        except UnicodeDecodeError as e:
+            raise OSError("stream did not contain valid UTF-8") from e
+        try:
+            return Spectrum._from_serialized(serde.from_str(text))
+        except serde.SerdeError as e:
+            raise serde.serialization_error(e) from None
+
+    def write_bin(self, path: str) -> None:
+        with open(path, "wb") as f:
+            f.write(serde.to_msgpack(self._serialized(as_array=True)))
+
+    @staticmethod
+    def read_bin(path: str) -> "Spectrum":
+        with open(path, "rb") as f:
+            raw = f.read()
+        try:
+            return Spectrum._from_serialized(serde.from_msgpack(raw))
+        except serde.SerdeError as e:
+            raise serde.serialization_error(e) from None
 
     def __repr__(self) -> str:
         return (f"Spectrum(n={self._cs.size}, range=({self._cs[0]}, {self._cs[-1]}), "

@@ -418,3 +418,37 @@ def test_optimize_settings_matches_exhaustive_oracle(name):
     s = d.settings
     assert (s.smooth_iterations, s.smooth_window, s.fit_iterations) == (best[1], best[2], best[4])
     assert s.threshold == best[3]
+
+
+def test_jcampdx_and_serde_inputs_through_the_device(tmp_path):
+    """Rows f3/f4 feeding the hot path: a spectrum read from the reference's
+    JCAMP-DX file, and the same spectrum after a MessagePack and a JSON round
+    trip (axis rebuilt as start + i * step), deconvolute bit-identically to the
+    oracle on the same arrays; the Deconvolution written as MessagePack reads
+    back as Lorentzian::new(sf * hw, hw^2, maxp)."""
+    import gzip
+    import shutil
+    import metabodecon as md
+    src = os.path.join(GOLDEN, "jcampdx", "blood_01.dx.gz")
+    p = str(tmp_path / "blood_01.dx")
+    with gzip.open(src, "rb") as g, open(p, "wb") as f:
+        shutil.copyfileobj(g, f)
+    s = md.Spectrum.read_jcampdx(p, (-2.2, 11.8))
+    s.write_bin(str(tmp_path / "s.bin"))
+    s.write_json(str(tmp_path / "s.json"))
+    dec = md.Deconvoluter()
+    dec.add_ignore_region((4.7, 4.9))
+    for sp in (s, md.Spectrum.read_bin(str(tmp_path / "s.bin")),
+               md.Spectrum.read_json(str(tmp_path / "s.json"))):
+        d = dec.deconvolute_spectrum(sp)
+        o = oracle.deconvolute(sp.chemical_shifts, sp.intensities, sp.signal_boundaries,
+                               ignore=[(4.7, 4.9)], threads=16)
+        assert o.status == 0
+        assert np.array_equal(d.params, o.params)
+        assert abs(d.mse - o.mse) <= MSE_RTOL * abs(o.mse)
+    d.write_bin(str(tmp_path / "d.bin"))
+    r = md.Deconvolution.read_bin(str(tmp_path / "d.bin"))
+    hw = np.sqrt(d.params[:, 1])
+    sf = d.params[:, 0] / hw
+    assert np.array_equal(r.params, np.stack([sf * hw, hw * hw, d.params[:, 2]], axis=1))
+    assert r.mse == d.mse
