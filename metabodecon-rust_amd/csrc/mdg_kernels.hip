@@ -682,14 +682,19 @@ __global__ __launch_bounds__(512) void k_smooth_waves(BatchArgs a, Workspace w, 
 // cycles, any other instruction of the same wave 3-10 more, an s_load_dwordx16
 // plus its wait almost nothing when it feeds 8 ticks, and one CU issues one
 // 16-byte vector store per ~16 cycles across all its waves. So each pass runs
-// on its own CU as a "chain" wave that issues little besides the reference's two
-// dependent adds per tick (moving_average.rs:69-80, in j = i + R form below),
-// with SGPR operands and one 16-byte store of raw sums per two ticks. A second
-// "helper" wave per workgroup prefetches input blocks into the scalar cache,
-// multiplies the raw sums by the reference's 1/len (moving_average.rs:66-81:
-// 1/len while the buffer grows, 1/ws, then 1/len in the tail), and publishes
-// finished blocks to the next pass (sc1 stores, vmcnt(0), sc1 counter; the
-// consumer polls with sc1 loads -- MI355X_MICROARCH.md, cross-CU hand-offs).
+// on its own CU, in three waves:
+//  * chain wave: issues little besides the reference's two dependent adds per
+//    tick (moving_average.rs:69-80, in j = i + R form below) on SGPR operands,
+//    and stores one checkpoint per 8 ticks (the group's last raw sum);
+//  * feeder wave: waits for the previous pass's published blocks (sc1 polls),
+//    pulls them into L2 and touches them into the scalar cache, and publishes
+//    in_ready in LDS;
+//  * scaler wave: replays each group of 8 ticks from its checkpoint with the same
+//    two operations (bit-identical sums), multiplies by the reference's 1/len
+//    (moving_average.rs:66-81: 1/len while the buffer grows, 1/ws, then 1/len
+//    in the tail) and publishes finished blocks to the next pass (sc1 stores,
+//    vmcnt(0), sc1 counter; the consumer polls with sc1 loads --
+//    MI355X_MICROARCH.md, cross-CU hand-offs).
 //
 // Per pass, in j = 0 .. N+R-1:  if j < N: sum += in[j];  if j >= WS: sum -= in[j-WS];
 //                               raw[j] = sum  (= the reference's sum after tick j-R)
@@ -2186,15 +2191,21 @@ __global__ __launch_bounds__(BS) void k_mse_partial(BatchArgs a, Workspace w, in
     }
 }
 
-__global__ void k_mse_final(BatchArgs a, Workspace w, int nparts) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= a.B) return;
+// One wave per spectrum: the nparts partial sums are folded left to right from +0.0
+// (the order k_mse_partial's tree fixes) with the ordered DPP fold, instead of a
+// single thread whose dependent global loads cost ~200 cycles each (42 us at B=1).
+__global__ __launch_bounds__(64) void k_mse_final(BatchArgs a, Workspace w, int nparts) {
+    const int s = blockIdx.x;
     if (w.status[s]) return;  // already reported by k_retain
     if (w.mse_panic[s]) {
-        a.out_status[s] = MDG_REFERENCE_PANIC;
-        a.out_mse[s] = 0.0;
+        if (threadIdx.x == 0) {
+            a.out_status[s] = MDG_REFERENCE_PANIC;
+            a.out_mse[s] = 0.0;
+        }
         return;
     }
+    const double t = dpp_fold(0.0, w.mse_part + (size_t)s * nparts, nparts);
+    if (threadIdx.x != 0) return;
     const int nig = w.n_ig[s];
     int64_t total = 0;
     for (int r = 0; r <= nig; ++r) {
@@ -2202,8 +2213,6 @@ __global__ void k_mse_final(BatchArgs a, Workspace w, int nparts) {
         mse_region(w, s, r, nig, &lo, &hi);
         total += hi - lo;
     }
-    double t = 0.0;
-    for (int k = 0; k < nparts; ++k) t += w.mse_part[(size_t)s * nparts + k];
     a.out_mse[s] = t / (double)total;
     a.out_status[s] = (w.kept_count[s] > a.cap) ? MDG_CAPACITY : MDG_OK;
 }
@@ -2407,7 +2416,7 @@ void launch_mse(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t 
     hipLaunchKernelGGL(k_mse_partial<256>, dim3(nparts * a.B), dim3(256), 0, st, a, w, nparts);
 }
 void launch_mse_final(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st) {
-    hipLaunchKernelGGL(k_mse_final, dim3(cdiv(a.B, 64)), dim3(64), 0, st, a, w, nparts);
+    hipLaunchKernelGGL(k_mse_final, dim3(a.B), dim3(64), 0, st, a, w, nparts);
 }
 void launch_mse_exact(const double* sup, const double* y, int64_t n, const ExactRegions& r,
                       double* scratch, double* out, hipStream_t st) {
