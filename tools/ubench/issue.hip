@@ -95,8 +95,6 @@ DEFK(t_pair, PAIR, 0)
 DEFK(t_pair_gst_same, PAIR "global_store_dwordx4 v8, v[0:3], s[56:57]\n", 0)
 DEFK(t_pair_gst_lane, PAIR "global_store_dwordx4 v9, v[0:3], s[56:57]\n", 0)
 DEFK(t_pair_gst_1lane, PAIR "s_mov_b64 exec, 1\n global_store_dwordx4 v8, v[0:3], s[56:57]\n s_mov_b64 exec, s[58:59]\n", 0)
-DEFK(t_pair_sst, PAIR "v_readfirstlane_b32 s68, v0\n v_readfirstlane_b32 s69, v1\n v_readfirstlane_b32 s70, v2\n v_readfirstlane_b32 s71, v3\n"
-                      "s_store_dwordx4 s[68:71], s[56:57], 0x0\n", 0)
 // four ticks in rotating pairs; each store writes the pair finished two ticks earlier
 DEFK(t_quad_gst_lag, "v_add_f64 v[0:1], v[6:7], s[64:65]\n v_add_f64 v[0:1], v[0:1], -s[66:67]\n"
                      "v_add_f64 v[2:3], v[0:1], s[64:65]\n v_add_f64 v[2:3], v[2:3], -s[66:67]\n"
@@ -172,7 +170,6 @@ int main() {
         {"pair + gstore x4 same addr", t_pair_gst_same, 2},
         {"pair + gstore x4 lane addr", t_pair_gst_lane, 2},
         {"pair + gstore x4 EXEC=1", t_pair_gst_1lane, 2},
-        {"pair + 4 rfl + s_store x4", t_pair_sst, 2},
         {"quad lagged gstore", t_quad_gst_lag, 4},
         {"quad lagged ds_write_b128", t_quad_dsw_lag, 4},
         {"oct: s_load + 4 lagged gstore", t_oct, 8},
