@@ -166,7 +166,7 @@ int ensure_workspace(mdg_ctx* c, int B, int N) {
         const size_t o_ig = take(Bs * 2 * kMaxIgnore * 8);
         const size_t o_nig = take(Bs * 4), o_panic = take(Bs * 4), o_status = take(Bs * 4);
         const size_t o_dcnt = take(Bs * 4), o_scnt = take(Bs * 4), o_kcnt = take(Bs * 4);
-        const size_t o_xok = take(Bs * 4), o_unsafe = take(Bs * 8), o_uk = take(Bs * 4);
+        const size_t o_xok = take(Bs * 4), o_unsafe = take(Bs * 16), o_uk = take(Bs * 4);
 
         if (c->arena.p) (void)hipFree(c->arena.p);
         c->arena.p = nullptr;
@@ -243,6 +243,11 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
         w.smooth_stride = a.y_stride;
     }
     const int det_only = s->selector == MDG_SELECT_DETECTOR_ONLY;
+    // the term-fold fit kernel also updates the stencils; its parameter versions
+    // alternate between params and the (then unused) ratio buffer
+    const bool fused = fit_sup_fused(a);
+    w.params_alt = fused ? w.ratio : nullptr;
+    w.fit_iters = (int)s->fit_iterations;
     int gfit = 24;  // k_fit_sup workgroups per spectrum (3 * 2048 / 256)
     if (const char* e = std::getenv("MDG_GFIT")) gfit = std::max(1, std::atoi(e));  // tuning
     const int gupd = std::max(1, std::min(16, 1024 / std::max(1, a.B)));
@@ -302,7 +307,7 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
             StageTimer t(c, ST_FIT_SUP);
             launch_fit_sup(a, w, gfit, (int)it, st);
         }
-        {
+        if (!fused) {
             StageTimer t(c, ST_FIT_UPDATE);
             launch_fit_update(a, w, gupd, (int)it, st);
         }

@@ -131,6 +131,8 @@ __device__ __forceinline__ double superpose(double x, const double* __restrict__
 // cycle sums of kernel phases, written to a side buffer only. Empty otherwise.
 #ifdef MDG_DIAG
 __device__ long long* g_diag = nullptr;
+__device__ int g_tf_mode = 0;
+__device__ int g_chain_mode = 0;  // chain_diag: 1 = feeder publishes everything at once, no scaler; 2 = no scaler; 3 = instant feeder  // fit_diag: 1 = evaluators skip LDS stores, 2 = skip evaluation
 #define KSTAMP(slot)                                                           \
     if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0 && g_diag)      \
         g_diag[512 + (slot)] = (long long)__builtin_amdgcn_s_memtime()
@@ -293,8 +295,10 @@ __global__ void k_prep(BatchArgs a, Workspace w) {
     w.mse_panic[s] = panic;
     // the axis is monotone (Spectrum invariant): its end points bound every x
     w.x_ok[s] = x_fast_ok(x0) && x_fast_ok(x[a.N - 1]);
-    w.unsafe[2 * s] = 0;
-    w.unsafe[2 * s + 1] = 0;
+    w.unsafe[4 * s] = 0;
+    w.unsafe[4 * s + 1] = 0;
+    w.unsafe[4 * s + 2] = 0;
+    w.unsafe[4 * s + 3] = 0;
     w.unsafe_kept[s] = 0;
     w.status[s] = (a.N < 2) ? MDG_INVALID_ARGUMENT : 0;
     w.det_count[s] = 0;
@@ -938,6 +942,12 @@ __global__ __launch_bounds__(192) void k_smooth_chain(BatchArgs a, Workspace w, 
         unsigned idle = 0;
         bool ok = true;
         DIAGC(8, __builtin_amdgcn_s_memtime());
+#ifdef MDG_DIAG
+        if (g_chain_mode == 1 || g_chain_mode == 3) {
+            CTL_ST(in_ready, nIB);
+            pf = nIB;
+        }
+#endif
         while (pf < nIB) {
             if (CTL_LD(abort)) {
                 ok = false;
@@ -987,6 +997,9 @@ __global__ __launch_bounds__(192) void k_smooth_chain(BatchArgs a, Workspace w, 
         unsigned idle = 0;
         bool ok = true;
         DIAGC(16, __builtin_amdgcn_s_memtime());
+#ifdef MDG_DIAG
+        if (g_chain_mode == 1 || g_chain_mode == 2) sc = nOB;
+#endif
         while (sc < nOB) {
             if (CTL_LD(abort)) {
                 ok = false;
@@ -1683,7 +1696,7 @@ __global__ void k_fit_init(BatchArgs a, Workspace w) {
         st[0] = q.x1; st[1] = q.x2; st[2] = q.x3; st[3] = q.y1; st[4] = q.y2; st[5] = q.y3;
         double* L = w.params + 3 * base + 3 * (size_t)p;
         solve(q, L);
-        if (!peak_fast_ok(L[0], L[1], L[2])) atomicAdd(&w.unsafe[2 * s], 1);
+        if (!peak_fast_ok(L[0], L[1], L[2])) atomicAdd(&w.unsafe[4 * s], 1);
     }
 }
 
@@ -1697,8 +1710,8 @@ __device__ __forceinline__ bool fit_done(const Workspace& w, int s, int it) {
 }
 
 __device__ __forceinline__ bool fit_fast(const Workspace& w, int s, int it) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) w.unsafe[2 * s + ((it + 1) & 1)] = 0;
-    return w.x_ok[s] && w.unsafe[2 * s + (it & 1)] == 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) w.unsafe[4 * s + ((it + 1) & 1)] = 0;
+    return w.x_ok[s] && w.unsafe[4 * s + (it & 1)] == 0;
 }
 
 // fold the first r < 16 terms of a row-replicated group (see fold16)
@@ -1962,6 +1975,135 @@ __global__ __launch_bounds__(256) void k_fit_sup_dpp(BatchArgs a, Workspace w, i
     else fit_dpp_body<false>(a, w, s, P, lds_p);
 }
 
+// K6e  fit superposition + stencil update, term-fold form (small batches). A
+// workgroup owns Q = 24 reduced points = 8 peaks of one spectrum. EW evaluator
+// waves compute the terms of a chunk of J = 64*EW peaks (lane = peak, parameters
+// in VGPRs; the Q x values are wave-uniform and sit in SGPRs) into LDS T[q][j].
+// One fold wave (lane = point, raised priority) adds the chunk into each point's
+// running sum in peak order -- the reference's left fold (lorentzian.rs:606-611),
+// so the sums equal K6's bit for bit -- while the evaluators produce the next
+// chunk into the other buffer (one barrier per chunk). The fold wave then owns
+// whole peaks, so it also does k_fit_update's work for its 8 peaks
+// (fitter_analytical.rs:48-65): ratio = y/sup, scale, mirror, re-solve. The new
+// parameters go to the other parameter buffer (version it+1; odd versions in
+// params_alt) because other workgroups still read version it; the range flags
+// rotate over three slots (read it%3, count (it+1)%3, clear (it+2)%3).
+// Measured (bench, P = 2048): 20.7 us per iteration at B = 1 against 28.0 for
+// the DPP fold, 36 against 42 at B = 2; the DPP fold and one thread per point
+// win from B = 4 (tools/fit_sweep.sh).
+constexpr int kTfQ = 24, kTfEW = 3;
+constexpr int kTfPad = 2;  // row padding (doubles): 16-byte aligned rows
+constexpr int kTfLds = 2 * kTfQ * (64 * kTfEW + kTfPad);
+
+__device__ __forceinline__ const double* params_version(const Workspace& w, size_t base, int v) {
+    return ((v & 1) ? w.params_alt : w.params) + 3 * base;
+}
+
+template <bool FAST>
+__device__ __forceinline__ void fit_tf_body(const Workspace& w, int s, int P, int it, double* T) {
+    constexpr int Q = kTfQ, EW = kTfEW, J = 64 * EW;
+    constexpr int RS = J + kTfPad;  // row stride of T (doubles)
+    static_assert(Q % 3 == 0 && Q / 3 <= 64, "whole peaks per tile");
+    const size_t base = (size_t)s * w.capD;
+    const int npts = 3 * P;
+    const int tiles = (npts + Q - 1) / Q;
+    const int nch = (P + J - 1) / J;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const double* __restrict__ params = params_version(w, base, it);
+    const bool folder = wv == EW;
+    if (folder) __builtin_amdgcn_s_setprio(3);
+    DIAG_DECL
+    for (int tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+        const int p0 = tile * Q;
+        if (!folder) {
+            // wave-uniform x of the tile's points; a tail tile reads past 3P into the
+            // arena (ry follows rx), and those points are never used
+            const const_f64_ptr rx = (const_f64_ptr)(w.rx + 3 * base + p0);
+            double xq[Q];
+#pragma unroll
+            for (int q = 0; q < Q; ++q) xq[q] = rx[q];
+            const int jl = wv * 64 + lane;
+            int j = min(jl, P - 1);
+            double f = params[3 * j], h = params[3 * j + 1], m = params[3 * j + 2];
+            for (int c = 0; c <= nch; ++c) {
+#ifdef MDG_DIAG
+                if (c < nch && g_tf_mode == 2) {
+                } else
+#endif
+                if (c < nch) {
+                    double* Tb = T + (c & 1) * Q * RS + jl;
+                    const double cf = f, ch = h, cm = m;
+                    j = min((c + 1) * J + jl, P - 1);  // prefetch the next chunk's peak
+                    f = params[3 * j];
+                    h = params[3 * j + 1];
+                    m = params[3 * j + 2];
+#pragma unroll
+                    for (int q = 0; q < Q; ++q) Tb[q * RS] = lorentz_t<FAST>(xq[q], cf, ch, cm);
+                }
+                DIAG_STAMP(0);
+                lds_barrier();
+                DIAG_STAMP(1);
+            }
+        } else {
+            double acc = -0.0;
+            const int q = lane < Q ? lane : Q - 1;
+            DIAG_STAMP(4);
+            lds_barrier();  // chunk 0 written
+            DIAG_STAMP(3);
+            for (int c = 0; c < nch; ++c) {
+                const double2* row = (const double2*)(T + (c & 1) * Q * RS + q * RS);
+                const int cn = min(J, P - c * J);
+                if (cn == J) {
+#pragma unroll 16
+                    for (int k = 0; k < J / 2; ++k) {
+                        const double2 v = row[k];
+                        acc += v.x;
+                        acc += v.y;
+                    }
+                } else {
+                    const double* r1 = (const double*)row;
+                    for (int k = 0; k < cn; ++k) acc += r1[k];
+                }
+                DIAG_STAMP(2);
+                lds_barrier();
+                DIAG_STAMP(3);
+            }
+            // stencil update of the tile's peaks (k_fit_update): lane k gathers the
+            // ratios y/sup of its peak's three points from lanes 3k..3k+2
+            const double ratio = w.ry[3 * base + min(p0 + q, npts - 1)] / acc;
+            const int k = lane < Q / 3 ? lane : 0;
+            const double r0 = __shfl(ratio, 3 * k, 64);
+            const double r1 = __shfl(ratio, 3 * k + 1, 64);
+            const double r2 = __shfl(ratio, 3 * k + 2, 64);
+            const int pk = p0 / 3 + lane;
+            if (lane < Q / 3 && pk < P) {
+                double* st = w.stencil + 6 * base + 6 * (size_t)pk;
+                Stencil sq{st[0], st[1], st[2], st[3], st[4], st[5]};
+                sq.y1 = sq.y1 * r0;
+                sq.y2 = sq.y2 * r1;
+                sq.y3 = sq.y3 * r2;
+                mirror_shoulder(sq);
+                st[0] = sq.x1; st[1] = sq.x2; st[2] = sq.x3; st[3] = sq.y1; st[4] = sq.y2; st[5] = sq.y3;
+                double* L = (((it + 1) & 1) ? w.params_alt : w.params) + 3 * base + 3 * (size_t)pk;
+                solve(sq, L);
+                if (!peak_fast_ok(L[0], L[1], L[2])) atomicAdd(&w.unsafe[4 * s + (it + 1) % 3], 1);
+            }
+            DIAG_STAMP(4);
+        }
+    }
+    DIAG_FLUSH();
+}
+
+__global__ __launch_bounds__(64 * (kTfEW + 1)) void k_fit_sup_tf(BatchArgs a, Workspace w, int it) {
+    __shared__ __attribute__((aligned(16))) double T[kTfLds];
+    const int s = blockIdx.y;
+    if (w.status[s] || fit_done(w, s, it)) return;
+    const int P = w.sel_count[s];
+    if (blockIdx.x == 0 && threadIdx.x == 0) w.unsafe[4 * s + (it + 2) % 3] = 0;
+    if (w.x_ok[s] && w.unsafe[4 * s + it % 3] == 0) fit_tf_body<true>(w, s, P, it, T);
+    else fit_tf_body<false>(w, s, P, it, T);
+}
+
 __global__ void k_fit_sup(BatchArgs a, Workspace w, int it) {
     const int s = blockIdx.y;
     if (w.status[s] || fit_done(w, s, it)) return;
@@ -2081,7 +2223,7 @@ __global__ void k_fit_update(BatchArgs a, Workspace w, int it) {
         st[0] = q.x1; st[1] = q.x2; st[2] = q.x3; st[3] = q.y1; st[4] = q.y2; st[5] = q.y3;
         double* L = w.params + 3 * base + 3 * (size_t)p;
         solve(q, L);
-        if (!peak_fast_ok(L[0], L[1], L[2])) atomicAdd(&w.unsafe[2 * s + ((it + 1) & 1)], 1);
+        if (!peak_fast_ok(L[0], L[1], L[2])) atomicAdd(&w.unsafe[4 * s + ((it + 1) & 1)], 1);
     }
 }
 
@@ -2101,7 +2243,10 @@ __global__ __launch_bounds__(BS) void k_retain(BatchArgs a, Workspace w) {
     }
     const int P = w.sel_count[s];
     const size_t base = (size_t)s * w.capD;
-    const double* params = w.params + 3 * base;
+    // k_fit_sup_tf leaves version min(iterations) of the parameters in the buffer of
+    // its parity; the k_fit_update path updates them in place
+    const int ver = w.params_alt ? (w.fit_iters_s ? min(w.fit_iters_s[s], w.fit_iters) : w.fit_iters) : 0;
+    const double* params = params_version(w, base, ver);
     const int per = (P + BS - 1) / BS;
     const int p0 = threadIdx.x * per, p1 = min(P, p0 + per);
     int keep = 0;
@@ -2384,19 +2529,28 @@ void launch_select(const BatchArgs& a, const Workspace& w, int detector_only, do
 void launch_fit_init(const BatchArgs& a, const Workspace& w, int gx, hipStream_t st) {
     hipLaunchKernelGGL(k_fit_init, dim3(gx, a.B), dim3(256), 0, st, a, w);
 }
-void launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st) {
-    // measured (bench, P = 2048, ms per 10 launches): B=2 dpp 0.43 / plain 1.65;
-    // B=8 dpp 1.49 / plain 2.50; B=16 dpp 2.76 / plain 2.67; the split kernel lost
-    // everywhere (kept for MDG_FITSUP=split)
+// Fit kernel choice by measurement (bench, P = 2048, ms per 10 launches):
+//   B=1 tf 0.207 / dpp 0.280 / plain 1.69;  B=2 tf 0.361 / dpp 0.423;
+//   B=4 dpp 0.609 / tf 0.665;  B=8 dpp 1.41 / tf 1.46 / plain 2.49;
+//   B=16 dpp 2.54 / plain 2.64;  B=32 plain 3.16 / dpp 4.76;  B=256 plain 15.7 / dpp 32.6.
+// MDG_FITSUP = tf | dpp | split | plain forces one (tests, tuning).
+static std::string fit_choice(const BatchArgs& a) {
     const char* force = std::getenv("MDG_FITSUP");
-    const std::string f = force ? force : "";
-    if ((!force && a.B <= 12) || f == "dpp") {
+    if (force && *force) return force;
+    return a.B <= 2 ? "tf" : a.B <= 12 ? "dpp" : "plain";
+}
+bool fit_sup_fused(const BatchArgs& a) { return fit_choice(a) == "tf"; }
+void launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st) {
+    const std::string f = fit_choice(a);
+    if (f == "tf") {
+        // 24 points per workgroup: 256 workgroups at P = 2048, grid-stride beyond
+        const int g = std::max(2, 256 / a.B);
+        hipLaunchKernelGGL(k_fit_sup_tf, dim3(g, a.B), dim3(64 * (kTfEW + 1)), 0, st, a, w, it);
+    } else if (f == "dpp") {
         // 32 points per workgroup: 192 workgroups at P = 2048, grid-stride beyond
         const int g = std::max(64, std::min(512, 1024 / a.B));
         hipLaunchKernelGGL(k_fit_sup_dpp, dim3(g, a.B), dim3(256), 0, st, a, w, it);
-        return;
-    }
-    if (f == "split") {
+    } else if (f == "split") {
         // 16 points per 1024-thread workgroup: 3P/16 workgroups per spectrum (384 at
         // P = 2048) keep every CU busy; grid-stride beyond that
         const int g = std::max(64, std::min(1024, 2048 / a.B));

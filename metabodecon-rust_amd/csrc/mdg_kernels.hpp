@@ -55,6 +55,8 @@ struct Workspace {
     int32_t* sel_r;
     double* scores;
     double* params;
+    double* params_alt;       // k_fit_sup_tf: odd params versions (null: k_fit_update in place)
+    int fit_iters;            // fit iterations launched for the batch
     double* kept;
     double* stencil;
     double* rx;
@@ -71,7 +73,8 @@ struct Workspace {
     int32_t* sel_count;
     int32_t* kept_count;
     int32_t* x_ok;            // B: axis inside the fast-division range
-    int32_t* unsafe;          // B x 2: ping-pong count of fit params outside it
+    int32_t* unsafe;          // B x 4: count of fit params outside it, per params version
+                              // (k_fit_update path: version & 1; fused k_fit_sup_tf: version % 3)
     int32_t* unsafe_kept;     // B: same for the retained Lorentzians
     // k_smooth_chain (allocated on first use; null otherwise)
     double* chain_raw;        // P x B x chain_stride: raw running sums of every pass
@@ -106,6 +109,8 @@ void launch_scores(const BatchArgs& a, const Workspace& w, hipStream_t st);
 void launch_select(const BatchArgs& a, const Workspace& w, int detector_only, double threshold,
                    hipStream_t st);
 void launch_fit_init(const BatchArgs& a, const Workspace& w, int gx, hipStream_t st);
+// returns true when the launched kernel also did the stencil update (no k_fit_update)
+bool fit_sup_fused(const BatchArgs& a);
 void launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st);
 void launch_fit_update(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st);
 void launch_retain(const BatchArgs& a, const Workspace& w, hipStream_t st);

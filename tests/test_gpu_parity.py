@@ -320,10 +320,10 @@ def test_chain_smoother_repeated_launches(ctx, monkeypatch):
             assert np.array_equal(row, oracle.moving_average(ys[s], 3, 3)), (rep, s)
 
 
-@pytest.mark.parametrize("path", ["dpp", "split", "plain"])
+@pytest.mark.parametrize("path", ["dpp", "split", "plain", "tf"])
 def test_fit_superposition_kernels(ctx, path, monkeypatch):
     """Every fit-superposition kernel (row-broadcast DPP fold, LDS split fold, one
-    thread per point; chosen by MDG_FITSUP) gives the oracle's Lorentzians bit for
+    thread per point, term fold; chosen by MDG_FITSUP) gives the oracle's Lorentzians bit for
     bit, including peak counts that are not multiples of the 16-peak groups."""
     monkeypatch.setenv("MDG_FITSUP", path)
     names = ["sim_03", "blood_03", "synth_128k_2k_s1"]
@@ -335,6 +335,24 @@ def test_fit_superposition_kernels(ctx, path, monkeypatch):
         assert np.array_equal(out[0, : counts[0]], o.params), name
         assert abs(mse[0] - o.mse) <= MSE_RTOL * abs(o.mse), name
 
+
+
+@pytest.mark.parametrize("path", ["dpp", "split", "plain", "tf"])
+def test_fit_superposition_kernels_batch(ctx, path, monkeypatch):
+    """The fit kernels on a batch whose spectra have different peak counts (tail
+    tiles, grid-stride loops, per-spectrum range flags) against the oracle."""
+    monkeypatch.setenv("MDG_FITSUP", path)
+    rows, ref = [], []
+    for seed in (3, 4, 5):
+        x, y = synth_spectrum(seed, n=65536, n_peaks=700 + 300 * seed)[:2]
+        rows.append(y)
+        ref.append(oracle.deconvolute(x, y, (11.8, -2.2)))
+    st = oracle.default_settings()
+    status, counts, out, mse = gpu_batch(ctx, x, np.stack(rows), [(11.8, -2.2)], st)
+    for s, o in enumerate(ref):
+        assert status[s] == o.status == 0
+        assert np.array_equal(out[s, : counts[s]], o.params), s
+        assert abs(mse[s] - o.mse) <= MSE_RTOL * abs(o.mse), s
 
 def test_device_graph_replay(ctx, monkeypatch):
     """mdg_deconvolute_batch_device replays a cached hipGraph for repeated argument

@@ -8,8 +8,13 @@ SGPR operands, one block of CB = 96 ticks per trip:
   * operands: groups of 8 doubles of the pass input, s_load_dwordx16 into three
     rotating SGPR buffers (prev / cur / next); each group prefetches the next
     and waits for it at its end (lgkmcnt(0): SMEM returns out of order);
-  * sums rotate through NV = 8 VGPR pairs v[0:15]; tick t writes pair t%NV; only
-    the last sum of each group of 8 ticks is stored (see block_body);
+  * sums: group q accumulates in pair ACC[q % 2] (v[0:1] / v[2:3]). Its first add
+    is a VOP3 v_add_f64 from the other pair; the other 15 operations are VOP2
+    v_fmac_f64 with the SGPR operand times +1.0 / -1.0 (v[4:5] / v[6:7]) --
+    fma(a, +-1, s) rounds exactly as s +- a, and the dependent VOP2 fmac chain
+    issues in 8.3 cycles per tick against 10.3 for VOP3 adds (tools/ubench/
+    eval_cost.hip). Only the last sum of each group of 8 ticks is stored (see
+    block_body), read from the previous group's pair while the next group runs;
   * per block: wait (LDS, cached) until the helper wave has published the input
     block the prefetch reaches; after the block, s_waitcnt vmcnt(GROUPS) proves
     the previous block's stores complete, then raw_done is published in LDS.
@@ -29,9 +34,8 @@ OUT = os.path.join(ROOT, "metabodecon-rust_amd", "csrc", "mdg_chain_asm.inc")
 IN, RAW = "s[88:89]", "s[90:91]"
 IN_LO, IN_HI, RAW_LO, RAW_HI = "s88", "s89", "s90", "s91"
 BLK, AVAIL, NIB, GUARD, CNT, TMP, NEED, STAT = "s92", "s93", "s94", "s95", "s96", "s97", "s98", "s99"
-NV = int(os.environ.get("CHAIN_NV", "8"))          # rotating sum pairs (4 or 8)
-V = [f"v[{2 * k}:{2 * k + 1}]" for k in range(NV)]
-PAIR = {k: f"v[{2 * k}:{2 * k + 3}]" for k in range(0, NV, 2)}
+ACC = ["v[0:1]", "v[2:3]"]   # running sum of even / odd groups
+ONE, MONE = "v[4:5]", "v[6:7]"
 LDSA, VT, VZ = "v16", "v17", "v18"
 GUARD_SPINS = 1 << 22  # ~0.3 s of s_sleep 1 before the wave gives up (never expected)
 
@@ -46,25 +50,31 @@ def block_body(ws):
     checkpoint raw[8G+7]) is stored, one 8-byte store placed after the first add
     of the next group's second tick. The scaler wave recomputes the other seven
     sums of the group from the previous checkpoint with the same two operations
-    per tick, so the stored data is 1/8 of the ticks."""
+    per tick, so the stored data is 1/8 of the ticks.
+
+    (Loading two groups ahead in pairs, with four buffers, was measured: no
+    change at 12.9 cycles/tick -- the cost of the SMEM feed is its issue and
+    SGPR write-back on this wave, ~2 cycles/tick, not its latency.)"""
     L = []
     for q in range(GROUPS):
         prev, cur, nxt = q % 3, (q + 1) % 3, (q + 2) % 3
         # IN points one group (64 B) before the block: group q+1 starts at 64*(q+2)
         if not os.environ.get("CHAIN_NOLOAD"):  # diagnostic variants only (wrong results)
             L.append(f"s_load_dwordx16 s[{BUF[nxt]}:{BUF[nxt] + 15}], {IN}, {64 * (q + 2)}")
+        acc, other = ACC[q % 2], ACC[(q - 1) % 2]
         for u in range(8):
-            t = 8 * q + u
-            dst, src = V[t % NV], V[(t - 1) % NV]
-            L.append(f"v_add_f64 {dst}, {src}, {sreg(cur, u)}")
+            if u == 0:
+                L.append(f"v_add_f64 {acc}, {other}, {sreg(cur, u)}")
+            else:
+                L.append(f"v_fmac_f64 {acc}, {sreg(cur, u)}, {ONE}")
             if u == 1 and q >= 1 and not os.environ.get("CHAIN_NOSTORE"):
-                c = 8 * q - 1  # checkpoint of the previous group, still in its register
-                L.append(f"global_store_dwordx2 {VZ}, {V[c % NV]}, {RAW} offset:{8 * c}")
+                c = 8 * q - 1  # checkpoint of the previous group, still in its pair
+                L.append(f"global_store_dwordx2 {VZ}, {other}, {RAW} offset:{8 * c}")
             pop = sreg(cur, u - ws) if u >= ws else sreg(prev, 8 + u - ws)
-            L.append(f"v_add_f64 {dst}, {dst}, -{pop}")
+            L.append(f"v_fmac_f64 {acc}, {pop}, {MONE}")
         L.append("s_waitcnt lgkmcnt(0)")
     if not os.environ.get("CHAIN_NOSTORE"):
-        L.append(f"global_store_dwordx2 {VZ}, {V[(CB - 1) % NV]}, {RAW} offset:{8 * (CB - 1)}")
+        L.append(f"global_store_dwordx2 {VZ}, {ACC[(GROUPS - 1) % 2]}, {RAW} offset:{8 * (CB - 1)}")
     return L
 
 
@@ -81,7 +91,9 @@ def program(ws):
         "s_mov_b32 s99, 0",
         f"v_mov_b32 {LDSA}, %[lds]",
         f"v_mov_b32 {VZ}, 0",
-        f"v_mov_b64 {V[NV - 1]}, %[sum]",
+        f"v_mov_b64 {ACC[1]}, %[sum]",
+        f"v_mov_b64 {ONE}, 1.0",
+        f"v_mov_b64 {MONE}, -1.0",
         f"s_load_dwordx16 s[{BUF[0]}:{BUF[0] + 15}], {IN}, 0",
         f"s_load_dwordx16 s[{BUF[1]}:{BUF[1] + 15}], {IN}, 64",
         "s_waitcnt lgkmcnt(0)",
@@ -127,7 +139,7 @@ def program(ws):
         "s_cbranch_scc1 Lblk%=",
         "Ldone%=:",
         "s_waitcnt vmcnt(0)",
-        f"v_mov_b64 %[sum], {V[(CB - 1) % NV]}",
+        f"v_mov_b64 %[sum], {ACC[(GROUPS - 1) % 2]}",
         "s_mov_b32 %[blk_out], s92",
         "s_mov_b32 %[stat], s99",
     ]

@@ -6,7 +6,9 @@
 #include <vector>
 using namespace mdg;
 int main(int argc, char** argv) {
-    const int N = 131072, B = argc > 1 ? atoi(argv[1]) : 1, P = 3, WS = 3;
+    const int N = 131072, B = argc > 1 ? atoi(argv[1]) : 1, P = argc > 2 ? atoi(argv[2]) : 3, WS = 3;
+    const int mode = argc > 3 ? atoi(argv[3]) : 0;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_chain_mode), &mode, sizeof(mode));
     std::vector<double> h(N * (size_t)B);
     for (size_t i = 0; i < h.size(); ++i) h[i] = (double)((i * 2654435761u) % 1000003) * 1e-3;
     double *y, *sm, *chain; int* status; long long* diag;

@@ -1,0 +1,83 @@
+// Phase breakdown and timing of the fit-superposition kernels on synthetic peak
+// tables (P peaks, 3P reduced points per spectrum): builds the library kernel source
+// with -DMDG_DIAG. usage: fit_diag [B] [P]
+#include "../../metabodecon-rust_amd/csrc/mdg_kernels.hip"
+#include <cstdio>
+#include <vector>
+using namespace mdg;
+int main(int argc, char** argv) {
+    const int B = argc > 1 ? atoi(argv[1]) : 1, P = argc > 2 ? atoi(argv[2]) : 2048;
+    const int N = 131072, capD = N / 2 + 2;
+    std::vector<double> par((size_t)B * capD * 3, 0.0), rx((size_t)B * capD * 3 + 64, 0.0),
+        ry((size_t)B * capD * 3, 1.0);
+    unsigned long long st = 12345;
+    auto U = [&]() { st = st * 6364136223846793005ull + 1442695040888963407ull; return (double)(st >> 11) * 0x1p-53; };
+    for (int s = 0; s < B; ++s)
+        for (int p = 0; p < P; ++p) {
+            const double m = -1.8 + 13.2 * U(), hw = 3e-4 + 5e-4 * U(), A = pow(10.0, 4.5 + 3.5 * U());
+            double* L = &par[((size_t)s * capD + p) * 3];
+            L[0] = A * hw * hw; L[1] = hw * hw; L[2] = m;
+            for (int k = 0; k < 3; ++k) rx[(size_t)s * capD * 3 + 3 * p + k] = m + (k - 1) * 1.5e-4;
+        }
+    double *d_par, *d_rx, *d_ry, *d_ratio, *d_alt, *d_st; int32_t *status, *sel, *xok, *unsafe; long long* diag;
+    (void)hipMalloc(&d_alt, par.size() * 8); (void)hipMalloc(&d_st, par.size() * 16);
+    {
+        std::vector<double> st6(par.size() * 2, 1.0);
+        (void)hipMemcpy(d_st, st6.data(), st6.size() * 8, hipMemcpyHostToDevice);
+    }
+    (void)hipMalloc(&d_par, par.size() * 8); (void)hipMalloc(&d_rx, rx.size() * 8);
+    (void)hipMalloc(&d_ry, ry.size() * 8); (void)hipMalloc(&d_ratio, ry.size() * 8);
+    (void)hipMemcpy(d_par, par.data(), par.size() * 8, hipMemcpyHostToDevice);
+    (void)hipMemcpy(d_rx, rx.data(), rx.size() * 8, hipMemcpyHostToDevice);
+    (void)hipMemcpy(d_ry, ry.data(), ry.size() * 8, hipMemcpyHostToDevice);
+    std::vector<int32_t> selv(B, P), ones(B, 1);
+    (void)hipMalloc(&status, 4 * B); (void)hipMemset(status, 0, 4 * B);
+    (void)hipMalloc(&sel, 4 * B); (void)hipMemcpy(sel, selv.data(), 4 * B, hipMemcpyHostToDevice);
+    (void)hipMalloc(&xok, 4 * B); (void)hipMemcpy(xok, ones.data(), 4 * B, hipMemcpyHostToDevice);
+    (void)hipMalloc(&unsafe, 16 * B); (void)hipMemset(unsafe, 0, 16 * B);
+    const size_t nd = 4096 * 16 * 8;
+    (void)hipMalloc(&diag, nd * 8);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_diag), &diag, sizeof(diag));
+    BatchArgs a{}; a.B = B; a.N = N;
+    Workspace w{}; w.capD = capD; w.status = status; w.sel_count = sel; w.params = d_par;
+    w.rx = d_rx; w.ry = d_ry; w.ratio = d_ratio; w.x_ok = xok; w.unsafe = unsafe;
+    w.stencil = d_st; w.fit_iters = 10;
+    const char* kinds[] = {"dpp", "plain", "tf", "tf/noeval"};
+    std::vector<double> ref;
+    for (const char* k : kinds) {
+        const std::string ks(k);
+        const int mode = ks.find("/nostore") != std::string::npos ? 1 : ks.find("/noeval") != std::string::npos ? 2 : 0;
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_tf_mode), &mode, sizeof(mode));
+        setenv("MDG_FITSUP", ks.substr(0, ks.find('/')).c_str(), 1);
+        w.params_alt = fit_sup_fused(a) ? d_alt : nullptr;
+        float best = 1e30f;
+        for (int rep = 0; rep < 6; ++rep) {
+            (void)hipMemset(diag, 0, nd * 8);
+            hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
+            (void)hipEventRecord(e0);
+            launch_fit_sup(a, w, 24, 0, 0);
+            (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
+            float ms; (void)hipEventElapsedTime(&ms, e0, e1);
+            if (rep > 0 && ms < best) best = ms;
+        }
+        std::vector<double> out(ry.size());
+        (void)hipMemcpy(out.data(), d_ratio, out.size() * 8, hipMemcpyDeviceToHost);
+        bool same = true;
+        if (ref.empty()) ref = out;
+        else if (!w.params_alt) for (int s = 0; s < B; ++s) for (int i = 0; i < 3 * P; ++i) same &= out[(size_t)s * capD * 3 + i] == ref[(size_t)s * capD * 3 + i];
+        const double evals = 3.0 * P * P * B;
+        printf("%-6s B=%d P=%d  %.2f us/launch  %.3f T evals/s  same_as_dpp=%d\n", k, B, P, best * 1e3,
+               evals / (best * 1e-3) / 1e12, (int)same);
+        if (k[0] == 't') {
+            std::vector<long long> d(nd);
+            (void)hipMemcpy(d.data(), diag, nd * 8, hipMemcpyDeviceToHost);
+            const char* nm[5] = {"eval", "ev-barrier", "fold", "fold-barrier", "fold-other"};
+            for (int wv = 0; wv < 4; ++wv) {
+                printf("   wave %d (block 0):", wv);
+                for (int i = 0; i < 5; ++i) printf(" %s=%lld", nm[i], d[wv * 8 + i]);
+                printf("\n");
+            }
+        }
+    }
+    return 0;
+}
