@@ -167,6 +167,7 @@ int ensure_workspace(mdg_ctx* c, int B, int N) {
         const size_t o_nig = take(Bs * 4), o_panic = take(Bs * 4), o_status = take(Bs * 4);
         const size_t o_dcnt = take(Bs * 4), o_scnt = take(Bs * 4), o_kcnt = take(Bs * 4);
         const size_t o_xok = take(Bs * 4), o_unsafe = take(Bs * 16), o_uk = take(Bs * 4);
+        const size_t o_pcnt = take(Bs * 2 * ((W + 255) / 256) * 4);
 
         if (c->arena.p) (void)hipFree(c->arena.p);
         c->arena.p = nullptr;
@@ -205,6 +206,7 @@ int ensure_workspace(mdg_ctx* c, int B, int N) {
         w.x_ok = (int32_t*)(base + o_xok);
         w.unsafe = (int32_t*)(base + o_unsafe);
         w.unsafe_kept = (int32_t*)(base + o_uk);
+        w.peak_cnt = (int32_t*)(base + o_pcnt);
 
         c->ws_B = nB;
         c->ws_N = nN;

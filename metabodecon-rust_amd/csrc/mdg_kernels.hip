@@ -1145,63 +1145,110 @@ __device__ __forceinline__ bool in_ignore(int v, const int64_t* pairs, int n) {
     return false;
 }
 
-template <int BS>
-__global__ __launch_bounds__(BS) void k_peaks(BatchArgs a, Workspace w, int detector_only) {
-    const int s = blockIdx.x;
-    __shared__ int lds_i[BS / 64 + 1];
-    __shared__ long long lds_l[BS / 64 + 1];
-    if (w.status[s]) return;  // uniform per block
-    const int N = a.N;
-    const int W = w.W;
+// The peaks of one mask word (64 points), in centre order: borders by bit scans,
+// the detector-only and ignore-region filters. Counts the bordered peaks; returns
+// the kept ones, writing them at out.. when WRITE.
+template <bool WRITE>
+__device__ __forceinline__ int word_peaks(const BatchArgs& a, const Workspace& w, int s, int wd,
+                                          int detector_only, int* bordered, size_t out) {
+    const int N = a.N, W = w.W;
     const uint64_t* mc = w.masks + (size_t)s * 3 * W;
     const uint64_t* mr = mc + W;
     const uint64_t* ml = mc + 2 * W;
     const int64_t* pairs = w.ig + (size_t)s * 2 * kMaxIgnore;
     const int nig = w.n_ig[s];
     const int64_t sbi0 = w.sbi[2 * s], sbi1 = w.sbi[2 * s + 1];
-    const int wpt = (W + BS - 1) / BS;
-    const int w0 = threadIdx.x * wpt;
-    const int w1 = min(W, w0 + wpt);
-    int n_bordered = 0, n_keep = 0;
-    for (int pass = 0; pass < 2; ++pass) {
-        int out = 0;
-        if (pass == 1) {
-            int total;
-            out = block_exclusive_scan<BS>(n_keep, lds_i, &total);
-            if (threadIdx.x == 0) w.det_count[s] = total;
+    // the word and its neighbours' border masks in one round trip; a border farther
+    // than the neighbouring word falls back to the scans over memory
+    uint64_t bits = mc[wd];
+    const uint64_t r0 = mr[wd], r1 = wd + 1 < W ? mr[wd + 1] : 0;
+    const uint64_t l0 = ml[wd], l1 = wd > 0 ? ml[wd - 1] : 0;
+    const int lim_r = N - 3, lim_l = 2;
+    int kept = 0;
+    while (bits) {
+        const int b = __ffsll((unsigned long long)bits) - 1;
+        bits &= bits - 1;
+        const int c = (wd << 6) + b;
+        // first right-border bit > c (<= N-3): this word above b, then the next word
+        int r;
+        const uint64_t ra = b == 63 ? 0 : (r0 & (~0ull << (b + 1)));
+        if (ra) r = (wd << 6) + __ffsll((unsigned long long)ra) - 1;
+        else if (r1) r = ((wd + 1) << 6) + __ffsll((unsigned long long)r1) - 1;
+        else r = find_next_bit(mr, (wd + 2) << 6, lim_r);
+        if (r > lim_r) r = -1;
+        // last left-border bit < c (>= 2): this word below b, then the previous word
+        int l;
+        const uint64_t la = b == 0 ? 0 : (l0 & ((1ull << b) - 1ull));
+        if (la) l = (wd << 6) + 63 - __clzll((long long)la);
+        else if (l1) l = ((wd - 1) << 6) + 63 - __clzll((long long)l1);
+        else l = find_prev_bit(ml, ((wd - 1) << 6) - 1, lim_l);
+        if (l < lim_l) l = -1;
+        if (r < 0 || l < 0) continue;  // right == N-1 or left == 0: dropped
+        ++*bordered;
+        bool keep = true;
+        if (detector_only) keep = (int64_t)l >= sbi0 && (int64_t)r <= sbi1;
+        if (keep && a.n_ignore > 0) keep = !(in_ignore(l, pairs, nig) || in_ignore(r, pairs, nig));
+        if (!keep) continue;
+        if constexpr (WRITE) {
+            w.det_l[out + kept] = l;
+            w.det_c[out + kept] = c;
+            w.det_r[out + kept] = r;
         }
-        for (int wd = w0; wd < w1; ++wd) {
-            uint64_t bits = mc[wd];
-            while (bits) {
-                const int b = __ffsll((unsigned long long)bits) - 1;
-                bits &= bits - 1;
-                const int c = (wd << 6) + b;
-                const int r = find_next_bit(mr, c + 1, N - 3);
-                const int l = find_prev_bit(ml, c - 1, 2);
-                if (r < 0 || l < 0) continue;  // right == N-1 or left == 0: dropped
-                bool keep = true;
-                if (detector_only) keep = (int64_t)l >= sbi0 && (int64_t)r <= sbi1;
-                if (keep && a.n_ignore > 0) keep = !(in_ignore(l, pairs, nig) || in_ignore(r, pairs, nig));
-                if (pass == 0) {
-                    ++n_bordered;
-                    n_keep += keep ? 1 : 0;
-                } else if (keep) {
-                    const size_t o = (size_t)s * w.capD + out;
-                    w.det_l[o] = l;
-                    w.det_c[o] = c;
-                    w.det_r[o] = r;
-                    ++out;
-                }
-            }
-        }
-        if (pass == 0) {
-            const long long tot = block_sum_ll<BS>(n_bordered, lds_l);
-            if (tot == 0) {
-                if (threadIdx.x == 0) w.status[s] = MDG_NO_PEAKS_DETECTED;
-                return;
-            }
-        }
+        ++kept;
     }
+    return kept;
+}
+
+// K3a per chunk of kPkWords mask words (one word per thread): kept and bordered
+// peak counts. K3b re-scans its chunk, places it after the kept peaks of the chunks
+// before it and compacts in centre order; chunk 0 publishes det_count, or
+// NoPeaksDetected when no peak has both borders (detector.rs:99-164). Many
+// workgroups per spectrum: the single-workgroup version took 46-53 us at N = 131072.
+constexpr int kPkWords = 256;
+__global__ __launch_bounds__(kPkWords) void k_peaks_count(BatchArgs a, Workspace w, int detector_only) {
+    const int s = blockIdx.y, chunk = blockIdx.x;
+    __shared__ long long lds_l[kPkWords / 64 + 1];
+    if (w.status[s]) return;
+    const int wd = chunk * kPkWords + threadIdx.x;
+    int bordered = 0, kept = 0;
+    if (wd < w.W) kept = word_peaks<false>(a, w, s, wd, detector_only, &bordered, 0);
+    const long long k_tot = block_sum_ll<kPkWords>(kept, lds_l);
+    const long long b_tot = block_sum_ll<kPkWords>(bordered, lds_l);
+    if (threadIdx.x == 0) {
+        const int nch = (w.W + kPkWords - 1) / kPkWords;
+        int32_t* cnt = w.peak_cnt + (size_t)s * 2 * nch;
+        cnt[2 * chunk] = (int32_t)k_tot;
+        cnt[2 * chunk + 1] = (int32_t)b_tot;
+    }
+}
+
+__global__ __launch_bounds__(kPkWords) void k_peaks_write(BatchArgs a, Workspace w, int detector_only) {
+    const int s = blockIdx.y, chunk = blockIdx.x;
+    __shared__ int lds_i[kPkWords / 64 + 1];
+    __shared__ long long lds_l[kPkWords / 64 + 1];
+    if (w.status[s]) return;
+    const int nch = (w.W + kPkWords - 1) / kPkWords;
+    const int32_t* cnt = w.peak_cnt + (size_t)s * 2 * nch;
+    long long before = 0, k_all = 0, b_all = 0;
+    for (int k = threadIdx.x; k < nch; k += kPkWords) {
+        before += k < chunk ? cnt[2 * k] : 0;
+        k_all += cnt[2 * k];
+        b_all += cnt[2 * k + 1];
+    }
+    before = block_sum_ll<kPkWords>(before, lds_l);
+    k_all = block_sum_ll<kPkWords>(k_all, lds_l);
+    b_all = block_sum_ll<kPkWords>(b_all, lds_l);
+    if (b_all == 0) {
+        if (chunk == 0 && threadIdx.x == 0) w.status[s] = MDG_NO_PEAKS_DETECTED;
+        return;
+    }
+    if (chunk == 0 && threadIdx.x == 0) w.det_count[s] = (int32_t)k_all;
+    const int wd = chunk * kPkWords + threadIdx.x;
+    int bordered = 0, kept = 0;
+    if (wd < w.W) kept = word_peaks<false>(a, w, s, wd, detector_only, &bordered, 0);
+    int total;
+    const int o = block_exclusive_scan<kPkWords>(kept, lds_i, &total);
+    if (kept) word_peaks<true>(a, w, s, wd, detector_only, &bordered, (size_t)s * w.capD + before + o);
 }
 
 // ----------------------------------------------------------------------------------
@@ -2513,7 +2560,9 @@ void launch_flags(const BatchArgs& a, const Workspace& w, hipStream_t st) {
     hipLaunchKernelGGL(k_flags, dim3(cdiv(a.N, 256), a.B), dim3(256), 0, st, a, w);
 }
 void launch_peaks(const BatchArgs& a, const Workspace& w, int detector_only, hipStream_t st) {
-    hipLaunchKernelGGL(k_peaks<1024>, dim3(a.B), dim3(1024), 0, st, a, w, detector_only);
+    const int nch = cdiv(w.W, kPkWords);
+    hipLaunchKernelGGL(k_peaks_count, dim3(nch, a.B), dim3(kPkWords), 0, st, a, w, detector_only);
+    hipLaunchKernelGGL(k_peaks_write, dim3(nch, a.B), dim3(kPkWords), 0, st, a, w, detector_only);
 }
 void launch_scores(const BatchArgs& a, const Workspace& w, hipStream_t st) {
     const int gx = std::max(1, std::min(64, 4096 / std::max(1, a.B)));
