@@ -70,52 +70,60 @@ __device__ __forceinline__ double lorentz_t(double x, double sfhw, double hw2, d
 // s_load_dwordx* and uses SGPR operands.
 typedef const __attribute__((address_space(4))) double* const_f64_ptr;
 
+// MDG_SUP_GP peaks per group: the prefetch of the next group covers one group's
+// evaluations (~62 cycles each per wave), which must outlast an L2 hit when only
+// one or two waves share a SIMD
+// (bench, B = 1: MSE 174 us with 4, 134 with 6 or 8; B = 256: no change)
+#ifndef MDG_SUP_GP
+#define MDG_SUP_GP 6
+#endif
+constexpr int kSupGP = MDG_SUP_GP;
+
 template <bool FAST>
-__device__ __forceinline__ void sup_group(double x, double& acc, const double (&c)[12], double (&n)[12],
-                                          const_f64_ptr next, bool load_next) {
-    const double e0 = lorentz_t<FAST>(x, c[0], c[1], c[2]);
+__device__ __forceinline__ void sup_group(double x, double& acc, const double (&c)[3 * kSupGP],
+                                          double (&n)[3 * kSupGP], const_f64_ptr next, bool load_next) {
+    double e[kSupGP];
+    e[0] = lorentz_t<FAST>(x, c[0], c[1], c[2]);
     // the wait for c precedes e0; the next group's loads go out only after it
     __builtin_amdgcn_sched_barrier(0);
     if (load_next) {
 #pragma unroll
-        for (int k = 0; k < 12; ++k) n[k] = next[k];
+        for (int k = 0; k < 3 * kSupGP; ++k) n[k] = next[k];
     }
-    const double e1 = lorentz_t<FAST>(x, c[3], c[4], c[5]);
-    const double e2 = lorentz_t<FAST>(x, c[6], c[7], c[8]);
-    const double e3 = lorentz_t<FAST>(x, c[9], c[10], c[11]);
-    acc += e0;
-    acc += e1;
-    acc += e2;
-    acc += e3;
+#pragma unroll
+    for (int k = 1; k < kSupGP; ++k) e[k] = lorentz_t<FAST>(x, c[3 * k], c[3 * k + 1], c[3 * k + 2]);
+#pragma unroll
+    for (int k = 0; k < kSupGP; ++k) acc += e[k];
 }
 
 template <bool FAST>
-__device__ __forceinline__ double superpose_t(double x, const double* __restrict__ params_g, int P) {
+__device__ __forceinline__ double superpose_t(double x, const double* __restrict__ params_g, int P,
+                                              double acc = -0.0) {
     // Parameters are read-only for the whole launch: address space 4 (constant)
     // lets the backend issue s_load_dwordx* and feed SGPR operands to the VALU.
-    // Groups of 4 Lorentzians alternate between two SGPR buffers (A, B): each
+    // Groups of kSupGP Lorentzians alternate between two SGPR buffers (A, B): each
     // group's loads for the group after it are issued behind the group's first
     // evaluation, so their latency hides behind the rest of the group.
+    constexpr int GW = 3 * kSupGP;
     const const_f64_ptr params = (const_f64_ptr)(params_g);
-    double acc = -0.0;
-    const int G = P / 4;  // full groups
+    const int G = P / kSupGP;  // full groups
     int g = 0;
     if (G > 0) {
-        double A[12], B[12];
+        double A[GW], B[GW];
 #pragma unroll
-        for (int k = 0; k < 12; ++k) A[k] = params[k];
+        for (int k = 0; k < GW; ++k) A[k] = params[k];
         for (; g + 2 < G; g += 2) {
-            sup_group<FAST>(x, acc, A, B, params + 12 * (g + 1), true);
-            sup_group<FAST>(x, acc, B, A, params + 12 * (g + 2), true);
+            sup_group<FAST>(x, acc, A, B, params + GW * (g + 1), true);
+            sup_group<FAST>(x, acc, B, A, params + GW * (g + 2), true);
         }
         if (g + 1 < G) {
-            sup_group<FAST>(x, acc, A, B, params + 12 * (g + 1), true);
+            sup_group<FAST>(x, acc, A, B, params + GW * (g + 1), true);
             sup_group<FAST>(x, acc, B, A, params, false);
         } else {
             sup_group<FAST>(x, acc, A, B, params, false);
         }
     }
-    for (int j = 4 * G; j < P; ++j) {
+    for (int j = kSupGP * G; j < P; ++j) {
         const_f64_ptr L = params + 3 * j;
         acc += lorentz_t<FAST>(x, L[0], L[1], L[2]);
     }
@@ -2383,6 +2391,18 @@ __global__ __launch_bounds__(BS) void k_mse_partial(BatchArgs a, Workspace w, in
     }
 }
 
+// total length of the MSE regions of spectrum s (the divisor of compute_mse)
+__device__ __forceinline__ int64_t mse_len(const Workspace& w, int s) {
+    const int nig = w.n_ig[s];
+    int64_t total = 0;
+    for (int r = 0; r <= nig; ++r) {
+        int64_t lo, hi;
+        mse_region(w, s, r, nig, &lo, &hi);
+        total += hi - lo;
+    }
+    return total;
+}
+
 // One wave per spectrum: the nparts partial sums are folded left to right from +0.0
 // (the order k_mse_partial's tree fixes) with the ordered DPP fold, instead of a
 // single thread whose dependent global loads cost ~200 cycles each (42 us at B=1).
@@ -2398,14 +2418,7 @@ __global__ __launch_bounds__(64) void k_mse_final(BatchArgs a, Workspace w, int 
     }
     const double t = dpp_fold(0.0, w.mse_part + (size_t)s * nparts, nparts);
     if (threadIdx.x != 0) return;
-    const int nig = w.n_ig[s];
-    int64_t total = 0;
-    for (int r = 0; r <= nig; ++r) {
-        int64_t lo, hi;
-        mse_region(w, s, r, nig, &lo, &hi);
-        total += hi - lo;
-    }
-    a.out_mse[s] = t / (double)total;
+    a.out_mse[s] = t / (double)mse_len(w, s);
     a.out_status[s] = (w.kept_count[s] > a.cap) ? MDG_CAPACITY : MDG_OK;
 }
 

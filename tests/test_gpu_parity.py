@@ -354,6 +354,28 @@ def test_fit_superposition_kernels_batch(ctx, path, monkeypatch):
         assert np.array_equal(out[s, : counts[s]], o.params), s
         assert abs(mse[s] - o.mse) <= MSE_RTOL * abs(o.mse), s
 
+
+def test_mse_cases(ctx):
+    """The MSE against the oracle: ignore regions (two in one spectrum), a short
+    signal region (sim) and a batch whose spectra differ in peak count."""
+    for name in ["blood_01_water", "blood_02_two_regions_increasing", "sim_05", "synth_128k_2k_s0"]:
+        x, y, sb, st, ign = load_case(name)
+        o = oracle.deconvolute(x, y, sb, st, ignore=ign)
+        status, counts, out, mse = gpu_batch(ctx, x, y[None, :], [sb], st, ignore=ign)
+        assert status[0] == o.status == 0, name
+        assert np.array_equal(out[0, : counts[0]], o.params), name
+        assert abs(mse[0] - o.mse) <= MSE_RTOL * abs(o.mse), (name, mse[0], o.mse)
+    rows, ref = [], []
+    for seed in (6, 7, 8):
+        x, y = synth_spectrum(seed, n=65536, n_peaks=500 + 400 * (seed - 6))[:2]
+        rows.append(y)
+        ref.append(oracle.deconvolute(x, y, (11.8, -2.2)))
+    status, counts, out, mse = gpu_batch(ctx, x, np.stack(rows), [(11.8, -2.2)], oracle.default_settings())
+    for s, o in enumerate(ref):
+        assert status[s] == o.status == 0
+        assert np.array_equal(out[s, : counts[s]], o.params), s
+        assert abs(mse[s] - o.mse) <= MSE_RTOL * abs(o.mse), s
+
 def test_device_graph_replay(ctx, monkeypatch):
     """mdg_deconvolute_batch_device replays a cached hipGraph for repeated argument
     sets: refilling the same device buffers with other spectra must still give the
