@@ -37,6 +37,8 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "metabodecon-rust_amd")]
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (= FP64 matrix) peak, AMD spec
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E, MI355X_MICROARCH.md (spec)
 FLOPS_PER_EVAL = 5        # sub, mul, add, div, accumulate (div counted once)
+CLOCK_GHZ = 2.35          # shader clock measured by tools/ubench/eval_cost.hip (cycles / wall ns)
+CHAIN_FLOOR_CYC = 8.34    # two dependent v_fmac_f64 per smoother tick, one wave (eval_cost.hip)
 WORK_STAGES = ["fit_superposition", "mse_superposition", "smooth", "detect"]
 
 
@@ -217,20 +219,19 @@ def main():
     ws, iters = settings.smooth_window, settings.smooth_iterations
     smooth_kernel = (f"k_smooth_chain<{ws}>" if 2 <= ws <= 8 and B * iters <= 2048 and n >= 400
                      else f"k_smooth_waves<{ws}>" if B > 21 else f"k_smooth_pipe<{ws}>")
-    fit_kernel = ("k_fit_sup_dpp" if B <= 4 else "k_fit_sup_split<16,128,1024>" if B <= 16
-                  else "k_fit_sup")
+    fit_kernel = ("k_fit_sup_tf" if B <= 2 else "k_fit_sup_dpp" if B <= 12 else "k_fit_sup")
     work = {
         "fit_superposition": ("fp64", fit_flops, "TFLOP/s", fit_kernel),
         "mse_superposition": ("fp64", mse_flops, "TFLOP/s", "k_mse_partial<256>"),
         "smooth": ("hbm", smooth_bytes, "GB/s", smooth_kernel),
-        "detect": ("hbm", detect_bytes, "GB/s", "k_flags+k_peaks<1024>"),
+        "detect": ("hbm", detect_bytes, "GB/s", "k_flags+k_peaks_count+k_peaks_write"),
     }
     limiter = {
         "smooth": ("sequential running sums (moving_average.rs:69-80): 2 dependent f64 adds "
                    "per point per pass, one CU per pass; not bandwidth-bound"),
         "fit_superposition": "FP64 VALU issue (IEEE division sequence per evaluation)",
         "mse_superposition": "FP64 VALU issue (IEEE division sequence per evaluation)",
-        "detect": "single-workgroup ordered compaction (latency)",
+        "detect": "launch latency (three short kernels)",
     }
     stage_ms_step = {k: v[0] / prof_steps for k, v in stages.items() if v[1]}
     roofline = None
@@ -259,6 +260,16 @@ def main():
                     "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                     "avg_launch_ms": avg_s * 1e3, "algorithmic_per_launch": amount,
                     "limiter": limiter[dom]}
+        if dom == "smooth":
+            # the bound that does apply: one pass is N ticks of two dependent FP64 adds
+            # on one wave, passes pipelined on separate CUs, so a launch lasts about one
+            # pass. Floor: two dependent VOP2 v_fmac_f64 on SGPR operands per tick,
+            # 8.34 cycles (tools/ubench/eval_cost.hip), at the 2.35 GHz measured there.
+            cyc = avg_s * CLOCK_GHZ * 1e9 / n
+            roofline["issue_roofline"] = {
+                "unit": "cycles/tick", "achieved": cyc, "floor": CHAIN_FLOOR_CYC,
+                "frac": CHAIN_FLOOR_CYC / cyc, "clock_ghz": CLOCK_GHZ,
+                "source": "tools/ubench/eval_cost.hip ('smoother tick: 2 fmac SGPR')"}
 
     total_spectra = world * B * args.steps
     value = total_spectra / elapsed

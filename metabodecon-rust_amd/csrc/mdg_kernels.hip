@@ -143,7 +143,7 @@ __device__ int g_tf_mode = 0;
 __device__ int g_chain_mode = 0;  // chain_diag: 1 = feeder publishes everything at once, no scaler; 2 = no scaler; 3 = instant feeder  // fit_diag: 1 = evaluators skip LDS stores, 2 = skip evaluation
 #define KSTAMP(slot)                                                           \
     if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0 && g_diag)      \
-        g_diag[512 + (slot)] = (long long)__builtin_amdgcn_s_memtime()
+        g_diag[(1 << 16) + (slot)] = (long long)__builtin_amdgcn_s_memtime()
 #define DIAG_DECL unsigned long long _d_t = __builtin_amdgcn_s_memtime(); unsigned long long _d_acc[8] = {0};
 #define DIAG_STAMP(i)                                                       \
     do {                                                                    \
@@ -883,9 +883,10 @@ __global__ __launch_bounds__(192) void k_smooth_chain(BatchArgs a, Workspace w, 
     if (threadIdx.x < 64) {
         // ---------------------------- chain wave ----------------------------
         double sum = 0.0;  // T::zero()
-        // first steady block: 1; steady blocks k need CB*(k+1) + 8 <= N (group prefetch)
+        // first steady block: 1; steady blocks k need CB*(k+1) + 8 <= N (group prefetch);
+        // the steady loop runs MDG_CHAIN_BPT blocks per trip, the rest go generic
         const int kA = 1;
-        const int kB = max(kA, (N - 8) / CB);
+        const int kB = kA + max(0, (N - 8) / CB - kA) / MDG_CHAIN_BPT * MDG_CHAIN_BPT;
         int avail = 0;
         auto wait_in = [&](int need) -> bool {
             unsigned spins = 0;
@@ -930,7 +931,7 @@ __global__ __launch_bounds__(192) void k_smooth_chain(BatchArgs a, Workspace w, 
         if (ok && kB > kA) {
             int stat = 0;
             const int done = chain_steady<WS>(in + (size_t)kA * CB - 8, raw + (size_t)kA * CB, kA,
-                                              kB - kA, nIB,
+                                              (kB - kA) / MDG_CHAIN_BPT, nIB,
                                               lds_offset(&ctl), sum, stat);
             ok = stat == 0 && done == kB;
             if (ok) CTL_ST(raw_done, kB);

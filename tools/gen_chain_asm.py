@@ -3,7 +3,7 @@
 The steady-state loop of the chain wave of k_smooth_chain (mdg_kernels.hip),
 one asm string per window size WS in 2..8. It runs the reference running sum
 (moving_average.rs:69-80: `sum += v[j]`, then `sum -= popped`) on wave-uniform
-SGPR operands, one block of CB = 96 ticks per trip:
+SGPR operands, BPT blocks of CB = 96 ticks per loop trip:
 
   * operands: groups of 8 doubles of the pass input, s_load_dwordx16 into three
     rotating SGPR buffers (prev / cur / next); each group prefetches the next
@@ -16,16 +16,18 @@ SGPR operands, one block of CB = 96 ticks per trip:
     eval_cost.hip). Only the last sum of each group of 8 ticks is stored (see
     block_body), read from the previous group's pair while the next group runs;
   * per block: wait (LDS, cached) until the helper wave has published the input
-    block the prefetch reaches; after the block, s_waitcnt vmcnt(GROUPS) proves
-    the previous block's stores complete, then raw_done is published in LDS.
+    block the prefetch reaches; after the trip, s_waitcnt vmcnt(GROUPS) proves
+    the previous trip's stores complete, then raw_done is published in LDS.
 
 Fixed registers: s[40:87] operand buffers, s[88:99] loop state, v[0:18].
 Operand %[in] is the address of the group before the first block (in + CB*k0 - 8).
 """
 import os
 
-CB = 96              # ticks per block
-GROUPS = CB // 8     # 12 (multiple of 3: buffer rotation period)
+CB = 96              # ticks per block (the feeder / scaler / LDS staging unit)
+BPT = 1              # blocks per loop trip (2 measured: 20 cycles/tick against 13 -- keep 1)
+TT = CB * BPT        # ticks per trip
+GROUPS = TT // 8     # multiple of 3: buffer rotation period
 BUF = [40, 56, 72]   # SGPR base of the three 8-double buffers
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "metabodecon-rust_amd", "csrc", "mdg_chain_asm.inc")
@@ -46,7 +48,7 @@ def sreg(buf, e):
 
 
 def block_body(ws):
-    """12 groups of 8 ticks; after each group only its LAST running sum (the
+    """GROUPS groups of 8 ticks (BPT blocks); after each group only its LAST running sum (the
     checkpoint raw[8G+7]) is stored, one 8-byte store placed after the first add
     of the next group's second tick. The scaler wave recomputes the other seven
     sums of the group from the previous checkpoint with the same two operations
@@ -74,7 +76,7 @@ def block_body(ws):
             L.append(f"v_fmac_f64 {acc}, {pop}, {MONE}")
         L.append("s_waitcnt lgkmcnt(0)")
     if not os.environ.get("CHAIN_NOSTORE"):
-        L.append(f"global_store_dwordx2 {VZ}, {ACC[(GROUPS - 1) % 2]}, {RAW} offset:{8 * (CB - 1)}")
+        L.append(f"global_store_dwordx2 {VZ}, {ACC[(GROUPS - 1) % 2]}, {RAW} offset:{8 * (TT - 1)}")
     return L
 
 
@@ -98,8 +100,8 @@ def program(ws):
         f"s_load_dwordx16 s[{BUF[1]}:{BUF[1] + 15}], {IN}, 64",
         "s_waitcnt lgkmcnt(0)",
         "Lblk%=:",
-        # need = min(blk + 2, nib); re-read the helper's in_ready only when the cached value is short
-        f"s_add_u32 {NEED}, {BLK}, 2",
+        # need = min(blk + BPT + 1, nib); re-read the helper's in_ready only when the cached value is short
+        f"s_add_u32 {NEED}, {BLK}, {BPT + 1}",
         f"s_min_i32 {NEED}, {NEED}, {NIB}",
         f"s_cmp_ge_i32 {AVAIL}, {NEED}",
         "s_cbranch_scc1 Lgo%=",
@@ -126,14 +128,14 @@ def program(ws):
     ]
     L += block_body(ws)
     L += [
-        f"s_add_u32 {IN_LO}, {IN_LO}, {8 * CB}",
+        f"s_add_u32 {IN_LO}, {IN_LO}, {8 * TT}",
         f"s_addc_u32 {IN_HI}, {IN_HI}, 0",
-        f"s_add_u32 {RAW_LO}, {RAW_LO}, {8 * CB}",
+        f"s_add_u32 {RAW_LO}, {RAW_LO}, {8 * TT}",
         f"s_addc_u32 {RAW_HI}, {RAW_HI}, 0",
         f"s_waitcnt vmcnt({GROUPS})",
         f"v_mov_b32 {VT}, {BLK}",
         f"ds_write_b32 {LDSA}, {VT} offset:4",   # raw_done = blocks < blk complete
-        f"s_add_u32 {BLK}, {BLK}, 1",
+        f"s_add_u32 {BLK}, {BLK}, {BPT}",
         f"s_sub_u32 {CNT}, {CNT}, 1",
         f"s_cmp_lg_u32 {CNT}, 0",
         "s_cbranch_scc1 Lblk%=",
@@ -149,7 +151,7 @@ def program(ws):
 def main():
     lines = ["// Generated by tools/gen_chain_asm.py -- do not edit.",
              f"// Steady loop of the k_smooth_chain chain wave, CB = {CB} ticks per block.",
-             f"#define MDG_CHAIN_CB {CB}", ""]
+             f"#define MDG_CHAIN_CB {CB}", f"#define MDG_CHAIN_BPT {BPT}", ""]
     for ws in range(2, 9):
         body = program(ws)
         lines.append(f"#define MDG_CHAIN_ASM_{ws} \\")
