@@ -809,18 +809,16 @@ MDG_CHAIN_STEADY(8)
 
 // touch the 64-byte lines of one input block (scalar cache prefetch for the chain)
 __device__ __forceinline__ void chain_touch(const double* p) {
-    asm volatile(
-        "s_load_dwordx16 s[40:55], %0, 0\n s_load_dwordx16 s[40:55], %0, 64\n"
-        "s_load_dwordx16 s[40:55], %0, 128\n s_load_dwordx16 s[40:55], %0, 192\n"
-        "s_load_dwordx16 s[40:55], %0, 256\n s_load_dwordx16 s[40:55], %0, 320\n"
-        "s_load_dwordx16 s[40:55], %0, 384\n s_load_dwordx16 s[40:55], %0, 448\n"
-        "s_load_dwordx16 s[40:55], %0, 512\n s_load_dwordx16 s[40:55], %0, 576\n"
-        "s_load_dwordx16 s[40:55], %0, 640\n s_load_dwordx16 s[40:55], %0, 704\n"
-        "s_waitcnt lgkmcnt(0)\n" ::"s"(sgpr_ptr(p))
-        : "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51",
-          "s52", "s53", "s54", "s55", "memory");
+    static_assert(kChainCB % 8 == 0, "whole 64-byte lines per block");
+    const auto q = sgpr_ptr(p);
+#pragma unroll
+    for (int k = 0; k < kChainCB / 8; ++k)
+        asm volatile("s_load_dwordx16 s[40:55], %0, %1" ::"s"(q), "i"(64 * k)
+                     : "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50",
+                       "s51", "s52", "s53", "s54", "s55", "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
-static_assert(kChainCB * 8 == 768, "chain_touch covers 12 lines of one block");
+
 
 // load cnt consecutive blocks (this lane's 16 bytes of each) into L2 and wait:
 // one asm statement, so no in-flight load can land in a register the compiler

@@ -24,7 +24,7 @@ Operand %[in] is the address of the group before the first block (in + CB*k0 - 8
 """
 import os
 
-CB = 96              # ticks per block (the feeder / scaler / LDS staging unit)
+CB = int(os.environ.get("CHAIN_CB", "96"))  # ticks per block (the feeder / scaler / LDS staging unit)
 BPT = 1              # blocks per loop trip (2 measured: 20 cycles/tick against 13 -- keep 1)
 TT = CB * BPT        # ticks per trip
 GROUPS = TT // 8     # multiple of 3: buffer rotation period
