@@ -21,7 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STAGES = [  # stage -> kernel-name prefixes (after "mdg::")
     ("smooth", ("k_smooth",)),
     ("detect", ("k_flags", "k_peaks")),
-    ("select", ("k_select",)),
+    ("select", ("k_scores", "k_select")),
     ("fit_init", ("k_fit_init",)),
     ("fit_superposition", ("k_fit_sup",)),
     ("fit_update", ("k_fit_update",)),
