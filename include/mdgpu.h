@@ -181,6 +181,13 @@ int mdg_superposition_vec(mdg_ctx* ctx, const double* x, size_t n, const mdg_lor
 int mdg_superposition_vec_device(mdg_ctx* ctx, const double* d_x, size_t n,
                                  const mdg_lorentzian* d_L, size_t p, double* d_out);
 
+/* Test support: acc0 + t[0] + ... + t[n-1] as a left fold (one rounding per add),
+ * computed on the device by the windowed parallel fold that k_select uses for the
+ * signal-free-region statistics (noise_score_filter.rs:129-138). The terms must be
+ * >= +0 (MDG_INVALID_ARGUMENT otherwise); the result is bit-identical to the
+ * sequential fold whatever the data. */
+int mdg_ordered_sum(mdg_ctx* ctx, const double* t, size_t n, double acc0, double* out);
+
 /* Device synthetic batch: d_x (n, shared axis x_i = xmax - (i*width)/(n-1)) and
  * d_y (b x n): y_s = in-order superposition of mdg_synth_lorentzians(seed0+s) +
  * mdg_synth_noise(seed0+s). */

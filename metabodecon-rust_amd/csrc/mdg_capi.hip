@@ -819,6 +819,24 @@ int mdg_superposition_vec(mdg_ctx* c, const double* x, size_t n, const mdg_loren
     return MDG_OK;
 }
 
+int mdg_ordered_sum(mdg_ctx* c, const double* t, size_t n, double acc0, double* out) {
+    if (!c || (!t && n) || !out || n > (size_t)INT32_MAX) return MDG_INVALID_ARGUMENT;
+    for (size_t i = 0; i < n; ++i)
+        if (!(t[i] >= 0.0) || std::signbit(t[i])) return MDG_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    int rc;
+    if ((rc = ensure(c->st_x, std::max<size_t>(n, 1) * 8))) return rc;
+    if ((rc = ensure(c->st_flag, 256))) return rc;
+    if (n) HIPCHK(hipMemcpyAsync(c->st_x.p, t, n * 8, hipMemcpyHostToDevice, st));
+    launch_ordered_sum((const double*)c->st_x.p, (int)n, acc0, (double*)c->st_flag.p, st);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(out, c->st_flag.p, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return MDG_OK;
+}
+
 int mdg_synth_batch_device(mdg_ctx* c, size_t b, size_t n, double xmax, double width,
                            uint64_t seed0, size_t n_peaks, double lo, double hi, double sigma,
                            double* d_x, double* d_y) {

@@ -1579,12 +1579,128 @@ __device__ double dpp_fold(double acc, const double* __restrict__ t, int n) {
     return acc;
 }
 
+// ----------------------------------------------------------------------------------
+// Windowed fold: acc0 + t[0] + ... + t[n-1], left to right with a rounding per add,
+// for NON-NEGATIVE terms, by the whole workgroup instead of one wave.
+//
+// The n terms (global memory, L2-resident) are cut into kWinSeg segments. A
+// running sum of non-negative terms grows monotonically and stays close to the
+// correctly rounded exact prefix sum (tools/probes/fold_window.py: at most 31
+// ulps for the SFR scores and squared deviations of every probed spectrum). So:
+//  A. the exact prefix sum at each segment start is estimated in double-double
+//     and rounded: E_k;
+//  B. each segment is folded from 64 candidate start values at once, lane j
+//     starting from E_k stepped by (j - 32) ulps (consecutive doubles), with the
+//     reference's additions (dpp_fold: every lane adds the same term, in order);
+//  C. one wave walks the segments in order: the true value entering segment k is
+//     one of its candidates (bit-equal) -> the true value leaving it is that
+//     lane's result. A true value outside the window is not an error: that
+//     segment is folded again from it.
+// Every step of the returned value is an IEEE add in the reference's order, so
+// the result is the reference's bits whatever the estimates (they only decide
+// how often step C falls back).
+// ----------------------------------------------------------------------------------
+constexpr int kWinSeg = 32;
+struct WinLds {
+    double F[kWinSeg][64];
+    double E[kWinSeg];
+    double out;
+};
+
+__device__ __forceinline__ void two_sum(double a, double b, double& s, double& e) {
+    s = a + b;
+    const double bb = s - a;
+    e = (a - (s - bb)) + (b - bb);
+}
+
+template <int BS>
+__device__ double window_fold(double acc0, WinLds& L, const double* __restrict__ t, int n) {
+    constexpr int NW = BS / 64;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int seg = (n + kWinSeg - 1) / kWinSeg;
+    // A. double-double sums of the segments (wave w: segments w, w+NW, ...)
+    for (int k = wv; k < kWinSeg; k += NW) {
+        double hi = 0.0, lo = 0.0;
+        for (int i = k * seg + lane; i < min(n, (k + 1) * seg); i += 64) {
+            double e;
+            two_sum(hi, t[i], hi, e);
+            lo += e;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const double h2 = __shfl_xor(hi, o, 64), l2 = __shfl_xor(lo, o, 64);
+            double e;
+            two_sum(hi, h2, hi, e);
+            lo += l2 + e;
+        }
+        if (lane == 0) L.F[k][0] = hi, L.F[k][1] = lo;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double hi = acc0 == 0.0 ? 0.0 : acc0, lo = 0.0;
+        for (int k = 0; k < kWinSeg; ++k) {
+            double e;
+            two_sum(hi, lo, hi, lo);  // renormalise
+            L.E[k] = hi;
+            two_sum(hi, L.F[k][0], hi, e);
+            lo += L.F[k][1] + e;
+        }
+    }
+    __syncthreads();
+    KSTAMP(40);
+    // B. every segment from 64 candidates (segment 0 from acc0 itself, exactly)
+    for (int k = wv; k < kWinSeg; k += NW) {
+        double acc;
+        if (k == 0) {
+            acc = acc0;
+        } else {
+            const long long b = __double_as_longlong(L.E[k]) + (lane - 32);
+            acc = __longlong_as_double(b < 0 ? 0ll : b);
+        }
+        const int i0 = min(n, k * seg), i1 = min(n, (k + 1) * seg);
+        L.F[k][lane] = dpp_fold(acc, t + i0, i1 - i0);
+    }
+    __syncthreads();
+    KSTAMP(41);
+    // C. the true chain through the segments, by wave 0
+    if (wv == 0) {
+        double tru = readlane_f64(L.F[0][lane], 0);
+        for (int k = 1; k < kWinSeg; ++k) {
+            const long long b = __double_as_longlong(L.E[k]) + (lane - 32);
+            const long long cand = b < 0 ? 0ll : b;
+            const unsigned long long hit = __ballot(cand == __double_as_longlong(tru));
+            if (hit) {
+                tru = readlane_f64(L.F[k][lane], __ffsll((unsigned long long)hit) - 1);
+            } else {  // outside the window: this segment from the true value
+                const int i0 = min(n, k * seg), i1 = min(n, (k + 1) * seg);
+                tru = dpp_fold(tru, t + i0, i1 - i0);
+            }
+        }
+        if (lane == 0) L.out = tru;
+    }
+    __syncthreads();
+    KSTAMP(42);
+    return L.out;
+}
+
+// test support (mdg_ordered_sum): the windowed fold of k_select on caller data
+__global__ __launch_bounds__(1024) void k_ordered_sum(const double* __restrict__ t, int n, double acc0,
+                                                      double* out) {
+    __shared__ WinLds wl;
+    const double r = window_fold<1024>(acc0, wl, t, n);
+    if (threadIdx.x == 0) out[0] = r;
+}
+void launch_ordered_sum(const double* t, int n, double acc0, double* out, hipStream_t st) {
+    hipLaunchKernelGGL(k_ordered_sum, dim3(1), dim3(1024), 0, st, t, n, acc0, out);
+}
+
 template <int BS>
 __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double threshold) {
     const int s = blockIdx.x;
     __shared__ int lds_i[BS / 64 + 1];
     __shared__ long long lds_l[BS / 64 + 1];
     __shared__ double thr_sh;
+    __shared__ WinLds wl;
     if (w.status[s]) return;
     const int P = w.det_count[s];
     if (P == 0) {  // peaks.len() - 1 underflows in peak_region_boundaries
@@ -1624,33 +1740,37 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
     // peaks[..left] ++ peaks[right..], staged contiguously (all threads) and folded
     // by wave 0; then the squared deviations, staged in place, folded the same way
     const int n_sfr = left + (P - right);
+    // scores and squared deviations are >= +0: the windowed fold applies (one wave
+    // folds short sets itself)
+    const bool win = n_sfr >= 4 * kWinSeg;
     double* sfr = w.tmp0 + (size_t)s * a.N;
     for (int k = threadIdx.x; k < n_sfr; k += BS) sfr[k] = scores[k < left ? k : right + (k - left)];
     __syncthreads();
-    if (threadIdx.x < 64) {
-        KSTAMP(15);
+    KSTAMP(15);
+    if (win) {
+        const double sum = window_fold<BS>(-0.0, wl, sfr, n_sfr);  // every thread: barriers inside
+        if (threadIdx.x == 0) thr_sh = sum / (double)n_sfr;
+    } else if (threadIdx.x < 64) {
         const double mean = dpp_fold(-0.0, sfr, n_sfr) / (double)n_sfr;
-        KSTAMP(16);
         if (threadIdx.x == 0) thr_sh = mean;
     }
     __syncthreads();
-    KSTAMP(12);
+    KSTAMP(16);
     const double mean = thr_sh;
     for (int k = threadIdx.x; k < n_sfr; k += BS) {
         const double d = sfr[k] - mean;
         sfr[k] = d * d;
     }
     __syncthreads();
-    if (threadIdx.x < 64) {
-        KSTAMP(17);
-        const double var = dpp_fold(-0.0, sfr, n_sfr) / (double)n_sfr;
-        KSTAMP(18);
+    double var = 0.0;
+    if (win) var = window_fold<BS>(-0.0, wl, sfr, n_sfr) / (double)n_sfr;
+    else if (threadIdx.x < 64) var = dpp_fold(-0.0, sfr, n_sfr) / (double)n_sfr;
+    KSTAMP(17);
+    if (threadIdx.x == 0) {
         const double sd = __builtin_sqrt(var);
-        if (threadIdx.x == 0) {
-            thr_sh = mean + (w.thr_s ? w.thr_s[s] : threshold) * sd;
-            w.sfr_stats[2 * s] = mean;
-            w.sfr_stats[2 * s + 1] = sd;
-        }
+        thr_sh = mean + (w.thr_s ? w.thr_s[s] : threshold) * sd;
+        w.sfr_stats[2 * s] = mean;
+        w.sfr_stats[2 * s + 1] = sd;
     }
     KSTAMP(13);
     __syncthreads();

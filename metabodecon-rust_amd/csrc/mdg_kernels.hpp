@@ -117,6 +117,8 @@ void launch_fit_update(const BatchArgs& a, const Workspace& w, int gx, int it, h
 void launch_retain(const BatchArgs& a, const Workspace& w, hipStream_t st);
 void launch_mse(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st);
 void launch_mse_final(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st);
+// windowed left fold of n <= kWinMax non-negative terms (test support)
+void launch_ordered_sum(const double* t, int n, double acc0, double* out, hipStream_t st);
 void launch_superposition_vec(const double* x, int64_t n, const double* params, int P,
                               double* out, int* flag, hipStream_t st);
 void launch_synth(double* x, double* y, int64_t n, int B, double xmax, double width,

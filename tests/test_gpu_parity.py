@@ -376,6 +376,41 @@ def test_mse_cases(ctx):
         assert np.array_equal(out[s, : counts[s]], o.params), s
         assert abs(mse[s] - o.mse) <= MSE_RTOL * abs(o.mse), s
 
+
+def _left_fold(acc, terms):
+    for t in terms:
+        acc = acc + float(t)
+    return acc
+
+
+def test_ordered_sum_window_fold(ctx):
+    """The windowed parallel fold behind k_select's SFR mean/variance equals the
+    sequential left fold bit for bit, including inputs that defeat its candidate
+    windows (a huge first term, then a long tail of terms below half an ulp; wide
+    dynamic range; zeros; subnormals; exact ties) and so run its fallback path."""
+    rng = np.random.default_rng(11)
+    cases = [
+        rng.uniform(0, 1e3, 8418),
+        rng.exponential(300.0, 5116) ** 2,
+        np.concatenate([[1e16], rng.uniform(0, 0.9, 4000)]),
+        10.0 ** rng.uniform(-300, 300, 3000),
+        np.zeros(500),
+        np.concatenate([np.full(100, 5e-324), rng.uniform(0, 1e-310, 900)]),
+        np.full(4096, 0.5) * np.arange(4096) % 7,
+        rng.uniform(0, 1, 129),
+        rng.uniform(0, 1e6, 16384),
+        rng.uniform(0, 1e6, 40000),
+    ]
+    for k, t in enumerate(cases):
+        t = np.ascontiguousarray(t, dtype=np.float64)
+        out = ctypes.c_double()
+        rc = nat.lib().mdg_ordered_sum(ctx.handle, nat.ptr(t), t.size, -0.0, ctypes.byref(out))
+        assert rc == 0, nat.strerror(rc)
+        ref = _left_fold(-0.0, t)
+        assert np.float64(out.value).tobytes() == np.float64(ref).tobytes(), (k, out.value, ref)
+    bad = np.array([1.0, -1.0])
+    assert nat.lib().mdg_ordered_sum(ctx.handle, nat.ptr(bad), 2, -0.0, ctypes.byref(out)) != 0
+
 def test_device_graph_replay(ctx, monkeypatch):
     """mdg_deconvolute_batch_device replays a cached hipGraph for repeated argument
     sets: refilling the same device buffers with other spectra must still give the

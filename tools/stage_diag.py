@@ -40,7 +40,7 @@ for _ in range(3):
     torch.cuda.synchronize()
 d = diag.cpu().tolist()[1 << 16:]
 groups = {"select": range(10, 19), "peaks": range(0, 5), "fit_dpp": range(20, 24),
-          "mse": range(30, 34)}
+          "mse": range(30, 34), "window": [15, 40, 41, 42, 16]}
 for name, r in groups.items():
     v = [d[k] for k in r]
     if not any(v):
