@@ -219,7 +219,7 @@ def main():
     ws, iters = settings.smooth_window, settings.smooth_iterations
     smooth_kernel = (f"k_smooth_chain<{ws}>" if 2 <= ws <= 8 and B * iters <= 2048 and n >= 400
                      else f"k_smooth_waves<{ws}>" if B > 21 else f"k_smooth_pipe<{ws}>")
-    fit_kernel = ("k_fit_sup_tf" if B <= 2 else "k_fit_sup_dpp" if B <= 12 else "k_fit_sup")
+    fit_kernel = ("k_fit_sup_tf" if B <= 2 else "k_fit_sup_dpp" if B <= 8 else "k_fit_sup")
     work = {
         "fit_superposition": ("fp64", fit_flops, "TFLOP/s", fit_kernel),
         "mse_superposition": ("fp64", mse_flops, "TFLOP/s", "k_mse_partial<256>"),

@@ -34,18 +34,22 @@ __device__ __forceinline__ double lorentz(double x, double sfhw, double hw2, dou
 // wrappers. hipcc expands `n / d` to: div_scale x2, rcp, two Newton steps
 // (fma, fma), q0 = n*r, rem = fma(-d, q0, n), div_fmas(rem, r, q0), div_fixup.
 // When div_scale does not scale (|n|, |d| in [2^-200, 2^203], quotient normal)
-// div_fmas is a plain fma and div_fixup returns its input, so this sequence
-// yields the SAME bits. Callers use it only for spectra whose flags prove the
-// operand ranges (peak_fast_ok + x_ok below); everything else takes `/`.
+// div_fmas is a plain fma and div_fixup returns its input. This sequence also
+// stops after ONE Newton step: the reciprocal then differs from the two-step one
+// in about a third of the cases (by an ulp), but the final residual correction
+// q0 + fma(-d, q0, n) * r gives the quotient of `/` bit for bit -- checked on
+// 4.4e12 random operand pairs over the whole range, mantissas random or with
+// long runs of ones / zeros (tools/ubench/div_check.hip), and by every parity
+// test. 9 instead of 11 issue slots plus the quarter-rate rcp per evaluation.
+// Callers use it only for spectra whose flags prove the operand ranges
+// (peak_fast_ok + x_ok below); everything else takes `/`.
 __device__ __forceinline__ double div_rn_fast(double n, double d) {
     const double r0 = __builtin_amdgcn_rcp(d);
     const double e0 = __builtin_fma(-d, r0, 1.0);
     const double r1 = __builtin_fma(r0, e0, r0);
-    const double e1 = __builtin_fma(-d, r1, 1.0);
-    const double r2 = __builtin_fma(r1, e1, r1);
-    const double q0 = n * r2;
+    const double q0 = n * r1;
     const double rem = __builtin_fma(-d, q0, n);
-    return __builtin_fma(rem, r2, q0);
+    return __builtin_fma(rem, r1, q0);
 }
 
 // Ranges under which sfhw / (hw2 + (x - maxp)^2) may use div_rn_fast: with
@@ -1942,7 +1946,7 @@ __device__ __forceinline__ void fold_partial(double& acc, double t, double one, 
 }
 
 // fold16 of ei into acc, interleaved with the FAST evaluation (lorentz_t<true>:
-// (x - mp)^2 + hw, then div_rn_fast's exact sequence) of the next group, returned:
+// (x - mp)^2 + hw, then div_rn_fast's sequence, one Newton step) of the next group, returned:
 // two independent dependency chains share the issue slots
 __device__ __forceinline__ double fold16_eval_fast(double& acc, double ei, double one, double x,
                                                    double sf, double hw, double mp) {
@@ -1962,9 +1966,7 @@ __device__ __forceinline__ double fold16_eval_fast(double& acc, double ei, doubl
         "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:5 row_mask:0xf bank_mask:0xf\n"
         "v_fma_f64 %[r], %[r], %[t], %[r]\n"
         "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:6 row_mask:0xf bank_mask:0xf\n"
-        "v_fma_f64 %[t], -%[den], %[r], 1.0\n"
         "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:7 row_mask:0xf bank_mask:0xf\n"
-        "v_fma_f64 %[r], %[r], %[t], %[r]\n"
         "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
         "v_mul_f64 %[q], %[sf], %[r]\n"
         "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:9 row_mask:0xf bank_mask:0xf\n"
@@ -2017,12 +2019,8 @@ __device__ __forceinline__ void fold2_eval_fast(double& accA, double& accB, doub
         "v_fma_f64 %[rB], %[rB], %[tB], %[rB]\n"
         "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:6 row_mask:0xf bank_mask:0xf\n"
         "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:6 row_mask:0xf bank_mask:0xf\n"
-        "v_fma_f64 %[tA], -%[denA], %[rA], 1.0\n"
-        "v_fma_f64 %[tB], -%[denB], %[rB], 1.0\n"
         "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:7 row_mask:0xf bank_mask:0xf\n"
         "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:7 row_mask:0xf bank_mask:0xf\n"
-        "v_fma_f64 %[rA], %[rA], %[tA], %[rA]\n"
-        "v_fma_f64 %[rB], %[rB], %[tB], %[rB]\n"
         "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
         "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
         "v_mul_f64 %[qA], %[sf], %[rA]\n"
@@ -2278,14 +2276,18 @@ __global__ __launch_bounds__(64 * (kTfEW + 1)) void k_fit_sup_tf(BatchArgs a, Wo
     else fit_tf_body<false>(w, s, P, it, T);
 }
 
+// 1-D grid, spectrum = block % B (as k_mse_partial): round-robin dispatch puts the
+// workgroups a CU holds at once on the same spectrum, so they share its Lorentzians
+// in the scalar cache instead of each streaming another spectrum's table
 __global__ void k_fit_sup(BatchArgs a, Workspace w, int it) {
-    const int s = blockIdx.y;
+    const int s = blockIdx.x % a.B, part = blockIdx.x / a.B, parts = gridDim.x / a.B;
     if (w.status[s] || fit_done(w, s, it)) return;
     const int P = w.sel_count[s];
     const size_t base = (size_t)s * w.capD;
     const double* __restrict__ params = w.params + 3 * base;
-    const bool fast = fit_fast(w, s, it);
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < 3 * P; i += gridDim.x * blockDim.x) {
+    if (part == 0 && threadIdx.x == 0) w.unsafe[4 * s + ((it + 1) & 1)] = 0;
+    const bool fast = w.x_ok[s] && w.unsafe[4 * s + (it & 1)] == 0;
+    for (int i = part * blockDim.x + threadIdx.x; i < 3 * P; i += parts * blockDim.x) {
         const double sup = superpose(w.rx[3 * base + i], params, P, fast);
         w.ratio[3 * base + i] = w.ry[3 * base + i] / sup;
     }
@@ -2710,15 +2712,15 @@ void launch_select(const BatchArgs& a, const Workspace& w, int detector_only, do
 void launch_fit_init(const BatchArgs& a, const Workspace& w, int gx, hipStream_t st) {
     hipLaunchKernelGGL(k_fit_init, dim3(gx, a.B), dim3(256), 0, st, a, w);
 }
-// Fit kernel choice by measurement (bench, P = 2048, ms per 10 launches):
-//   B=1 tf 0.207 / dpp 0.280 / plain 1.69;  B=2 tf 0.361 / dpp 0.423;
-//   B=4 dpp 0.609 / tf 0.665;  B=8 dpp 1.41 / tf 1.46 / plain 2.49;
-//   B=16 dpp 2.54 / plain 2.64;  B=32 plain 3.16 / dpp 4.76;  B=256 plain 15.7 / dpp 32.6.
+// Fit kernel choice by measurement (tools/fit_sweep.sh, P = 2048, ms per 10 launches):
+//   B=1 tf 0.215 / dpp 0.277 / plain 0.81;  B=2 tf 0.369 / dpp 0.428;
+//   B=4 dpp 0.589 / tf 0.668;  B=8 dpp 1.37 / plain 1.44 / tf 1.46;
+//   B=12 plain 1.57 / dpp 1.96;  B=256 plain 12.0 / tf 25.4 / dpp 30.6.
 // MDG_FITSUP = tf | dpp | split | plain forces one (tests, tuning).
 static std::string fit_choice(const BatchArgs& a) {
     const char* force = std::getenv("MDG_FITSUP");
     if (force && *force) return force;
-    return a.B <= 2 ? "tf" : a.B <= 12 ? "dpp" : "plain";
+    return a.B <= 2 ? "tf" : a.B <= 8 ? "dpp" : "plain";
 }
 bool fit_sup_fused(const BatchArgs& a) { return fit_choice(a) == "tf"; }
 void launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st) {
@@ -2738,7 +2740,7 @@ void launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int it, hipS
         hipLaunchKernelGGL((k_fit_sup_split<16, 128, 1024>), dim3(g, a.B), dim3(1024), 0, st, a, w, it);
     } else {
         // gx 256-thread workgroups per spectrum (24: one point per thread at P = 2048)
-        hipLaunchKernelGGL(k_fit_sup, dim3(gx, a.B), dim3(256), 0, st, a, w, it);
+        hipLaunchKernelGGL(k_fit_sup, dim3(gx * a.B), dim3(256), 0, st, a, w, it);
     }
 }
 void launch_fit_update(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st) {
