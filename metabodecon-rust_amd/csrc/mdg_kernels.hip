@@ -884,6 +884,9 @@ __global__ __launch_bounds__(192) void k_smooth_chain(BatchArgs a, Workspace w, 
 
     if (threadIdx.x < 64) {
         // ---------------------------- chain wave ----------------------------
+        // top priority: the feeder and scaler share the CU's issue paths with it
+        // (chain_diag: 13.0 -> 12.8 / 14.2 -> 13.6 cycles per tick, passes 1 / 3)
+        __builtin_amdgcn_s_setprio(3);
         double sum = 0.0;  // T::zero()
         // first steady block: 1; steady blocks k need CB*(k+1) + 8 <= N (group prefetch);
         // the steady loop runs MDG_CHAIN_BPT blocks per trip, the rest go generic
@@ -1001,6 +1004,10 @@ __global__ __launch_bounds__(192) void k_smooth_chain(BatchArgs a, Workspace w, 
         if (!ok) CTL_ST(abort, 1);
     } else {
         // ---------------------------- scaler wave ----------------------------
+        // the reference's div = 1/len (moving_average.rs:66-81), one division per len
+        double inv_len[WS + 1];
+#pragma unroll
+        for (int k = 0; k <= WS; ++k) inv_len[k] = 1.0 / (double)(k > 0 ? k : 1);
         // scales every finished raw block by 1/len and publishes them in one batch
         // (sc1 stores, vmcnt(0), sc1 counter: the downstream pass polls it)
         constexpr int MAXB = 8;                   // blocks per batch
@@ -1065,7 +1072,7 @@ __global__ __launch_bounds__(192) void k_smooth_chain(BatchArgs a, Workspace w, 
                 for (int i = i0 + lane; i < i1; i += 64) {
                     // len of the circular buffer after tick i (moving_average.rs:66-81)
                     const int len = i < N - R ? min(i + R + 1, WS) : WS - 1 - (i - (N - R));
-                    __hip_atomic_store(out + i, sc_raw[i + R - base] * (1.0 / (double)len),
+                    __hip_atomic_store(out + i, sc_raw[i + R - base] * inv_len[len],
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
