@@ -134,7 +134,8 @@ int mdg_deconvolute(mdg_ctx* ctx, const double* x, const double* y, size_t n, do
 
 /* Batch of b spectra of n points. Row i of x is x + i*x_stride (x_stride 0 =
  * one shared axis), row i of y is y + i*y_stride. sb: b (sb0,sb1) pairs.
- * out: b*cap Lorentzians (row i at out + i*cap). counts/mse/status: b each.
+ * out: b*cap Lorentzians (row i at out + i*cap); only rows below counts[i] are
+ * written. counts/mse/status: b each.
  * Returns the first nonzero status (the reference's fail-fast error) or 0. */
 int mdg_deconvolute_batch(mdg_ctx* ctx, size_t b, size_t n, const double* x, size_t x_stride,
                           const double* y, size_t y_stride, const double* sb,

@@ -751,7 +751,14 @@ int mdg_deconvolute_batch(mdg_ctx* c, size_t b, size_t n, const double* x, size_
     HIPCHK(hipMemcpyAsync(cnt.data(), c->st_cnt.p, b * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(stv.data(), c->st_status.p, b * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(mse, c->st_mse.p, b * 8, hipMemcpyDeviceToHost, st));
-    if (cap) HIPCHK(hipMemcpyAsync(out, c->st_out.p, b * cap * 24, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    // only the rows the spectra filled travel back (cap is usually N/2 + 2 rows,
+    // 1.5 MiB per 131072-point spectrum, against ~24 KiB of Lorentzians)
+    size_t rows = 0;
+    for (size_t i = 0; i < b; ++i) rows = std::max(rows, std::min(cap, (size_t)std::max(0, cnt[i])));
+    if (rows)
+        HIPCHK(hipMemcpy2DAsync(out, cap * 24, c->st_out.p, cap * 24, rows * 24, b,
+                                hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     drain_timers(c);
     int first = MDG_OK;
