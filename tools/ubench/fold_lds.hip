@@ -1,30 +1,10 @@
-// LDS-fed ordered fold microbenchmark (gfx950): one wave folds rows of 192 terms
-// (lane = row, row stride 194 doubles) with the library's fold_row24 asm; variants
-// vary the lanes' row addresses to separate LDS latency/bandwidth from the chain.
+// LDS-fed ordered fold microbenchmark (gfx950): one wave folds 192-term rows with
+// ds_read_b128 feeding dependent v_fmac_f64; variants separate the LDS read cost,
+// the fmac chain and the waits (EXEC = 24 lanes: the term-fold fit's fold wave).
 #include "../../metabodecon-rust_amd/csrc/mdg_kernels.hip"
 #include <cstdio>
 using namespace mdg;
 constexpr int RS = 194;
-template <int MODE>
-__global__ void k_fold(double* out, long long* cyc, int reps) {
-    __shared__ __attribute__((aligned(16))) double T[24 * RS];
-    for (int i = threadIdx.x; i < 24 * RS; i += blockDim.x) T[i] = 1.0 + i * 1e-9;
-    __syncthreads();
-    const int lane = threadIdx.x & 63;
-    int q = lane < 24 ? lane : 23;
-    if (MODE == 1) q = 0;            // every lane on row 0 (broadcast)
-    if (MODE == 2) q = lane % 24;    // 64 distinct-ish rows
-    double acc = -0.0;
-    if (MODE == 3 && lane >= 24) return;
-    if (MODE == 4 && lane >= 8) return;
-    if (MODE == 5 && lane >= 1) return;
-    const long long t0 = __builtin_amdgcn_s_memtime();
-    for (int r = 0; r < reps; ++r) acc = fold_row24(acc, lds_offset(T + q * RS), 192 / 24 - 1);
-    const long long t1 = __builtin_amdgcn_s_memtime();
-    out[threadIdx.x] = acc;
-    if (threadIdx.x == 0) cyc[0] = t1 - t0;
-}
-
 // raw loop variants: 12 b128 reads + 24 fmacs per trip (192 terms = 8 trips)
 #define RD(r, off) "ds_read_b128 v[" #r "], %[a] offset:" #off "\n"
 #define FM(lo) "v_fmac_f64 %[acc], v[" #lo "], %[one]\n"
@@ -42,13 +22,15 @@ __global__ void k_raw(double* out, long long* cyc, int reps) {
     for (int i = threadIdx.x; i < 24 * RS; i += blockDim.x) T[i] = 1.0 + i * 1e-9;
     __syncthreads();
     double acc = -0.0; const double one = 1.0;
-    unsigned a = lds_offset(T);
+    unsigned a = lds_offset(T) + (threadIdx.x & 63) * (RS * 8 % 4096 == 0 ? 16 : 0);
+    if (V >= 4 && (threadIdx.x & 63) >= 24) return;  // EXEC = 24 lanes
     const long long t0 = __builtin_amdgcn_s_memtime();
     for (int r = 0; r < reps * 8; ++r) {
         if (V == 0) asm volatile(TRIP_BOTH : [acc] "+v"(acc) : [a] "v"(a), [one] "v"(one) : CLOB12);
         if (V == 1) asm volatile(TRIP_FMA : [acc] "+v"(acc) : [a] "v"(a), [one] "v"(one) : CLOB12);
         if (V == 2) asm volatile(TRIP_RD "s_waitcnt lgkmcnt(0)\n" : [acc] "+v"(acc) : [a] "v"(a), [one] "v"(one) : CLOB12);
-        if (V == 3) asm volatile(TRIP_RD : [acc] "+v"(acc) : [a] "v"(a), [one] "v"(one) : CLOB12);
+        if (V == 3 || V == 5) asm volatile(TRIP_RD : [acc] "+v"(acc) : [a] "v"(a), [one] "v"(one) : CLOB12);
+        if (V == 4) asm volatile(TRIP_BOTH : [acc] "+v"(acc) : [a] "v"(a), [one] "v"(one) : CLOB12);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const long long t1 = __builtin_amdgcn_s_memtime();
@@ -67,16 +49,11 @@ int main() {
         long long c; (void)hipMemcpy(&c, cyc, 8, hipMemcpyDeviceToHost);
         printf("%-34s threads=%d  %.2f cycles/term\n", name, threads, (double)c / (reps * 192.0));
     };
-    run(k_fold<0>, "24 rows (lanes>=24 dup row 23)", 64);
-    run(k_fold<1>, "1 row broadcast", 64);
-    run(k_fold<2>, "lane%24 rows", 64);
-    run(k_fold<0>, "24 rows, 4 waves", 256);
-    run(k_fold<3>, "24 rows, EXEC=24 lanes", 64);
-    run(k_fold<4>, "8 rows, EXEC=8 lanes", 64);
-    run(k_fold<5>, "1 row, EXEC=1 lane", 64);
     run(k_raw<0>, "raw: reads+fmacs no waits", 64);
     run(k_raw<1>, "raw: fmacs only", 64);
     run(k_raw<2>, "raw: 12 reads + wait0", 64);
     run(k_raw<3>, "raw: reads, no waits", 64);
+    run(k_raw<4>, "raw: reads+fmacs, EXEC=24", 64);
+    run(k_raw<5>, "raw: reads only, EXEC=24", 64);
     return 0;
 }
