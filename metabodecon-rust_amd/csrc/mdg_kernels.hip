@@ -2226,6 +2226,10 @@ __device__ __forceinline__ void fit_tf_body(const Workspace& w, int s, int P, in
         } else {
             double acc = -0.0;
             const int q = lane < Q ? lane : Q - 1;
+            // acc = fma(t, 1, acc) rounds as acc + t; the VOP2 v_fmac_f64 chain issues
+            // a cycle faster per term than dependent v_add_f64 (eval_cost.hip)
+            double one = 1.0;
+            asm volatile("" : "+v"(one));
             DIAG_STAMP(4);
             lds_barrier();  // chunk 0 written
             DIAG_STAMP(3);
@@ -2236,12 +2240,12 @@ __device__ __forceinline__ void fit_tf_body(const Workspace& w, int s, int P, in
 #pragma unroll 16
                     for (int k = 0; k < J / 2; ++k) {
                         const double2 v = row[k];
-                        acc += v.x;
-                        acc += v.y;
+                        acc = __builtin_fma(v.x, one, acc);
+                        acc = __builtin_fma(v.y, one, acc);
                     }
                 } else {
                     const double* r1 = (const double*)row;
-                    for (int k = 0; k < cn; ++k) acc += r1[k];
+                    for (int k = 0; k < cn; ++k) acc = __builtin_fma(r1[k], one, acc);
                 }
                 DIAG_STAMP(2);
                 lds_barrier();
