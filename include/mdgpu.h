@@ -189,6 +189,13 @@ int mdg_superposition_vec_device(mdg_ctx* ctx, const double* d_x, size_t n,
  * sequential fold whatever the data. */
 int mdg_ordered_sum(mdg_ctx* ctx, const double* t, size_t n, double acc0, double* out);
 
+/* Test support: the superposition's fast quotient (one Newton step after
+ * v_rcp_f64, used when every operand lies in [2^-200, 2^200]) against the IEEE
+ * division the reference performs (lorentzian.rs:546-548), on n pseudo-random
+ * operand pairs of that range drawn from seed. *mismatches receives the number of
+ * pairs whose bits differ (expected 0). */
+int mdg_check_fast_division(mdg_ctx* ctx, uint64_t seed, uint64_t n, uint64_t* mismatches);
+
 /* Device synthetic batch: d_x (n, shared axis x_i = xmax - (i*width)/(n-1)) and
  * d_y (b x n): y_s = in-order superposition of mdg_synth_lorentzians(seed0+s) +
  * mdg_synth_noise(seed0+s). */

@@ -844,6 +844,21 @@ int mdg_ordered_sum(mdg_ctx* c, const double* t, size_t n, double acc0, double* 
     return MDG_OK;
 }
 
+int mdg_check_fast_division(mdg_ctx* c, uint64_t seed, uint64_t n, uint64_t* mismatches) {
+    if (!c || !mismatches || n > (uint64_t)INT64_MAX) return MDG_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    int rc;
+    if ((rc = ensure(c->st_flag, 256))) return rc;
+    HIPCHK(hipMemsetAsync(c->st_flag.p, 0, 8, st));
+    launch_division_check(seed, (long long)n, (unsigned long long*)c->st_flag.p, st);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(mismatches, c->st_flag.p, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return MDG_OK;
+}
+
 int mdg_synth_batch_device(mdg_ctx* c, size_t b, size_t n, double xmax, double width,
                            uint64_t seed0, size_t n_peaks, double lo, double hi, double sigma,
                            double* d_x, double* d_y) {

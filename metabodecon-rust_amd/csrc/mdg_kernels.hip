@@ -1624,18 +1624,59 @@ __device__ __forceinline__ void two_sum(double a, double b, double& s, double& e
     e = (a - (s - bb)) + (b - bb);
 }
 
+// dpp_fold for one window segment (a few hundred terms): groups of 16 terms are
+// loaded 8 groups at a time, the next 8 in flight while the current 8 are folded
+// (dpp_fold's own steady loop starts at 24 groups; below that it waits on every load)
+__device__ __noinline__ double seg_fold(double acc, const double* __restrict__ t, int n) {
+    const int sub = threadIdx.x & 15;
+    const double one = 1.0;
+    const int G = n / 16;
+    double cur[8], nxt[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) cur[u] = t[min(16 * u + sub, max(n - 1, 0))];
+    for (int g0 = 0; g0 < G; g0 += 8) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) nxt[u] = t[min(16 * (g0 + 8 + u) + sub, max(n - 1, 0))];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (g0 + u < G) fold16(acc, cur[u], one);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) cur[u] = nxt[u];
+    }
+    const int r = n - 16 * G;
+    if (r > 0) {
+        const double v = t[min(16 * G + sub, n - 1)];
+        for (int k = 0; k < r; ++k) acc += readlane_f64(v, k);
+    }
+    return acc;
+}
+
 template <int BS>
-__device__ double window_fold(double acc0, WinLds& L, const double* __restrict__ t, int n) {
+__device__ double window_fold(double acc0, WinLds& L, const double* __restrict__ t, int n,
+                              int stamp = 40) {
     constexpr int NW = BS / 64;
+    static_assert(kWinSeg <= 64, "one lane per segment in the prefix scan");
+    KSTAMP(stamp + 5);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int seg = (n + kWinSeg - 1) / kWinSeg;
-    // A. double-double sums of the segments (wave w: segments w, w+NW, ...)
+    // A. double-double sums of the segments (wave w: segments w, w+NW, ...); each
+    // lane's terms of a segment are loaded together
     for (int k = wv; k < kWinSeg; k += NW) {
         double hi = 0.0, lo = 0.0;
-        for (int i = k * seg + lane; i < min(n, (k + 1) * seg); i += 64) {
-            double e;
-            two_sum(hi, t[i], hi, e);
-            lo += e;
+        const int i0 = k * seg, i1 = min(n, (k + 1) * seg);
+        for (int c = i0; c < i1; c += 8 * 64) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int i = c + 64 * u + lane;
+                v[u] = i < i1 ? t[i] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                double e;
+                two_sum(hi, v[u], hi, e);
+                lo += e;
+            }
         }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
@@ -1647,18 +1688,24 @@ __device__ double window_fold(double acc0, WinLds& L, const double* __restrict__
         if (lane == 0) L.F[k][0] = hi, L.F[k][1] = lo;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        double hi = acc0 == 0.0 ? 0.0 : acc0, lo = 0.0;
+    KSTAMP(stamp + 6);
+    if (threadIdx.x < 64) {
+        // exclusive prefix of the segment sums, in double-double, by wave 0: the
+        // segment sums are read once into lanes and walked with readlanes
+        const double fh = lane < kWinSeg ? L.F[lane][0] : 0.0;
+        const double fl = lane < kWinSeg ? L.F[lane][1] : 0.0;
+        double hi = acc0 == 0.0 ? 0.0 : acc0, lo = 0.0, mine = 0.0;
         for (int k = 0; k < kWinSeg; ++k) {
             double e;
             two_sum(hi, lo, hi, lo);  // renormalise
-            L.E[k] = hi;
-            two_sum(hi, L.F[k][0], hi, e);
-            lo += L.F[k][1] + e;
+            if (lane == k) mine = hi;
+            two_sum(hi, readlane_f64(fh, k), hi, e);
+            lo += readlane_f64(fl, k) + e;
         }
+        if (lane < kWinSeg) L.E[lane] = mine;
     }
     __syncthreads();
-    KSTAMP(40);
+    KSTAMP(stamp);
     // B. every segment from 64 candidates (segment 0 from acc0 itself, exactly)
     for (int k = wv; k < kWinSeg; k += NW) {
         double acc;
@@ -1669,28 +1716,33 @@ __device__ double window_fold(double acc0, WinLds& L, const double* __restrict__
             acc = __longlong_as_double(b < 0 ? 0ll : b);
         }
         const int i0 = min(n, k * seg), i1 = min(n, (k + 1) * seg);
-        L.F[k][lane] = dpp_fold(acc, t + i0, i1 - i0);
+        L.F[k][lane] = seg_fold(acc, t + i0, i1 - i0);
     }
     __syncthreads();
-    KSTAMP(41);
+    KSTAMP(stamp + 1);
     // C. the true chain through the segments, by wave 0
     if (wv == 0) {
         double tru = readlane_f64(L.F[0][lane], 0);
+#pragma unroll 1
         for (int k = 1; k < kWinSeg; ++k) {
             const long long b = __double_as_longlong(L.E[k]) + (lane - 32);
             const long long cand = b < 0 ? 0ll : b;
+            const double fk = L.F[k][lane];
             const unsigned long long hit = __ballot(cand == __double_as_longlong(tru));
             if (hit) {
-                tru = readlane_f64(L.F[k][lane], __ffsll((unsigned long long)hit) - 1);
+                tru = readlane_f64(fk, __ffsll((unsigned long long)hit) - 1);
             } else {  // outside the window: this segment from the true value
                 const int i0 = min(n, k * seg), i1 = min(n, (k + 1) * seg);
-                tru = dpp_fold(tru, t + i0, i1 - i0);
+                tru = seg_fold(tru, t + i0, i1 - i0);
+#ifdef MDG_DIAG
+                if (lane == 0 && blockIdx.x == 0 && g_diag) g_diag[(1 << 16) + stamp + 7] += 1;
+#endif
             }
         }
         if (lane == 0) L.out = tru;
     }
     __syncthreads();
-    KSTAMP(42);
+    KSTAMP(stamp + 2);
     return L.out;
 }
 
@@ -1703,6 +1755,37 @@ __global__ __launch_bounds__(1024) void k_ordered_sum(const double* __restrict__
 }
 void launch_ordered_sum(const double* t, int n, double acc0, double* out, hipStream_t st) {
     hipLaunchKernelGGL(k_ordered_sum, dim3(1), dim3(1024), 0, st, t, n, acc0, out);
+}
+
+// test support (mdg_check_fast_division): div_rn_fast against the compiler's IEEE
+// division on n pseudo-random operand pairs of the FAST range [2^-200, 2^200]
+// (random mantissas, and mantissas made of long runs of ones or zeros)
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+    z += 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ double fast_range_operand(unsigned long long h, bool runs) {
+    unsigned long long m = h & 0xfffffffffffffull;
+    if (runs) m = (h & 1) ? (0xfffffffffffffull >> (h >> 58)) : (1ull << ((h >> 52) & 51));
+    const int e = (int)((h >> 12) % 401) - 200;
+    return __longlong_as_double((long long)(((unsigned long long)(e + 1023) << 52) | m));
+}
+__global__ void k_division_check(unsigned long long seed, long long n, unsigned long long* bad) {
+    unsigned long long nb = 0;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x) {
+        const unsigned long long h1 = mix64(seed ^ (2 * i)), h2 = mix64(seed ^ (2 * i + 1));
+        const bool runs = (h1 >> 63) & (h2 >> 63);
+        const double num = fast_range_operand(h1, runs), d = fast_range_operand(h2, runs);
+        nb += __double_as_longlong(div_rn_fast(num, d)) != __double_as_longlong(num / d);
+    }
+    if (nb) atomicAdd(bad, nb);
+}
+void launch_division_check(unsigned long long seed, long long n, unsigned long long* bad,
+                           hipStream_t st) {
+    hipLaunchKernelGGL(k_division_check, dim3(4096), dim3(256), 0, st, seed, n, bad);
 }
 
 template <int BS>
@@ -1774,7 +1857,7 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
     }
     __syncthreads();
     double var = 0.0;
-    if (win) var = window_fold<BS>(-0.0, wl, sfr, n_sfr) / (double)n_sfr;
+    if (win) var = window_fold<BS>(-0.0, wl, sfr, n_sfr, 50) / (double)n_sfr;
     else if (threadIdx.x < 64) var = dpp_fold(-0.0, sfr, n_sfr) / (double)n_sfr;
     KSTAMP(17);
     if (threadIdx.x == 0) {

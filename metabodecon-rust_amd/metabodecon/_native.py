@@ -44,7 +44,7 @@ EXPORTS = [
     "mdg_deconvolute", "mdg_deconvolute_batch", "mdg_deconvolute_batch_device",
     "mdg_superposition_vec", "mdg_superposition_vec_device", "mdg_synth_batch_device",
     "mdg_ctx_last_peaks", "mdg_ctx_last_smoothed", "mdg_ctx_set_profiling_mask",
-    "mdg_optimize_settings", "mdg_ordered_sum",
+    "mdg_optimize_settings", "mdg_ordered_sum", "mdg_check_fast_division",
 ]
 
 
@@ -148,6 +148,7 @@ def _declare(L):
     L.mdg_optimize_settings.argtypes = [_vp, _dp, _dp, _sz, ctypes.c_double, ctypes.c_double, _dp,
                                         _sz, sp, _dp]
     L.mdg_ordered_sum.argtypes = [_vp, _dp, _sz, ctypes.c_double, _dp]
+    L.mdg_check_fast_division.argtypes = [_vp, ctypes.c_uint64, ctypes.c_uint64, _u64p]
     L.mdg_synth_batch_device.argtypes = [_vp, _sz, _sz, ctypes.c_double, ctypes.c_double,
                                          ctypes.c_uint64, _sz, ctypes.c_double, ctypes.c_double,
                                          ctypes.c_double, _vp, _vp]

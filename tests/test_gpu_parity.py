@@ -411,6 +411,21 @@ def test_ordered_sum_window_fold(ctx):
     bad = np.array([1.0, -1.0])
     assert nat.lib().mdg_ordered_sum(ctx.handle, nat.ptr(bad), 2, -0.0, ctypes.byref(out)) != 0
 
+
+@pytest.mark.parametrize("seed", [0x9E3779B97F4A7C15, 20261016])
+def test_fast_division_matches_ieee(ctx, seed):
+    """div_rn_fast (reciprocal + one Newton step + one residual correction) is the
+    divider of every FAST-path Lorentzian evaluation. It must round exactly like
+    IEEE '/' on operands in [2^-200, 2^200] (the range the fast flags gate): 2^33
+    seeded pairs per seed, three quarters with uniform mantissas, a quarter with
+    trailing-ones / single-bit mantissas (the usual worst cases for Newton
+    quotients); exponents uniform in [-200, 200]."""
+    bad = ctypes.c_uint64(1)
+    rc = nat.lib().mdg_check_fast_division(ctx.handle, seed, 1 << 33, ctypes.byref(bad))
+    assert rc == 0, nat.strerror(rc)
+    assert bad.value == 0
+
+
 def test_device_graph_replay(ctx, monkeypatch):
     """mdg_deconvolute_batch_device replays a cached hipGraph for repeated argument
     sets: refilling the same device buffers with other spectra must still give the

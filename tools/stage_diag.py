@@ -40,10 +40,11 @@ for _ in range(3):
     torch.cuda.synchronize()
 d = diag.cpu().tolist()[1 << 16:]
 groups = {"select": range(10, 19), "peaks": range(0, 5), "fit_dpp": range(20, 24),
-          "mse": range(30, 34), "window": [15, 40, 41, 42, 16]}
+          "mse": range(30, 34), "window_mean": [45, 46, 40, 41, 42], "window_var": [55, 56, 50, 51, 52]}
 for name, r in groups.items():
     v = [d[k] for k in r]
     if not any(v):
         continue
     t0 = v[0]
     print(f"{name:10s}", " ".join(f"s{k}:{(d[k] - t0) if d[k] else '-'}" for k in r))
+print("window fallbacks mean/var (3 runs):", d[47], d[57])
