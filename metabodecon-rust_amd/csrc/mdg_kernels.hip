@@ -701,11 +701,11 @@ __global__ __launch_bounds__(512) void k_smooth_waves(BatchArgs a, Workspace w, 
 // on its own CU, in three waves:
 //  * chain wave: issues little besides the reference's two dependent adds per
 //    tick (moving_average.rs:69-80, in j = i + R form below) on SGPR operands,
-//    and stores one checkpoint per 8 ticks (the group's last raw sum);
+//    and stores one checkpoint per kChainG = 32 ticks (the group's last raw sum);
 //  * feeder wave: waits for the previous pass's published blocks (sc1 polls),
 //    pulls them into L2 and touches them into the scalar cache, and publishes
 //    in_ready in LDS;
-//  * scaler wave: replays each group of 8 ticks from its checkpoint with the same
+//  * scaler wave: replays each group of 32 ticks from its checkpoint with the same
 //    two operations (bit-identical sums), multiplies by the reference's 1/len
 //    (moving_average.rs:66-81: 1/len while the buffer grows, 1/ws, then 1/len
 //    in the tail) and publishes finished blocks to the next pass (sc1 stores,
@@ -720,6 +720,8 @@ __global__ __launch_bounds__(512) void k_smooth_waves(BatchArgs a, Workspace w, 
 // all its waves drain (never expected; it bounds a protocol bug).
 // ----------------------------------------------------------------------------------
 constexpr int kChainCB = MDG_CHAIN_CB;
+constexpr int kChainG = MDG_CHAIN_G;      // ticks per stored checkpoint in steady blocks
+static_assert(kChainG % 8 == 0 && kChainCB % kChainG == 0, "checkpoint groups tile the blocks");
 constexpr int kChainPrefetch = 6;        // input blocks touched into the scalar cache ahead
 constexpr int kChainL2Ahead = 64;        // pass-0 input blocks pulled into L2 ahead
 constexpr unsigned kChainSpins = 1u << 22;
@@ -868,8 +870,8 @@ __global__ __launch_bounds__(192) void k_smooth_chain(BatchArgs a, Workspace w, 
 
     __shared__ ChainCtl ctl;
     // scaler staging (one wave): inputs and raw sums of one batch of output blocks
-    __shared__ double sc_in[8 * kChainCB + 24];
-    __shared__ double sc_raw[8 * kChainCB + 24];
+    __shared__ double sc_in[8 * kChainCB + kChainG + 8];
+    __shared__ double sc_raw[8 * kChainCB + kChainG + 8];
     const int lane = threadIdx.x & 63;
     if (threadIdx.x == 0) {
         ctl.in_ready = 0;
@@ -908,7 +910,7 @@ __global__ __launch_bounds__(192) void k_smooth_chain(BatchArgs a, Workspace w, 
         // (fold8_ticks), operands zero-padded: the running sum starts at +0.0 and can
         // never become -0.0 (x + y is -0 only for -0 + -0, x - y only for -0 - +0),
         // so adding or subtracting +0.0 is exactly the reference's skipped term.
-        // Only the per-8-tick checkpoints are stored, as in the steady loop.
+        // Checkpoints every 8 ticks are stored (a superset of the steady loop's).
         const double one = 1.0;
         auto generic = [&](int k) -> bool {
             if (!wait_in(min(k + 2, nIB))) return false;
@@ -1029,15 +1031,16 @@ __global__ __launch_bounds__(192) void k_smooth_chain(BatchArgs a, Workspace w, 
             if (ready > sc) {
                 const int hi = min(ready, sc + MAXB);
                 const int i0 = sc * CB, i1 = min(hi * CB, N);
-                // raw sums j = i + R of the batch, staged in LDS: groups of 8 ticks in
+                // raw sums j = i + R of the batch, staged in LDS: groups of G ticks in
                 // steady j-blocks [kA, kB) hold only their last sum (the checkpoint), so
                 // one lane per group replays it from the previous checkpoint with the
                 // chain's own two operations per tick; all HBM traffic is coalesced
-                const int g0 = (i0 + R) / 8, g1 = (i1 - 1 + R) / 8 + 1;
-                const int base = 8 * g0 - 8;               // LDS index = j - base
-                const int span = 8 * (g1 - g0) + 8;
+                constexpr int G = kChainG;
+                const int g0 = (i0 + R) / G, g1 = (i1 - 1 + R) / G + 1;
+                const int base = G * g0 - 8;               // LDS index = j - base
+                const int span = G * (g1 - g0) + 8;
                 {
-                    constexpr int SLOTS = (8 * kChainCB + 24 + 63) / 64;
+                    constexpr int SLOTS = (8 * kChainCB + G + 8 + 63) / 64;
                     double vin[SLOTS], vraw[SLOTS];
 #pragma unroll
                     for (int k = 0; k < SLOTS; ++k) {  // all loads in flight together
@@ -1057,17 +1060,17 @@ __global__ __launch_bounds__(192) void k_smooth_chain(BatchArgs a, Workspace w, 
                 for (int g = g0 + lane; g < g1; g += 64) {
                     // every group holds only its checkpoint; replay from the previous one
                     // (group 0 from T::zero()) with the zero-padded operands of the chain
-                    const int e0 = 8 * g - base;
+                    const int e0 = G * g - base;
                     double sum_g = g == 0 ? 0.0 : sc_raw[e0 - 1];
-                    double rv[8];
+                    double rv[G];
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) {
+                    for (int u = 0; u < G; ++u) {
                         sum_g += sc_in[e0 + u];
                         sum_g -= sc_in[e0 + u - WS];
                         rv[u] = sum_g;
                     }
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) sc_raw[e0 + u] = rv[u];
+                    for (int u = 0; u < G; ++u) sc_raw[e0 + u] = rv[u];
                 }
                 for (int i = i0 + lane; i < i1; i += 64) {
                     // len of the circular buffer after tick i (moving_average.rs:66-81)

@@ -8,15 +8,13 @@ SGPR operands, BPT blocks of CB = 96 ticks per loop trip:
   * operands: groups of 8 doubles of the pass input, s_load_dwordx16 into three
     rotating SGPR buffers (prev / cur / next); each group prefetches the next
     and waits for it at its end (lgkmcnt(0): SMEM returns out of order);
-  * sums: group q accumulates in pair ACC[q % 2] (v[0:1] / v[2:3]). Its first add
-    is a VOP3 v_add_f64 from the other pair; the other 15 operations are VOP2
-    v_fmac_f64 with the SGPR operand times +1.0 / -1.0 (v[4:5] / v[6:7]) --
-    fma(a, +-1, s) rounds exactly as s +- a, and the dependent VOP2 fmac chain
-    issues in 8.3 cycles per tick against 10.3 for VOP3 adds (tools/ubench/
-    eval_cost.hip). Only the last sum of each group of 8 ticks is stored (see
-    block_body), read from the previous group's pair while the next group runs;
+  * sums: one VGPR pair ACC; every operation is a VOP2 v_fmac_f64 with the SGPR
+    operand times +1.0 / -1.0 (v[4:5] / v[6:7]) -- fma(a, +-1, s) rounds exactly
+    as s +- a, and the dependent VOP2 fmac chain issues in 8.3 cycles per tick
+    against 10.3 for VOP3 adds (tools/ubench/eval_cost.hip). Only the last sum
+    of each G = 32 ticks is stored (see block_body);
   * per block: wait (LDS, cached) until the helper wave has published the input
-    block the prefetch reaches; after the trip, s_waitcnt vmcnt(GROUPS) proves
+    block the prefetch reaches; after the trip, s_waitcnt vmcnt(TT/G) proves
     the previous trip's stores complete, then raw_done is published in LDS.
 
 Fixed registers: s[40:87] operand buffers, s[88:99] loop state, v[0:18].
@@ -28,6 +26,8 @@ CB = int(os.environ.get("CHAIN_CB", "96"))  # ticks per block (the feeder / scal
 BPT = 1              # blocks per loop trip (2 measured: 20 cycles/tick against 13 -- keep 1)
 TT = CB * BPT        # ticks per trip
 GROUPS = TT // 8     # multiple of 3: buffer rotation period
+G = int(os.environ.get("CHAIN_G", "32"))  # ticks per stored checkpoint (scaler replay group)
+assert G % 8 == 0 and TT % G == 0 and TT // G <= 63
 BUF = [40, 56, 72]   # SGPR base of the three 8-double buffers
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "metabodecon-rust_amd", "csrc", "mdg_chain_asm.inc")
@@ -36,7 +36,7 @@ OUT = os.path.join(ROOT, "metabodecon-rust_amd", "csrc", "mdg_chain_asm.inc")
 IN, RAW = "s[88:89]", "s[90:91]"
 IN_LO, IN_HI, RAW_LO, RAW_HI = "s88", "s89", "s90", "s91"
 BLK, AVAIL, NIB, GUARD, CNT, TMP, NEED, STAT = "s92", "s93", "s94", "s95", "s96", "s97", "s98", "s99"
-ACC = ["v[0:1]", "v[2:3]"]   # running sum of even / odd groups
+ACC = "v[0:1]"               # running sum
 ONE, MONE = "v[4:5]", "v[6:7]"
 LDSA, VT, VZ = "v16", "v17", "v18"
 GUARD_SPINS = 1 << 22  # ~0.3 s of s_sleep 1 before the wave gives up (never expected)
@@ -48,11 +48,13 @@ def sreg(buf, e):
 
 
 def block_body(ws):
-    """GROUPS groups of 8 ticks (BPT blocks); after each group only its LAST running sum (the
-    checkpoint raw[8G+7]) is stored, one 8-byte store placed after the first add
-    of the next group's second tick. The scaler wave recomputes the other seven
-    sums of the group from the previous checkpoint with the same two operations
-    per tick, so the stored data is 1/8 of the ticks.
+    """GROUPS groups of 8 ticks (BPT blocks), all in one accumulator pair ACC; after
+    every G ticks only the last running sum (the checkpoint raw[G*k + G-1]) is
+    stored, straight from ACC (an 8-byte store reads its data before a later VALU
+    write can land: no hazard). The scaler wave recomputes the other G-1 sums from
+    the previous checkpoint with the same two operations per tick, so the stored
+    data is 1/G of the ticks and the chain wave spends one issue slot per G ticks
+    on it.
 
     (Loading two groups ahead in pairs, with four buffers, was measured: no
     change at 12.9 cycles/tick -- the cost of the SMEM feed is its issue and
@@ -63,20 +65,13 @@ def block_body(ws):
         # IN points one group (64 B) before the block: group q+1 starts at 64*(q+2)
         if not os.environ.get("CHAIN_NOLOAD"):  # diagnostic variants only (wrong results)
             L.append(f"s_load_dwordx16 s[{BUF[nxt]}:{BUF[nxt] + 15}], {IN}, {64 * (q + 2)}")
-        acc, other = ACC[q % 2], ACC[(q - 1) % 2]
         for u in range(8):
-            if u == 0:
-                L.append(f"v_add_f64 {acc}, {other}, {sreg(cur, u)}")
-            else:
-                L.append(f"v_fmac_f64 {acc}, {sreg(cur, u)}, {ONE}")
-            if u == 1 and q >= 1 and not os.environ.get("CHAIN_NOSTORE"):
-                c = 8 * q - 1  # checkpoint of the previous group, still in its pair
-                L.append(f"global_store_dwordx2 {VZ}, {other}, {RAW} offset:{8 * c}")
+            L.append(f"v_fmac_f64 {ACC}, {sreg(cur, u)}, {ONE}")
             pop = sreg(cur, u - ws) if u >= ws else sreg(prev, 8 + u - ws)
-            L.append(f"v_fmac_f64 {acc}, {pop}, {MONE}")
+            L.append(f"v_fmac_f64 {ACC}, {pop}, {MONE}")
         L.append("s_waitcnt lgkmcnt(0)")
-    if not os.environ.get("CHAIN_NOSTORE"):
-        L.append(f"global_store_dwordx2 {VZ}, {ACC[(GROUPS - 1) % 2]}, {RAW} offset:{8 * (TT - 1)}")
+        if (8 * q + 8) % G == 0 and not os.environ.get("CHAIN_NOSTORE"):
+            L.append(f"global_store_dwordx2 {VZ}, {ACC}, {RAW} offset:{8 * (8 * q + 7)}")
     return L
 
 
@@ -93,7 +88,7 @@ def program(ws):
         "s_mov_b32 s99, 0",
         f"v_mov_b32 {LDSA}, %[lds]",
         f"v_mov_b32 {VZ}, 0",
-        f"v_mov_b64 {ACC[1]}, %[sum]",
+        f"v_mov_b64 {ACC}, %[sum]",
         f"v_mov_b64 {ONE}, 1.0",
         f"v_mov_b64 {MONE}, -1.0",
         f"s_load_dwordx16 s[{BUF[0]}:{BUF[0] + 15}], {IN}, 0",
@@ -132,7 +127,7 @@ def program(ws):
         f"s_addc_u32 {IN_HI}, {IN_HI}, 0",
         f"s_add_u32 {RAW_LO}, {RAW_LO}, {8 * TT}",
         f"s_addc_u32 {RAW_HI}, {RAW_HI}, 0",
-        f"s_waitcnt vmcnt({GROUPS})",
+        f"s_waitcnt vmcnt({TT // G})",
         f"v_mov_b32 {VT}, {BLK}",
         f"ds_write_b32 {LDSA}, {VT} offset:4",   # raw_done = blocks < blk complete
         f"s_add_u32 {BLK}, {BLK}, {BPT}",
@@ -141,7 +136,7 @@ def program(ws):
         "s_cbranch_scc1 Lblk%=",
         "Ldone%=:",
         "s_waitcnt vmcnt(0)",
-        f"v_mov_b64 %[sum], {ACC[(GROUPS - 1) % 2]}",
+        f"v_mov_b64 %[sum], {ACC}",
         "s_mov_b32 %[blk_out], s92",
         "s_mov_b32 %[stat], s99",
     ]
@@ -151,7 +146,7 @@ def program(ws):
 def main():
     lines = ["// Generated by tools/gen_chain_asm.py -- do not edit.",
              f"// Steady loop of the k_smooth_chain chain wave, CB = {CB} ticks per block.",
-             f"#define MDG_CHAIN_CB {CB}", f"#define MDG_CHAIN_BPT {BPT}", ""]
+             f"#define MDG_CHAIN_CB {CB}", f"#define MDG_CHAIN_BPT {BPT}", f"#define MDG_CHAIN_G {G}", ""]
     for ws in range(2, 9):
         body = program(ws)
         lines.append(f"#define MDG_CHAIN_ASM_{ws} \\")
