@@ -144,7 +144,7 @@ __device__ __forceinline__ double superpose(double x, const double* __restrict__
 #ifdef MDG_DIAG
 __device__ long long* g_diag = nullptr;
 __device__ int g_tf_mode = 0;
-__device__ int g_chain_mode = 0;  // chain_diag: 1 = feeder publishes everything at once, no scaler; 2 = no scaler; 3 = instant feeder  // fit_diag: 1 = evaluators skip LDS stores, 2 = skip evaluation
+__device__ int g_chain_mode = 0;  // chain_diag: 1 = feeder publishes everything at once, no scaler; 2 = no scaler; 3 = instant feeder; 4 = passes one after another  // fit_diag: 1 = evaluators skip LDS stores, 2 = skip evaluation
 #define KSTAMP(slot)                                                           \
     if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0 && g_diag)      \
         g_diag[(1 << 16) + (slot)] = (long long)__builtin_amdgcn_s_memtime()
@@ -720,9 +720,14 @@ __global__ __launch_bounds__(512) void k_smooth_waves(BatchArgs a, Workspace w, 
 // all its waves drain (never expected; it bounds a protocol bug).
 // ----------------------------------------------------------------------------------
 constexpr int kChainCB = MDG_CHAIN_CB;
+#ifndef MDG_CHAIN_PF
+#define MDG_CHAIN_PF 8
+#endif
+constexpr int kChainScalers = 2;         // scaler waves (round-robin batches)
+constexpr int kChainScBatch = 8;         // output blocks per scaler batch
 constexpr int kChainG = MDG_CHAIN_G;      // ticks per stored checkpoint in steady blocks
 static_assert(kChainG % 8 == 0 && kChainCB % kChainG == 0, "checkpoint groups tile the blocks");
-constexpr int kChainPrefetch = 6;        // input blocks touched into the scalar cache ahead
+constexpr int kChainPrefetch = MDG_CHAIN_PF;  // input blocks touched into the scalar cache ahead
 constexpr int kChainL2Ahead = 64;        // pass-0 input blocks pulled into L2 ahead
 constexpr unsigned kChainSpins = 1u << 22;
 
@@ -755,7 +760,7 @@ struct ChainCtl {
     int in_ready;  // input blocks available in the scalar cache (helper -> chain)
     int raw_done;  // j-blocks whose raw sums are stored (chain -> helper)
     int abort;
-    int pad;
+    int pub;       // scaler batches published (scaler -> scaler)
 };
 
 // wave-uniform copies for "s" asm operands (values computed under a branch the
@@ -813,16 +818,29 @@ MDG_CHAIN_STEADY(6)
 MDG_CHAIN_STEADY(7)
 MDG_CHAIN_STEADY(8)
 
-// touch the 64-byte lines of one input block (scalar cache prefetch for the chain)
-__device__ __forceinline__ void chain_touch(const double* p) {
-    static_assert(kChainCB % 8 == 0, "whole 64-byte lines per block");
-    const auto q = sgpr_ptr(p);
-#pragma unroll
-    for (int k = 0; k < kChainCB / 8; ++k)
-        asm volatile("s_load_dwordx16 s[40:55], %0, %1" ::"s"(q), "i"(64 * k)
-                     : "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50",
-                       "s51", "s52", "s53", "s54", "s55", "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+// touch the 64-byte lines of cnt consecutive input blocks (scalar cache prefetch
+// for the chain). All loads are in flight together and land in the same scratch
+// SGPRs (their values are never used); one wait at the end, so no load is still
+// outstanding when the compiler reuses those registers.
+__device__ __forceinline__ void chain_touch(const double* p, int cnt) {
+    static_assert(kChainCB == 96, "the touch loop below covers 12 lines per block");
+#define MDG_TOUCH_LINE(k) "s_load_dwordx16 s[40:55], s[56:57], " #k "\n"
+    asm volatile(
+        "s_mov_b64 s[56:57], %0\n"
+        "s_mov_b32 s58, %1\n"
+        "Ltouch%=:\n" MDG_TOUCH_LINE(0) MDG_TOUCH_LINE(64) MDG_TOUCH_LINE(128) MDG_TOUCH_LINE(192)
+            MDG_TOUCH_LINE(256) MDG_TOUCH_LINE(320) MDG_TOUCH_LINE(384) MDG_TOUCH_LINE(448)
+                MDG_TOUCH_LINE(512) MDG_TOUCH_LINE(576) MDG_TOUCH_LINE(640) MDG_TOUCH_LINE(704)
+        "s_add_u32 s56, s56, 768\n"
+        "s_addc_u32 s57, s57, 0\n"
+        "s_sub_u32 s58, s58, 1\n"
+        "s_cmp_lg_u32 s58, 0\n"
+        "s_cbranch_scc1 Ltouch%=\n"
+        "s_waitcnt lgkmcnt(0)\n" ::"s"(sgpr_ptr(p)),
+        "s"(sgpr_int(cnt))
+        : "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52",
+          "s53", "s54", "s55", "s56", "s57", "s58", "scc", "memory");
+#undef MDG_TOUCH_LINE
 }
 
 
@@ -845,7 +863,7 @@ __device__ __forceinline__ void chain_l2_pull(const double* p, int cnt) {
 }
 
 template <int WS>
-__global__ __launch_bounds__(192) void k_smooth_chain(BatchArgs a, Workspace w, int P) {
+__global__ __launch_bounds__(64 * (2 + kChainScalers)) void k_smooth_chain(BatchArgs a, Workspace w, int P) {
     // workgroup id -> (spectrum, pass): the P passes of a spectrum share id % 8
     // (the XCD of round-robin dispatch), so their hand-offs stay in one L2
     const int id = blockIdx.x;
@@ -870,13 +888,17 @@ __global__ __launch_bounds__(192) void k_smooth_chain(BatchArgs a, Workspace w, 
 
     __shared__ ChainCtl ctl;
     // scaler staging (one wave): inputs and raw sums of one batch of output blocks
-    __shared__ double sc_in[8 * kChainCB + kChainG + 8];
-    __shared__ double sc_raw[8 * kChainCB + kChainG + 8];
+    // (one pad double per 32: the replay lanes, G doubles apart, hit distinct banks)
+    constexpr int kScSpan = kChainScBatch * kChainCB + kChainG + 8;
+    __shared__ double sc_in_all[kChainScalers][kScSpan + kScSpan / 32 + 1];
+    __shared__ double sc_raw_all[kChainScalers][kScSpan + kScSpan / 32 + 1];
+#define SCI(e) ((e) + ((e) >> 5))
     const int lane = threadIdx.x & 63;
     if (threadIdx.x == 0) {
         ctl.in_ready = 0;
         ctl.raw_done = 0;
         ctl.abort = 0;
+        ctl.pub = 0;
     }
     __syncthreads();
     asm volatile("s_dcache_inv" ::: "memory");
@@ -933,6 +955,7 @@ __global__ __launch_bounds__(192) void k_smooth_chain(BatchArgs a, Workspace w, 
         };
         bool ok = true;
         DIAGC(0, __builtin_amdgcn_s_memtime());
+        DIAGC(5, __builtin_amdgcn_s_getreg((4) | (0 << 6) | ((32 - 1) << 11)));  // HW_ID: wave / SIMD / CU / SE
         for (int k = 0; ok && k < kA; ++k) ok = generic(k);
         DIAGC(1, __builtin_amdgcn_s_memtime());
         if (ok && kB > kA) {
@@ -940,7 +963,8 @@ __global__ __launch_bounds__(192) void k_smooth_chain(BatchArgs a, Workspace w, 
             const int done = chain_steady<WS>(in + (size_t)kA * CB - 8, raw + (size_t)kA * CB, kA,
                                               (kB - kA) / MDG_CHAIN_BPT, nIB,
                                               lds_offset(&ctl), sum, stat);
-            ok = stat == 0 && done == kB;
+            ok = (stat & 1) == 0 && done == kB;  // stat >> 1: in_ready waits (diagnostic)
+            DIAGC(6, stat >> 1);
             if (ok) CTL_ST(raw_done, kB);
         }
         DIAGC(2, __builtin_amdgcn_s_memtime());
@@ -952,17 +976,25 @@ __global__ __launch_bounds__(192) void k_smooth_chain(BatchArgs a, Workspace w, 
         // ---------------------------- feeder wave ----------------------------
         // polls the upstream pass, touches newly available input blocks into the
         // scalar cache (kChainPrefetch blocks ahead of the chain) and publishes them
-        int pf = 0;
+        int pf = 0;     // next input block to touch
+        int ready = 0;  // in_ready published
         int up = p == 0 ? nIB : 0;
         int l2 = 0;  // next input block pulled into L2
         unsigned idle = 0;
         bool ok = true;
         DIAGC(8, __builtin_amdgcn_s_memtime());
+        DIAGC(12, __builtin_amdgcn_s_getreg((4) | (0 << 6) | ((32 - 1) << 11)));  // HW_ID: wave / SIMD / CU / SE
 #ifdef MDG_DIAG
         if (g_chain_mode == 1 || g_chain_mode == 3) {
             CTL_ST(in_ready, nIB);
             pf = nIB;
         }
+#endif
+#ifdef MDG_DIAG
+        if (g_chain_mode == 4 && p > 0)  // upstream pass finished before this one starts
+            while (__hip_atomic_load(const_cast<int32_t*>(up_flag), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT) < nOB)
+                __builtin_amdgcn_s_sleep(8);
 #endif
         while (pf < nIB) {
             if (CTL_LD(abort)) {
@@ -984,10 +1016,18 @@ __global__ __launch_bounds__(192) void k_smooth_chain(BatchArgs a, Workspace w, 
                 l2 += cnt;
                 prog = true;
             }
+            // the chain may read every published block (in_ready gates correctness
+            // only); the touches run kChainPrefetch blocks ahead of it, in one batch
+            if (min(up, nIB) > ready) {
+                ready = min(up, nIB);
+                CTL_ST(in_ready, ready);
+                prog = true;
+            }
             const int hi = min(min(up, nIB), rd + kChainPrefetch);
-            for (; pf < hi; ++pf) {
-                if ((pf + 1) * CB <= N) chain_touch(in + (size_t)pf * CB);
-                CTL_ST(in_ready, pf + 1);
+            if (hi > pf) {
+                const int full = min(hi, N / CB) - pf;  // whole blocks only (no read past N)
+                if (full > 0) chain_touch(in + (size_t)pf * CB, full);
+                pf = hi;
                 prog = true;
             }
             if (prog) {
@@ -1005,105 +1045,166 @@ __global__ __launch_bounds__(192) void k_smooth_chain(BatchArgs a, Workspace w, 
         DIAGC(9, __builtin_amdgcn_s_memtime());
         if (!ok) CTL_ST(abort, 1);
     } else {
-        // ---------------------------- scaler wave ----------------------------
+        // ---------------------------- scaler waves ---------------------------
+        // batch b = output blocks [b*MB, b*MB + MB) goes to scaler wave b % kChainScalers;
+        // each scales its batch, stores it (sc1), waits vmcnt(0) and then, in batch
+        // order (ctl.pub), raises the pass's block counter (atomic max, so the order
+        // the counter updates land in does not matter)
+        const int sw = (threadIdx.x >> 6) - 2;
+        double* sc_in = sc_in_all[sw];
+        double* sc_raw = sc_raw_all[sw];
         // the reference's div = 1/len (moving_average.rs:66-81), one division per len
         double inv_len[WS + 1];
 #pragma unroll
         for (int k = 0; k <= WS; ++k) inv_len[k] = 1.0 / (double)(k > 0 ? k : 1);
-        // scales every finished raw block by 1/len and publishes them in one batch
-        // (sc1 stores, vmcnt(0), sc1 counter: the downstream pass polls it)
-        constexpr int MAXB = 8;                   // blocks per batch
-        int sc = 0;
+        double one = 1.0, mone = -1.0;  // opaque: keep the replay as VOP2 fmacs
+        asm volatile("" : "+v"(one), "+v"(mone));
+        constexpr int MB = kChainScBatch;
+        const int nBatch = (nOB + MB - 1) / MB;
         unsigned idle = 0;
         bool ok = true;
-        DIAGC(16, __builtin_amdgcn_s_memtime());
+        if (sw == 0) {
+            DIAGC(16, __builtin_amdgcn_s_memtime());
+            DIAGC(20, __builtin_amdgcn_s_getreg((4) | (0 << 6) | ((32 - 1) << 11)));  // HW_ID
+        }
+        int b = sw;
 #ifdef MDG_DIAG
-        if (g_chain_mode == 1 || g_chain_mode == 2) sc = nOB;
+        if (g_chain_mode == 1 || g_chain_mode == 2) b = nBatch;
 #endif
-        while (sc < nOB) {
+        while (b < nBatch) {
             if (CTL_LD(abort)) {
                 ok = false;
                 break;
             }
+            const int sc = b * MB, hi = min(nOB, sc + MB);
             const int rd = CTL_LD(raw_done);
             // output block m needs raw j-blocks <= m+1: finished once raw_done >= m+2
             const int ready = rd >= nJB ? nOB : min(nOB, max(0, rd - 1));
-            if (ready > sc) {
-                const int hi = min(ready, sc + MAXB);
-                const int i0 = sc * CB, i1 = min(hi * CB, N);
-                // raw sums j = i + R of the batch, staged in LDS: groups of G ticks in
-                // steady j-blocks [kA, kB) hold only their last sum (the checkpoint), so
-                // one lane per group replays it from the previous checkpoint with the
-                // chain's own two operations per tick; all HBM traffic is coalesced
-                constexpr int G = kChainG;
-                const int g0 = (i0 + R) / G, g1 = (i1 - 1 + R) / G + 1;
-                const int base = G * g0 - 8;               // LDS index = j - base
-                const int span = G * (g1 - g0) + 8;
-                {
-                    constexpr int SLOTS = (8 * kChainCB + G + 8 + 63) / 64;
-                    double vin[SLOTS], vraw[SLOTS];
-#pragma unroll
-                    for (int k = 0; k < SLOTS; ++k) {  // all loads in flight together
-                        const int e = 64 * k + lane, j = base + e;
-                        vin[k] = (e < span && j >= 0 && j < N) ? ld_sc1(in + j) : 0.0;
-                        vraw[k] = (e < span && j >= 0 && j < nJ) ? ld_sc1(raw + j) : 0.0;
-                    }
-#pragma unroll
-                    for (int k = 0; k < SLOTS; ++k) {
-                        const int e = 64 * k + lane;
-                        if (e < span) {
-                            sc_in[e] = vin[k];
-                            sc_raw[e] = vraw[k];
-                        }
-                    }
+            if (ready < hi) {
+                if (sw == 0) DIAGC_ADD(19, 1);
+                __builtin_amdgcn_s_sleep(1);
+                if (++idle > kChainSpins) {
+                    ok = false;
+                    break;
                 }
-                for (int g = g0 + lane; g < g1; g += 64) {
-                    // every group holds only its checkpoint; replay from the previous one
-                    // (group 0 from T::zero()) with the zero-padded operands of the chain
-                    const int e0 = G * g - base;
-                    double sum_g = g == 0 ? 0.0 : sc_raw[e0 - 1];
-                    double rv[G];
-#pragma unroll
-                    for (int u = 0; u < G; ++u) {
-                        sum_g += sc_in[e0 + u];
-                        sum_g -= sc_in[e0 + u - WS];
-                        rv[u] = sum_g;
-                    }
-#pragma unroll
-                    for (int u = 0; u < G; ++u) sc_raw[e0 + u] = rv[u];
-                }
-                for (int i = i0 + lane; i < i1; i += 64) {
-                    // len of the circular buffer after tick i (moving_average.rs:66-81)
-                    const int len = i < N - R ? min(i + R + 1, WS) : WS - 1 - (i - (N - R));
-                    __hip_atomic_store(out + i, sc_raw[i + R - base] * inv_len[len],
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (lane == 0) __hip_atomic_store(my_flag, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                DIAGC_ADD(18, 1);
-                sc = hi;
-                idle = 0;
                 continue;
             }
-            DIAGC_ADD(19, 1);
-            __builtin_amdgcn_s_sleep(1);
-            if (++idle > kChainSpins) {
-                ok = false;
-                break;
+#ifdef MDG_DIAG
+            const long long tr0 = __builtin_amdgcn_s_memtime();
+            long long trp = tr0;
+#define DIAG_PH(k)                                            \
+    if (sw == 0) {                                            \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");    \
+        const long long tn = __builtin_amdgcn_s_memtime();    \
+        DIAGC_ADD(k, tn - trp);                               \
+        trp = tn;                                             \
+    }
+#else
+#define DIAG_PH(k)
+#endif
+            const int i0 = sc * CB, i1 = min(hi * CB, N);
+            // raw sums j = i + R of the batch, staged in LDS: groups of G ticks in
+            // steady j-blocks [kA, kB) hold only their last sum (the checkpoint), so
+            // one lane per group replays it from the previous checkpoint with the
+            // chain's own two operations per tick; all HBM traffic is coalesced
+            constexpr int G = kChainG;
+            const int g0 = (i0 + R) / G, g1 = (i1 - 1 + R) / G + 1;
+            const int base = G * g0 - 8;               // LDS index = j - base
+            const int span = G * (g1 - g0) + 8;
+            static_assert((MB * kChainCB) / G + 1 <= 64, "one replay group per lane");
+            // lane g - g0: the checkpoint its group starts from (group 0: T::zero())
+            const int gl = g0 + lane;
+            const bool has_g = gl < g1;
+            const double ck = has_g && gl > 0 ? ld_sc1(raw + (G * gl - 1)) : 0.0;
+            {
+                constexpr int SLOTS = (MB * kChainCB + G + 8 + 63) / 64;
+                double vin[SLOTS];
+#pragma unroll
+                for (int k = 0; k < SLOTS; ++k) {  // all loads in flight together
+                    const int e = 64 * k + lane, j = base + e;
+                    vin[k] = (e < span && j >= 0 && j < N) ? ld_sc1(in + j) : 0.0;
+                }
+#pragma unroll
+                for (int k = 0; k < SLOTS; ++k) {
+                    const int e = 64 * k + lane;
+                    if (e < span) sc_in[SCI(e)] = vin[k];
+                }
             }
+            DIAG_PH(23);
+            if (has_g) {
+                // replay the group from its checkpoint with the chain's own two
+                // operations per tick (fma(x, +-1, s) rounds as s +- x; VOP2 fmacs)
+                const int e0 = G * gl - base;
+                double sum_g = ck;
+                double xin[G + 8], rv[G];
+#pragma unroll
+                for (int u = -8; u < G; ++u) xin[u + 8] = sc_in[SCI(e0 + u)];
+#pragma unroll
+                for (int u = 0; u < G; ++u) {
+                    sum_g = __builtin_fma(xin[u + 8], one, sum_g);
+                    sum_g = __builtin_fma(xin[u + 8 - WS], mone, sum_g);
+                    rv[u] = sum_g;
+                }
+#pragma unroll
+                for (int u = 0; u < G; ++u) sc_raw[SCI(e0 + u)] = rv[u];
+            }
+            DIAG_PH(24);
+            {
+                constexpr int OSL = MB * kChainCB / 64;
+                double ov[OSL];
+#pragma unroll
+                for (int k = 0; k < OSL; ++k) {  // LDS reads in flight together
+                    const int i = i0 + 64 * k + lane;
+                    ov[k] = i < i1 ? sc_raw[SCI(i + R - base)] : 0.0;
+                }
+#pragma unroll
+                for (int k = 0; k < OSL; ++k) {
+                    const int i = i0 + 64 * k + lane;
+                    // len of the circular buffer after tick i (moving_average.rs:66-81)
+                    const int len = i < N - R ? min(i + R + 1, WS) : WS - 1 - (i - (N - R));
+                    if (i < i1)
+                        __hip_atomic_store(out + i, ov[k] * inv_len[len], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            DIAG_PH(25);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            DIAG_PH(26);
+            // publish in batch order: the batches before b are stored and counted
+            unsigned spins = 0;
+            while (CTL_LD(pub) != b) {
+                if (CTL_LD(abort) || ++spins > kChainSpins) {
+                    ok = false;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (!ok) break;
+            if (lane == 0)
+                __hip_atomic_fetch_max(my_flag, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            CTL_ST(pub, b + 1);
+            if (sw == 0) {
+                DIAGC_ADD(18, 1);
+                DIAGC_ADD(21, __builtin_amdgcn_s_memtime() - tr0);
+                DIAGC_ADD(22, hi - sc);
+            }
+            b += kChainScalers;
+            idle = 0;
         }
-        DIAGC(17, __builtin_amdgcn_s_memtime());
+        if (sw == 0) DIAGC(17, __builtin_amdgcn_s_memtime());
         if (!ok) {
             CTL_ST(abort, 1);
             if (lane == 0) {
                 w.status[s] = MDG_ERR_HIP;
                 // release every downstream pass so all waves drain
-                __hip_atomic_store(my_flag, 1 << 30, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_max(my_flag, 1 << 30, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
     }
 #undef CTL_LD
 #undef CTL_ST
+#undef SCI
+#undef DIAG_PH
 }
 
 __global__ void k_smooth(BatchArgs a, Workspace w, int iters, int ws) {
@@ -2734,7 +2835,7 @@ static void launch_pipe(const BatchArgs& a, const Workspace& w, int iters, hipSt
 template <int WS>
 static void launch_chain(const BatchArgs& a, const Workspace& w, int iters, hipStream_t st) {
     const unsigned grid = 8u * (unsigned)iters * cdiv(a.B, 8);
-    hipLaunchKernelGGL(k_smooth_chain<WS>, dim3(grid), dim3(192), 0, st, a, w, iters);
+    hipLaunchKernelGGL(k_smooth_chain<WS>, dim3(grid), dim3(64 * (2 + kChainScalers)), 0, st, a, w, iters);
 }
 void launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int ws, hipStream_t st) {
     // chain kernel (one CU per pass) for windows <= 8 and batches <= 512; then

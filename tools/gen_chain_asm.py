@@ -101,6 +101,7 @@ def program(ws):
         f"s_cmp_ge_i32 {AVAIL}, {NEED}",
         "s_cbranch_scc1 Lgo%=",
         f"s_mov_b32 {GUARD}, {GUARD_SPINS}",
+        f"s_add_u32 {STAT}, {STAT}, {1 << 17}",  # STAT >> 1: wait episodes << 16 | sleeps
         "Lwait%=:",
         f"ds_read_b32 {VT}, {LDSA}",
         "s_waitcnt lgkmcnt(0)",
@@ -113,11 +114,12 @@ def program(ws):
         f"s_cmp_lg_u32 {TMP}, 0",
         "s_cbranch_scc1 Lto%=",
         "s_sleep 1",
+        f"s_add_u32 {STAT}, {STAT}, 2",
         f"s_sub_u32 {GUARD}, {GUARD}, 1",
         f"s_cmp_lg_u32 {GUARD}, 0",
         "s_cbranch_scc1 Lwait%=",
         "Lto%=:",
-        f"s_mov_b32 {STAT}, 1",
+        f"s_or_b32 {STAT}, {STAT}, 1",
         "s_branch Ldone%=",
         "Lgo%=:",
     ]

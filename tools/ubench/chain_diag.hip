@@ -61,6 +61,13 @@ int main(int argc, char** argv) {
                    "feeder %lld..%lld rounds %lld idle %lld | scaler %lld..%lld rounds %lld idle %lld\n",
                    s, p, q[0] - t0, q[1] - q[0], q[2] - q[1], (q[2] - q[1]) / (ticks > 0 ? ticks : 1), q[4],
                    q[3] - q[2], q[8] - t0, q[9] - t0, q[10], q[11], q[16] - t0, q[17] - t0, q[18], q[19]);
+            printf("    scaler busy %lld cycles for %lld blocks (%.0f per block)\n", q[21], q[22],
+                   q[22] ? (double)q[21] / q[22] : 0.0);
+            printf("    scaler phases: loads+stage %lld replay %lld stores %lld vmcnt %lld\n", q[23], q[24], q[25], q[26]);
+            printf("    chain in_ready waits %lld, sleeps %lld\n", q[6] >> 16, q[6] & 0xffff);
+            for (int k : {5, 12, 20})
+                printf("    HW_ID[%d]: wave %lld simd %lld cu %lld sh %lld se %lld\n", k, q[k] & 15,
+                       (q[k] >> 4) & 3, (q[k] >> 8) & 15, (q[k] >> 12) & 1, (q[k] >> 13) & 7);
         }
     return 0;
 }
