@@ -23,7 +23,7 @@ Operand %[in] is the address of the group before the first block (in + CB*k0 - 8
 import os
 
 CB = int(os.environ.get("CHAIN_CB", "96"))  # ticks per block (the feeder / scaler / LDS staging unit)
-BPT = 1              # blocks per loop trip (2 measured: 20 cycles/tick against 13 -- keep 1)
+BPT = int(os.environ.get("CHAIN_BPT", "2"))  # blocks per loop trip (chain_diag, p0 cycles/tick: 1: 10.85, 2: 10.06, 3: 10.28, 4: 12.35)
 TT = CB * BPT        # ticks per trip
 GROUPS = TT // 8     # multiple of 3: buffer rotation period
 G = int(os.environ.get("CHAIN_G", "32"))  # ticks per stored checkpoint (scaler replay group)
