@@ -17,7 +17,7 @@ SGPR operands, BPT blocks of CB = 96 ticks per loop trip:
     block the prefetch reaches; after the trip, s_waitcnt vmcnt(TT/G) proves
     the previous trip's stores complete, then raw_done is published in LDS.
 
-Fixed registers: s[40:87] operand buffers, s[88:99] loop state, v[0:18].
+Fixed registers: s[16:31] and s[40:87] operand buffers (s[40:87] only with CHAIN_RING3), s[88:99] loop state, v[0:18].
 Operand %[in] is the address of the group before the first block (in + CB*k0 - 8).
 """
 import os
@@ -28,7 +28,11 @@ TT = CB * BPT        # ticks per trip
 GROUPS = TT // 8     # multiple of 3: buffer rotation period
 G = int(os.environ.get("CHAIN_G", "32"))  # ticks per stored checkpoint (scaler replay group)
 assert G % 8 == 0 and TT % G == 0 and TT // G <= 63
-BUF = [40, 56, 72]   # SGPR base of the three 8-double buffers
+RING4 = not os.environ.get("CHAIN_RING3")  # four operand buffers, one lgkmcnt wait per two groups
+# SGPR base of the 8-double buffers (s32 is the stack pointer: not clobbered)
+BUF = [16, 40, 56, 72] if RING4 else [40, 56, 72]
+NB = len(BUF)
+assert GROUPS % NB == 0, "buffer rotation must close within a trip"
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "metabodecon-rust_amd", "csrc", "mdg_chain_asm.inc")
 
@@ -37,6 +41,8 @@ IN, RAW = "s[88:89]", "s[90:91]"
 IN_LO, IN_HI, RAW_LO, RAW_HI = "s88", "s89", "s90", "s91"
 BLK, AVAIL, NIB, GUARD, CNT, TMP, NEED, STAT = "s92", "s93", "s94", "s95", "s96", "s97", "s98", "s99"
 ACC = "v[0:1]"               # running sum
+CKP = "v[2:3]"               # checkpoint copy being stored
+STORE_COPY = bool(os.environ.get("CHAIN_STORE_COPY"))  # measured slower: 10.27 against 10.05 cycles/tick
 ONE, MONE = "v[4:5]", "v[6:7]"
 LDSA, VT, VZ = "v16", "v17", "v18"
 GUARD_SPINS = 1 << 22  # ~0.3 s of s_sleep 1 before the wave gives up (never expected)
@@ -60,18 +66,34 @@ def block_body(ws):
     change at 12.9 cycles/tick -- the cost of the SMEM feed is its issue and
     SGPR write-back on this wave, ~2 cycles/tick, not its latency.)"""
     L = []
+    pending = None  # checkpoint copied into CKP, stored one tick into the next group
     for q in range(GROUPS):
-        prev, cur, nxt = q % 3, (q + 1) % 3, (q + 2) % 3
-        # IN points one group (64 B) before the block: group q+1 starts at 64*(q+2)
+        # group t lives in buffer (t + 1) % NB; IN points one group (64 B) before the
+        # block, so group t starts at 64*(t+1). Three buffers: load group q+1 now,
+        # wait at the end of q. Four: load q+2 now (into q-2's buffer), wait at the
+        # end of odd groups only (q+1 and q+2 are both in flight by then).
+        prev, cur = q % NB, (q + 1) % NB
+        ahead = NB - 2
+        nxt = (q + 1 + ahead) % NB
         if not os.environ.get("CHAIN_NOLOAD"):  # diagnostic variants only (wrong results)
-            L.append(f"s_load_dwordx16 s[{BUF[nxt]}:{BUF[nxt] + 15}], {IN}, {64 * (q + 2)}")
+            L.append(f"s_load_dwordx16 s[{BUF[nxt]}:{BUF[nxt] + 15}], {IN}, {64 * (q + 1 + ahead)}")
         for u in range(8):
             L.append(f"v_fmac_f64 {ACC}, {sreg(cur, u)}, {ONE}")
             pop = sreg(cur, u - ws) if u >= ws else sreg(prev, 8 + u - ws)
             L.append(f"v_fmac_f64 {ACC}, {pop}, {MONE}")
-        L.append("s_waitcnt lgkmcnt(0)")
+            if u == 0 and pending is not None:
+                L.append(f"global_store_dwordx2 {VZ}, {CKP}, {RAW} offset:{pending}")
+                pending = None
+        if not os.environ.get("CHAIN_NOWAIT") and (not RING4 or q % 2 == 1):
+            L.append("s_waitcnt lgkmcnt(0)")
         if (8 * q + 8) % G == 0 and not os.environ.get("CHAIN_NOSTORE"):
-            L.append(f"global_store_dwordx2 {VZ}, {ACC}, {RAW} offset:{8 * (8 * q + 7)}")
+            if STORE_COPY:
+                L.append(f"v_mov_b64 {CKP}, {ACC}")
+                pending = 8 * (8 * q + 7)
+            else:
+                L.append(f"global_store_dwordx2 {VZ}, {ACC}, {RAW} offset:{8 * (8 * q + 7)}")
+    if pending is not None:  # the trip's last checkpoint
+        L.append(f"global_store_dwordx2 {VZ}, {CKP}, {RAW} offset:{pending}")
     return L
 
 
@@ -91,8 +113,7 @@ def program(ws):
         f"v_mov_b64 {ACC}, %[sum]",
         f"v_mov_b64 {ONE}, 1.0",
         f"v_mov_b64 {MONE}, -1.0",
-        f"s_load_dwordx16 s[{BUF[0]}:{BUF[0] + 15}], {IN}, 0",
-        f"s_load_dwordx16 s[{BUF[1]}:{BUF[1] + 15}], {IN}, 64",
+    ] + [f"s_load_dwordx16 s[{BUF[t]}:{BUF[t] + 15}], {IN}, {64 * t}" for t in range(NB - 1)] + [
         "s_waitcnt lgkmcnt(0)",
         "Lblk%=:",
         # need = min(blk + BPT + 1, nib); re-read the helper's in_ready only when the cached value is short
