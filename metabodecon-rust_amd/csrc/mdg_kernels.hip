@@ -698,18 +698,19 @@ __global__ __launch_bounds__(512) void k_smooth_waves(BatchArgs a, Workspace w, 
 // cycles, any other instruction of the same wave 3-10 more, an s_load_dwordx16
 // plus its wait almost nothing when it feeds 8 ticks, and one CU issues one
 // 16-byte vector store per ~16 cycles across all its waves. So each pass runs
-// on its own CU, in three waves:
+// on its own CU, in four waves (one per SIMD):
 //  * chain wave: issues little besides the reference's two dependent adds per
 //    tick (moving_average.rs:69-80, in j = i + R form below) on SGPR operands,
 //    and stores one checkpoint per kChainG = 32 ticks (the group's last raw sum);
 //  * feeder wave: waits for the previous pass's published blocks (sc1 polls),
-//    pulls them into L2 and touches them into the scalar cache, and publishes
-//    in_ready in LDS;
-//  * scaler wave: replays each group of 32 ticks from its checkpoint with the same
-//    two operations (bit-identical sums), multiplies by the reference's 1/len
-//    (moving_average.rs:66-81: 1/len while the buffer grows, 1/ws, then 1/len
-//    in the tail) and publishes finished blocks to the next pass (sc1 stores,
-//    vmcnt(0), sc1 counter; the consumer polls with sc1 loads --
+//    publishes them to the chain (in_ready in LDS), pulls them into L2 and
+//    touches them into the scalar cache ahead of the chain;
+//  * two scaler waves, batches of kChainScBatch output blocks round-robin: replay
+//    each group of 32 ticks from its checkpoint with the same two operations
+//    (bit-identical sums), multiply by the reference's 1/len (moving_average.rs:
+//    66-81: 1/len while the buffer grows, 1/ws, then 1/len in the tail) and
+//    publish finished batches to the next pass in batch order (sc1 stores,
+//    vmcnt(0), atomic-max counter; the consumer polls with sc1 loads --
 //    MI355X_MICROARCH.md, cross-CU hand-offs).
 //
 // Per pass, in j = 0 .. N+R-1:  if j < N: sum += in[j];  if j >= WS: sum -= in[j-WS];
