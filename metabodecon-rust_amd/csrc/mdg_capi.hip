@@ -253,7 +253,7 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     int gfit = 24;  // k_fit_sup workgroups per spectrum (3 * 2048 / 256)
     if (const char* e = std::getenv("MDG_GFIT")) gfit = std::max(1, std::atoi(e));  // tuning
     const int gupd = std::max(1, std::min(16, 1024 / std::max(1, a.B)));
-    const int nparts = std::max(1, std::min({1024, (a.N + 255) / 256, std::max(1, 4096 / a.B)}));
+    const int nparts = mse_nparts(a);
     // chain smoother buffers: raw sums of every pass, scaled outputs of passes
     // 0..P-2 and one 128-byte progress counter per (spectrum, pass)
     w.thr_s = c->ovr_thr;

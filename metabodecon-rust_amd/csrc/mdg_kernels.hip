@@ -134,6 +134,62 @@ __device__ __forceinline__ double superpose_t(double x, const double* __restrict
     return acc;
 }
 
+// NPT points per thread against the same Lorentzian groups: each point's sum is the
+// same left fold as superpose_t (bit-identical), the parameter loads are shared and
+// the NPT evaluations of a term are independent (ILP with one wave per SIMD)
+template <bool FAST, int NPT>
+__device__ __forceinline__ void sup_group_n(const double (&x)[NPT], double (&acc)[NPT],
+                                            const double (&c)[3 * kSupGP], double (&n)[3 * kSupGP],
+                                            const_f64_ptr next, bool load_next) {
+    double e[NPT][kSupGP];
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) e[i][0] = lorentz_t<FAST>(x[i], c[0], c[1], c[2]);
+    __builtin_amdgcn_sched_barrier(0);
+    if (load_next) {
+#pragma unroll
+        for (int k = 0; k < 3 * kSupGP; ++k) n[k] = next[k];
+    }
+#pragma unroll
+    for (int k = 1; k < kSupGP; ++k)
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) e[i][k] = lorentz_t<FAST>(x[i], c[3 * k], c[3 * k + 1], c[3 * k + 2]);
+#pragma unroll
+    for (int i = 0; i < NPT; ++i)
+#pragma unroll
+        for (int k = 0; k < kSupGP; ++k) acc[i] += e[i][k];
+}
+
+template <bool FAST, int NPT>
+__device__ __forceinline__ void superpose_n(const double (&x)[NPT], const double* __restrict__ params_g,
+                                            int P, double (&acc)[NPT]) {
+    constexpr int GW = 3 * kSupGP;
+    const const_f64_ptr params = (const_f64_ptr)(params_g);
+    const int G = P / kSupGP;
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) acc[i] = -0.0;
+    int g = 0;
+    if (G > 0) {
+        double A[GW], B[GW];
+#pragma unroll
+        for (int k = 0; k < GW; ++k) A[k] = params[k];
+        for (; g + 2 < G; g += 2) {
+            sup_group_n<FAST, NPT>(x, acc, A, B, params + GW * (g + 1), true);
+            sup_group_n<FAST, NPT>(x, acc, B, A, params + GW * (g + 2), true);
+        }
+        if (g + 1 < G) {
+            sup_group_n<FAST, NPT>(x, acc, A, B, params + GW * (g + 1), true);
+            sup_group_n<FAST, NPT>(x, acc, B, A, params, false);
+        } else {
+            sup_group_n<FAST, NPT>(x, acc, A, B, params, false);
+        }
+    }
+    for (int j = kSupGP * G; j < P; ++j) {
+        const_f64_ptr L = params + 3 * j;
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) acc[i] += lorentz_t<FAST>(x[i], L[0], L[1], L[2]);
+    }
+}
+
 __device__ __forceinline__ double superpose(double x, const double* __restrict__ params, int P,
                                             bool fast) {
     return fast ? superpose_t<true>(x, params, P) : superpose_t<false>(x, params, P);
@@ -2713,6 +2769,70 @@ __global__ __launch_bounds__(BS) void k_mse_partial(BatchArgs a, Workspace w, in
     }
 }
 
+// NPT points per thread: with 91.8k signal-region points, one point
+// per lane needs 1434 waves on 1024 SIMDs, so 410 SIMDs run two waves back to back;
+// two points per lane fit every thread block on its own SIMDs (718 waves) with two
+// independent evaluations per term. Same per-point folds, same residual order
+// within a thread (point i before i + 1), then the same shuffle / LDS tree.
+template <int BS, int NPT>
+__global__ __launch_bounds__(BS) void k_mse_partial_n(BatchArgs a, Workspace w, int nparts) {
+    const int s = blockIdx.x % a.B, part = blockIdx.x / a.B;
+    __shared__ double red[BS / 64];
+    if (w.status[s] || w.mse_panic[s]) return;
+    const int P = w.kept_count[s];
+    const double* __restrict__ kept = w.kept + 3 * (size_t)s * w.capD;
+    const double* x = a.x + (size_t)s * a.x_stride;
+    const double* y = a.y + (size_t)s * a.y_stride;
+    const int nig = w.n_ig[s];
+    int64_t total = 0;
+    for (int r = 0; r <= nig; ++r) {
+        int64_t lo, hi;
+        mse_region(w, s, r, nig, &lo, &hi);
+        total += hi - lo;
+    }
+    const bool fast = w.x_ok[s] && w.unsafe_kept[s] == 0;
+    double acc = 0.0;
+    for (int64_t v0 = (int64_t)part * BS * NPT + threadIdx.x; v0 < total;
+         v0 += (int64_t)nparts * BS * NPT) {
+        double xv[NPT], yv[NPT];
+        bool ok[NPT];
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) {
+            const int64_t v = v0 + (int64_t)i * BS;
+            ok[i] = v < total;
+            int64_t rem = ok[i] ? v : 0, idx = 0;
+            for (int r = 0; r <= nig; ++r) {
+                int64_t lo, hi;
+                mse_region(w, s, r, nig, &lo, &hi);
+                if (rem < hi - lo) {
+                    idx = lo + rem;
+                    break;
+                }
+                rem -= hi - lo;
+            }
+            xv[i] = x[idx];
+            yv[i] = y[idx];
+        }
+        double sup[NPT];
+        if (fast) superpose_n<true, NPT>(xv, kept, P, sup);
+        else superpose_n<false, NPT>(xv, kept, P, sup);
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) {
+            const double d = sup[i] - yv[i];
+            if (ok[i]) acc += d * d;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int k = 0; k < BS / 64; ++k) t += red[k];
+        w.mse_part[(size_t)s * nparts + part] = t;
+    }
+}
+
 // total length of the MSE regions of spectrum s (the divisor of compute_mse)
 __device__ __forceinline__ int64_t mse_len(const Workspace& w, int s) {
     const int nig = w.n_ig[s];
@@ -2950,8 +3070,21 @@ void launch_fit_update(const BatchArgs& a, const Workspace& w, int gx, int it, h
 void launch_retain(const BatchArgs& a, const Workspace& w, hipStream_t st) {
     hipLaunchKernelGGL(k_retain<1024>, dim3(a.B), dim3(1024), 0, st, a, w);
 }
+// points per thread of the MSE superposition (MDG_MSE_NPT overrides, for tuning)
+static int mse_npt(const BatchArgs& a) {
+    if (const char* e = std::getenv("MDG_MSE_NPT")) return std::atoi(e) == 2 ? 2 : 1;
+    return 2;  // bench: B = 1 124 -> 113 us, B = 256 16.79 -> 16.62 ms
+}
+int mse_nparts(const BatchArgs& a) {
+    const int base = std::max(1, std::min({1024, (a.N + 255) / 256, std::max(1, 4096 / a.B)}));
+    const int npt = mse_npt(a);
+    return std::max(1, (base + npt - 1) / npt);
+}
 void launch_mse(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st) {
-    hipLaunchKernelGGL(k_mse_partial<256>, dim3(nparts * a.B), dim3(256), 0, st, a, w, nparts);
+    if (mse_npt(a) == 2)
+        hipLaunchKernelGGL((k_mse_partial_n<256, 2>), dim3(nparts * a.B), dim3(256), 0, st, a, w, nparts);
+    else
+        hipLaunchKernelGGL(k_mse_partial<256>, dim3(nparts * a.B), dim3(256), 0, st, a, w, nparts);
 }
 void launch_mse_final(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st) {
     hipLaunchKernelGGL(k_mse_final, dim3(a.B), dim3(64), 0, st, a, w, nparts);

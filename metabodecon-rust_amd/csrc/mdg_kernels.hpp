@@ -115,6 +115,8 @@ bool fit_sup_fused(const BatchArgs& a);
 void launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st);
 void launch_fit_update(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st);
 void launch_retain(const BatchArgs& a, const Workspace& w, hipStream_t st);
+// MSE partial sums per spectrum for launch_mse / launch_mse_final (<= 1024)
+int mse_nparts(const BatchArgs& a);
 void launch_mse(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st);
 void launch_mse_final(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st);
 // windowed left fold of n <= kWinMax non-negative terms (test support)
