@@ -222,7 +222,7 @@ def main():
     fit_kernel = ("k_fit_sup_tf" if B <= 2 else "k_fit_sup_dpp" if B <= 8 else "k_fit_sup")
     work = {
         "fit_superposition": ("fp64", fit_flops, "TFLOP/s", fit_kernel),
-        "mse_superposition": ("fp64", mse_flops, "TFLOP/s", "k_mse_partial<256>"),
+        "mse_superposition": ("fp64", mse_flops, "TFLOP/s", "k_mse_partial_n<256, 2>"),
         "smooth": ("hbm", smooth_bytes, "GB/s", smooth_kernel),
         "detect": ("hbm", detect_bytes, "GB/s", "k_flags+k_peaks_count+k_peaks_write"),
     }
