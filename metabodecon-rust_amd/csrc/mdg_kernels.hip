@@ -1774,7 +1774,7 @@ __device__ double dpp_fold(double acc, const double* __restrict__ t, int n) {
 // the result is the reference's bits whatever the estimates (they only decide
 // how often step C falls back).
 // ----------------------------------------------------------------------------------
-constexpr int kWinSeg = 32;
+constexpr int kWinSeg = 16;  // one segment per wave of k_select (32: 6% slower, the walk is serial)
 struct WinLds {
     double F[kWinSeg][64];
     double E[kWinSeg];
@@ -1822,8 +1822,8 @@ __device__ double window_fold(double acc0, WinLds& L, const double* __restrict__
     KSTAMP(stamp + 5);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int seg = (n + kWinSeg - 1) / kWinSeg;
-    // A. double-double sums of the segments (wave w: segments w, w+NW, ...); each
-    // lane's terms of a segment are loaded together
+    // A. double-double sums of the segments (wave w: segments w, w+NW, ...); a
+    // lane's terms of a segment are loaded 8 at a time (16: slower, 12k against 8k cycles)
     for (int k = wv; k < kWinSeg; k += NW) {
         double hi = 0.0, lo = 0.0;
         const int i0 = k * seg, i1 = min(n, (k + 1) * seg);
@@ -1853,19 +1853,30 @@ __device__ double window_fold(double acc0, WinLds& L, const double* __restrict__
     __syncthreads();
     KSTAMP(stamp + 6);
     if (threadIdx.x < 64) {
-        // exclusive prefix of the segment sums, in double-double, by wave 0: the
-        // segment sums are read once into lanes and walked with readlanes
-        const double fh = lane < kWinSeg ? L.F[lane][0] : 0.0;
-        const double fl = lane < kWinSeg ? L.F[lane][1] : 0.0;
-        double hi = acc0 == 0.0 ? 0.0 : acc0, lo = 0.0, mine = 0.0;
-        for (int k = 0; k < kWinSeg; ++k) {
+        // exclusive prefix of the segment sums in double-double, by wave 0 as a
+        // log-depth (Kogge-Stone) scan over lanes: the estimates only decide which
+        // candidate windows step C tries, so their summation order is free
+        double hi = lane < kWinSeg ? L.F[lane][0] : 0.0;
+        double lo = lane < kWinSeg ? L.F[lane][1] : 0.0;
+        if (lane == 0) {  // acc0 enters before segment 0
             double e;
-            two_sum(hi, lo, hi, lo);  // renormalise
-            if (lane == k) mine = hi;
-            two_sum(hi, readlane_f64(fh, k), hi, e);
-            lo += readlane_f64(fl, k) + e;
+            two_sum(acc0 == 0.0 ? 0.0 : acc0, hi, hi, e);
+            lo += e;
         }
-        if (lane < kWinSeg) L.E[lane] = mine;
+#pragma unroll
+        for (int o = 1; o < kWinSeg; o <<= 1) {
+            const double h2 = __shfl_up(hi, o, 64), l2 = __shfl_up(lo, o, 64);
+            if (lane >= o) {
+                double e;
+                two_sum(hi, h2, hi, e);
+                lo += l2 + e;
+            }
+        }
+        // inclusive -> exclusive: segment k starts at the sum through segment k-1
+        double ih, il;
+        two_sum(hi, lo, ih, il);
+        const double ex = __shfl_up(ih, 1, 64);
+        if (lane < kWinSeg) L.E[lane] = lane == 0 ? (acc0 == 0.0 ? 0.0 : acc0) : ex;
     }
     __syncthreads();
     KSTAMP(stamp);
@@ -1883,17 +1894,20 @@ __device__ double window_fold(double acc0, WinLds& L, const double* __restrict__
     }
     __syncthreads();
     KSTAMP(stamp + 1);
-    // C. the true chain through the segments, by wave 0
+    // C. the true chain through the segments, by wave 0: the true value entering
+    // segment k is candidate d = bits(tru) - bits(E_k) + 32 when that lies in
+    // [0, 64) (clamped candidates below +0 only ever equal +0, which d then names),
+    // and the value leaving it is that candidate's result, one LDS read away
     if (wv == 0) {
-        double tru = readlane_f64(L.F[0][lane], 0);
+        const long long eb = lane < kWinSeg ? __double_as_longlong(L.E[lane]) : 0;
+        double tru = L.F[0][0];
 #pragma unroll 1
         for (int k = 1; k < kWinSeg; ++k) {
-            const long long b = __double_as_longlong(L.E[k]) + (lane - 32);
-            const long long cand = b < 0 ? 0ll : b;
-            const double fk = L.F[k][lane];
-            const unsigned long long hit = __ballot(cand == __double_as_longlong(tru));
-            if (hit) {
-                tru = readlane_f64(fk, __ffsll((unsigned long long)hit) - 1);
+            const long long ek = ((long long)__builtin_amdgcn_readlane((int)(eb >> 32), k) << 32) |
+                                 (long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)(eb & 0xffffffffll), k);
+            const long long d = __double_as_longlong(tru) - ek + 32;
+            if (d >= 0 && d < 64) {
+                tru = L.F[k][(int)d];
             } else {  // outside the window: this segment from the true value
                 const int i0 = min(n, k * seg), i1 = min(n, (k + 1) * seg);
                 tru = seg_fold(tru, t + i0, i1 - i0);
