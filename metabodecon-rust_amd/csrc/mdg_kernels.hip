@@ -1304,6 +1304,9 @@ __global__ void k_flags(BatchArgs a, Workspace w) {
         fr = d0 > dm && (d0 >= dp || (d0 < 0. && dp >= 0.));
         fl = d0 > dp && (d0 >= dm || (d0 < 0. && dm >= 0.));
     }
+    // k_peaks' per-chunk slots start empty
+    if (blockIdx.x == 0 && (int)threadIdx.x < (w.W + 255) / 256)
+        ((unsigned long long*)w.peak_cnt)[(size_t)s * ((w.W + 255) / 256) + threadIdx.x] = 0;
     const uint64_t bc = __ballot(fc), br = __ballot(fr), bl = __ballot(fl);
     if ((threadIdx.x & 63) == 0 && k < N) {
         const int word = k >> 6;
@@ -1401,6 +1404,62 @@ __global__ __launch_bounds__(kPkWords) void k_peaks_count(BatchArgs a, Workspace
         cnt[2 * chunk] = (int32_t)k_tot;
         cnt[2 * chunk + 1] = (int32_t)b_tot;
     }
+}
+
+// K3 in one pass (decoupled look-back): every chunk counts its peaks, publishes
+// {bordered, kept} in its slot of w.peak_cnt (cleared by k_flags), then reads the
+// slots of all chunks of its spectrum -- they publish before they wait, so one
+// round of flag latency -- and compacts its peaks after the kept peaks of the
+// chunks before it. Replaces k_peaks_count + k_peaks_write (one launch and one
+// word scan fewer).
+constexpr unsigned long long kPkValid = 1ull << 62;
+__global__ __launch_bounds__(kPkWords) void k_peaks(BatchArgs a, Workspace w, int detector_only) {
+    const int s = blockIdx.y, chunk = blockIdx.x;
+    __shared__ int lds_i[kPkWords / 64 + 1];
+    __shared__ long long lds_l[kPkWords / 64 + 1];
+    if (w.status[s]) return;  // uniform per spectrum: no chunk waits for a returned one
+    const int nch = (w.W + kPkWords - 1) / kPkWords;
+    unsigned long long* slot = (unsigned long long*)w.peak_cnt + (size_t)s * nch;
+    const int wd = chunk * kPkWords + threadIdx.x;
+    int bordered = 0, kept = 0;
+    if (wd < w.W) kept = word_peaks<false>(a, w, s, wd, detector_only, &bordered, 0);
+    int total;
+    const int o = block_exclusive_scan<kPkWords>(kept, lds_i, &total);
+    const long long b_tot = block_sum_ll<kPkWords>(bordered, lds_l);
+    if (threadIdx.x == 0)
+        __hip_atomic_store(slot + chunk, kPkValid | ((unsigned long long)b_tot << 31) | (unsigned)total,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    long long before = 0, k_all = 0, b_all = 0;
+    bool ok = true;
+    for (int k = threadIdx.x; k < nch; k += kPkWords) {
+        unsigned long long v;
+        unsigned spins = 0;
+        while (!((v = __hip_atomic_load(slot + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & kPkValid)) {
+            if (++spins > (1u << 22)) {
+                ok = false;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        const long long kk = (long long)(v & 0x7fffffffull), bb = (long long)((v >> 31) & 0x7fffffffull);
+        before += k < chunk ? kk : 0;
+        k_all += kk;
+        b_all += bb;
+    }
+    before = block_sum_ll<kPkWords>(before, lds_l);
+    k_all = block_sum_ll<kPkWords>(k_all, lds_l);
+    b_all = block_sum_ll<kPkWords>(b_all, lds_l);
+    const long long bad = block_sum_ll<kPkWords>(ok ? 0 : 1, lds_l);
+    if (bad) {
+        if (threadIdx.x == 0) w.status[s] = MDG_ERR_HIP;
+        return;
+    }
+    if (b_all == 0) {
+        if (chunk == 0 && threadIdx.x == 0) w.status[s] = MDG_NO_PEAKS_DETECTED;
+        return;
+    }
+    if (chunk == 0 && threadIdx.x == 0) w.det_count[s] = (int32_t)k_all;
+    if (kept) word_peaks<true>(a, w, s, wd, detector_only, &bordered, (size_t)s * w.capD + before + o);
 }
 
 __global__ __launch_bounds__(kPkWords) void k_peaks_write(BatchArgs a, Workspace w, int detector_only) {
@@ -3030,8 +3089,13 @@ void launch_flags(const BatchArgs& a, const Workspace& w, hipStream_t st) {
 }
 void launch_peaks(const BatchArgs& a, const Workspace& w, int detector_only, hipStream_t st) {
     const int nch = cdiv(w.W, kPkWords);
-    hipLaunchKernelGGL(k_peaks_count, dim3(nch, a.B), dim3(kPkWords), 0, st, a, w, detector_only);
-    hipLaunchKernelGGL(k_peaks_write, dim3(nch, a.B), dim3(kPkWords), 0, st, a, w, detector_only);
+    static_assert(kPkWords == 256, "k_flags clears ceil(W / 256) slots");
+    if (std::getenv("MDG_PEAKS_2PASS")) {  // the two-kernel form, for comparison
+        hipLaunchKernelGGL(k_peaks_count, dim3(nch, a.B), dim3(kPkWords), 0, st, a, w, detector_only);
+        hipLaunchKernelGGL(k_peaks_write, dim3(nch, a.B), dim3(kPkWords), 0, st, a, w, detector_only);
+        return;
+    }
+    hipLaunchKernelGGL(k_peaks, dim3(nch, a.B), dim3(kPkWords), 0, st, a, w, detector_only);
 }
 void launch_scores(const BatchArgs& a, const Workspace& w, hipStream_t st) {
     const int gx = std::max(1, std::min(64, 4096 / std::max(1, a.B)));
