@@ -168,6 +168,7 @@ int ensure_workspace(mdg_ctx* c, int B, int N) {
         const size_t o_dcnt = take(Bs * 4), o_scnt = take(Bs * 4), o_kcnt = take(Bs * 4);
         const size_t o_xok = take(Bs * 4), o_unsafe = take(Bs * 16), o_uk = take(Bs * 4);
         const size_t o_pcnt = take(Bs * 2 * ((W + 255) / 256) * 4);
+        const size_t o_mcnt = take(Bs * 4);
 
         if (c->arena.p) (void)hipFree(c->arena.p);
         c->arena.p = nullptr;
@@ -207,6 +208,9 @@ int ensure_workspace(mdg_ctx* c, int B, int N) {
         w.unsafe = (int32_t*)(base + o_unsafe);
         w.unsafe_kept = (int32_t*)(base + o_uk);
         w.peak_cnt = (int32_t*)(base + o_pcnt);
+        w.mse_done = (int32_t*)(base + o_mcnt);
+        // k_mse_partial_n's arrival counters start (and are always left) at zero
+        HIPCHK(hipMemset(w.mse_done, 0, Bs * 4));
 
         c->ws_B = nB;
         c->ws_N = nN;

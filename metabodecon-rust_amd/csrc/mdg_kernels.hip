@@ -2847,11 +2847,22 @@ __global__ __launch_bounds__(BS) void k_mse_partial(BatchArgs a, Workspace w, in
 // two points per lane fit every thread block on its own SIMDs (718 waves) with two
 // independent evaluations per term. Same per-point folds, same residual order
 // within a thread (point i before i + 1), then the same shuffle / LDS tree.
+__device__ __forceinline__ int64_t mse_len(const Workspace& w, int s);
+__device__ __forceinline__ void mse_panic_out(const BatchArgs& a, int s);
+
+// The last workgroup of a spectrum to finish (arrival counter, acq_rel at agent
+// scope: the partials of the others are visible to it) folds the partials itself
+// (k_mse_final's work, one launch fewer) and resets the counter.
 template <int BS, int NPT>
 __global__ __launch_bounds__(BS) void k_mse_partial_n(BatchArgs a, Workspace w, int nparts) {
     const int s = blockIdx.x % a.B, part = blockIdx.x / a.B;
     __shared__ double red[BS / 64];
-    if (w.status[s] || w.mse_panic[s]) return;
+    __shared__ int last;
+    if (w.status[s]) return;  // already reported by k_retain
+    if (w.mse_panic[s]) {
+        if (part == 0) mse_panic_out(a, s);
+        return;
+    }
     const int P = w.kept_count[s];
     const double* __restrict__ kept = w.kept + 3 * (size_t)s * w.capD;
     const double* x = a.x + (size_t)s * a.x_stride;
@@ -2902,7 +2913,37 @@ __global__ __launch_bounds__(BS) void k_mse_partial_n(BatchArgs a, Workspace w, 
     if (threadIdx.x == 0) {
         double t = 0.0;
         for (int k = 0; k < BS / 64; ++k) t += red[k];
-        w.mse_part[(size_t)s * nparts + part] = t;
+        // sc1 store, its completion, then the arrival (the smoother's hand-off; an
+        // acq_rel RMW here writes back L2 in every workgroup: +10 us at B = 1)
+        __hip_atomic_store(w.mse_part + (size_t)s * nparts + part, t, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int done = __hip_atomic_fetch_add(w.mse_done + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = done == nparts - 1;
+        if (last) __hip_atomic_store(w.mse_done + s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!last) return;
+    __shared__ double parts[1024];
+    for (int k = threadIdx.x; k < nparts; k += BS) parts[k] = ld_sc1(w.mse_part + (size_t)s * nparts + k);
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        // dpp_fold's order (groups of 16 by row broadcast, then the remainder) on the
+        // LDS copy; dpp_fold itself streams with global loads, which LDS cannot serve
+        const int sub = threadIdx.x & 15;
+        const double one = 1.0;
+        double t = 0.0;
+        const int G = nparts / 16;
+        for (int g = 0; g < G; ++g) fold16(t, parts[16 * g + sub], one);
+        const int r = nparts - 16 * G;
+        if (r > 0) {
+            const double v = parts[min(16 * G + sub, nparts - 1)];
+            for (int k = 0; k < r; ++k) t += readlane_f64(v, k);
+        }
+        if (threadIdx.x == 0) {
+            a.out_mse[s] = t / (double)mse_len(w, s);
+            a.out_status[s] = (w.kept_count[s] > a.cap) ? MDG_CAPACITY : MDG_OK;
+        }
     }
 }
 
@@ -2921,20 +2962,30 @@ __device__ __forceinline__ int64_t mse_len(const Workspace& w, int s) {
 // One wave per spectrum: the nparts partial sums are folded left to right from +0.0
 // (the order k_mse_partial's tree fixes) with the ordered DPP fold, instead of a
 // single thread whose dependent global loads cost ~200 cycles each (42 us at B=1).
+// the nparts partials of spectrum s, folded by one wave (threads 0..63)
+__device__ __forceinline__ void mse_finish(const BatchArgs& a, const Workspace& w, int s,
+                                           const double* part, int nparts) {
+    const double t = dpp_fold(0.0, part, nparts);
+    if (threadIdx.x != 0) return;
+    a.out_mse[s] = t / (double)mse_len(w, s);
+    a.out_status[s] = (w.kept_count[s] > a.cap) ? MDG_CAPACITY : MDG_OK;
+}
+
+__device__ __forceinline__ void mse_panic_out(const BatchArgs& a, int s) {
+    if (threadIdx.x == 0) {
+        a.out_status[s] = MDG_REFERENCE_PANIC;
+        a.out_mse[s] = 0.0;
+    }
+}
+
 __global__ __launch_bounds__(64) void k_mse_final(BatchArgs a, Workspace w, int nparts) {
     const int s = blockIdx.x;
     if (w.status[s]) return;  // already reported by k_retain
     if (w.mse_panic[s]) {
-        if (threadIdx.x == 0) {
-            a.out_status[s] = MDG_REFERENCE_PANIC;
-            a.out_mse[s] = 0.0;
-        }
+        mse_panic_out(a, s);
         return;
     }
-    const double t = dpp_fold(0.0, w.mse_part + (size_t)s * nparts, nparts);
-    if (threadIdx.x != 0) return;
-    a.out_mse[s] = t / (double)mse_len(w, s);
-    a.out_status[s] = (w.kept_count[s] > a.cap) ? MDG_CAPACITY : MDG_OK;
+    mse_finish(a, w, s, w.mse_part + (size_t)s * nparts, nparts);
 }
 
 // ----------------------------------------------------------------------------------
@@ -3165,6 +3216,7 @@ void launch_mse(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t 
         hipLaunchKernelGGL(k_mse_partial<256>, dim3(nparts * a.B), dim3(256), 0, st, a, w, nparts);
 }
 void launch_mse_final(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st) {
+    if (mse_npt(a) == 2) return;  // k_mse_partial_n folded the partials itself
     hipLaunchKernelGGL(k_mse_final, dim3(a.B), dim3(64), 0, st, a, w, nparts);
 }
 void launch_mse_exact(const double* sup, const double* y, int64_t n, const ExactRegions& r,

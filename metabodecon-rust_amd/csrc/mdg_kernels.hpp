@@ -76,6 +76,7 @@ struct Workspace {
     int32_t* unsafe;          // B x 4: count of fit params outside it, per params version
                               // (k_fit_update path: version & 1; fused k_fit_sup_tf: version % 3)
     int32_t* unsafe_kept;     // B: same for the retained Lorentzians
+    int32_t* mse_done;        // B: k_mse_partial_n workgroups finished (the last one folds, resets)
     int32_t* peak_cnt;        // B x ceil(W/256) u64: k_peaks slots {valid, bordered, kept} per mask chunk
     // k_smooth_chain (allocated on first use; null otherwise)
     double* chain_raw;        // P x B x chain_stride: raw running sums of every pass
