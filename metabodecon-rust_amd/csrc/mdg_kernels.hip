@@ -2044,14 +2044,45 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
     const int64_t sbi0 = w.sbi[2 * s], sbi1 = w.sbi[2 * s + 1];
     double* scores = w.scores + base;
     KSTAMP(10);
-    long long c0 = 0, c1 = 0;
-    for (int p = threadIdx.x; p < P; p += BS) {  // scores: k_scores
-        const int64_t c = pc[p];
-        c0 += c <= sbi0;
-        c1 += c <= sbi1;
+    // #(center <= sbi0) and #(center <= sbi1) over the ascending centers (scores:
+    // k_scores), by a two-level search: every step-th center first, then the step-1
+    // centers after the last sampled one that passed (both counts packed in one sum)
+    const int step = (P + BS - 1) / BS;
+    long long k01;
+    {
+        const int i = threadIdx.x * step;
+        long long v = 0;
+        if (i < P) {
+            const int64_t c = pc[i];
+            v = ((long long)(c <= sbi0) << 32) | (long long)(c <= sbi1);
+        }
+        k01 = block_sum_ll<BS>(v, lds_l);
     }
-    const long long cnt0 = block_sum_ll<BS>(c0, lds_l);
-    const long long cnt1 = block_sum_ll<BS>(c1, lds_l);
+    const long long k0 = k01 >> 32, k1 = k01 & 0xffffffffll;
+    long long cnt0 = k0 > 0 ? (k0 - 1) * step + 1 : 0, cnt1 = k1 > 0 ? (k1 - 1) * step + 1 : 0;
+    if (2 * (step - 1) > BS) {  // more than 2 * 513 * BS / 2 peaks: plain count
+        long long c0 = 0, c1 = 0;
+        for (int p = threadIdx.x; p < P; p += BS) {
+            const int64_t c = pc[p];
+            c0 += c <= sbi0;
+            c1 += c <= sbi1;
+        }
+        cnt0 = block_sum_ll<BS>(c0, lds_l);
+        cnt1 = block_sum_ll<BS>(c1, lds_l);
+    } else if (step > 1) {
+        const int t = threadIdx.x;
+        long long v = 0;
+        if (t < step - 1 && k0 > 0) {
+            const long long i = (k0 - 1) * step + 1 + t;
+            if (i < P) v += (long long)(pc[i] <= sbi0) << 32;
+        } else if (t >= step - 1 && t < 2 * (step - 1) && k1 > 0) {
+            const long long i = (k1 - 1) * step + 1 + (t - (step - 1));
+            if (i < P) v += (long long)(pc[i] <= sbi1);
+        }
+        const long long r = block_sum_ll<BS>(v, lds_l);
+        cnt0 += r >> 32;
+        cnt1 += r & 0xffffffffll;
+    }
     // centers ascend: position(center > sb) == #(center <= sb)
     const int left = cnt0 < P ? (int)cnt0 : 0;
     const long long r1 = cnt1 > left ? cnt1 : left;
