@@ -781,7 +781,10 @@ constexpr int kChainCB = MDG_CHAIN_CB;
 #define MDG_CHAIN_PF 8
 #endif
 constexpr int kChainScalers = 2;         // scaler waves (round-robin batches)
-constexpr int kChainScBatch = 8;         // output blocks per scaler batch
+#ifndef MDG_CHAIN_SCB
+#define MDG_CHAIN_SCB 8  // chain_diag ms: 2: 1.27, 4: 0.77, 8: 0.595, 12: 0.589, 16: 0.596; bench: 12 is 1% slower
+#endif
+constexpr int kChainScBatch = MDG_CHAIN_SCB;  // output blocks per scaler batch
 constexpr int kChainG = MDG_CHAIN_G;      // ticks per stored checkpoint in steady blocks
 static_assert(kChainG % 8 == 0 && kChainCB % kChainG == 0, "checkpoint groups tile the blocks");
 constexpr int kChainPrefetch = MDG_CHAIN_PF;  // input blocks touched into the scalar cache ahead
