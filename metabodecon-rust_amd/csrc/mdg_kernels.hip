@@ -2789,13 +2789,52 @@ __global__ __launch_bounds__(BS) void k_retain(BatchArgs a, Workspace w) {
     const double* params = params_version(w, base, ver);
     const int per = (P + BS - 1) / BS;
     const int p0 = threadIdx.x * per, p1 = min(P, p0 + per);
+    double* kept = w.kept + 3 * base;
+    double* out = a.out + 3 * (size_t)s * a.cap;
+    constexpr int R = 4;  // up to R parameters per thread stay in registers (one load round)
+    if (per <= R) {
+        double v[R][3];
+        int keep = 0;
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            const int p = min(p0 + u, P - 1);
+            v[u][0] = params[3 * p];
+            v[u][1] = params[3 * p + 1];
+            v[u][2] = params[3 * p + 2];
+        }
+#pragma unroll
+        for (int u = 0; u < R; ++u)
+            keep += p0 + u < p1 && v[u][0] > kCheckPrecision && v[u][1] > kCheckPrecision;
+        int total;
+        int o = block_exclusive_scan<BS>(keep, lds_i, &total);
+        int unsafe = 0;
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            if (p0 + u < p1 && v[u][0] > kCheckPrecision && v[u][1] > kCheckPrecision) {
+                kept[3 * o] = v[u][0];
+                kept[3 * o + 1] = v[u][1];
+                kept[3 * o + 2] = v[u][2];
+                unsafe += !peak_fast_ok(v[u][0], v[u][1], v[u][2]);
+                if (o < a.cap) {
+                    out[3 * o] = v[u][0];
+                    out[3 * o + 1] = v[u][1];
+                    out[3 * o + 2] = v[u][2];
+                }
+                ++o;
+            }
+        }
+        if (unsafe) atomicAdd(&w.unsafe_kept[s], unsafe);
+        if (threadIdx.x == 0) {
+            w.kept_count[s] = total;
+            a.out_count[s] = total;
+        }
+        return;
+    }
     int keep = 0;
     for (int p = p0; p < p1; ++p)
         keep += (params[3 * p] > kCheckPrecision && params[3 * p + 1] > kCheckPrecision);
     int total;
     int o = block_exclusive_scan<BS>(keep, lds_i, &total);
-    double* kept = w.kept + 3 * base;
-    double* out = a.out + 3 * (size_t)s * a.cap;
     for (int p = p0; p < p1; ++p) {
         if (params[3 * p] > kCheckPrecision && params[3 * p + 1] > kCheckPrecision) {
             kept[3 * o] = params[3 * p];
