@@ -189,12 +189,23 @@ int mdg_superposition_vec_device(mdg_ctx* ctx, const double* d_x, size_t n,
  * sequential fold whatever the data. */
 int mdg_ordered_sum(mdg_ctx* ctx, const double* t, size_t n, double acc0, double* out);
 
-/* Test support: the superposition's fast quotient (one Newton step after
- * v_rcp_f64, used when every operand lies in [2^-200, 2^200]) against the IEEE
- * division the reference performs (lorentzian.rs:546-548), on n pseudo-random
- * operand pairs of that range drawn from seed. *mismatches receives the number of
- * pairs whose bits differ (expected 0). */
+/* Test support: the superposition's fast quotients (used when every operand lies
+ * in [2^-200, 2^200]) against the IEEE division the reference performs
+ * (lorentzian.rs:546-548). variant 0 = div_rn (v_rcp_f64 + two Newton steps +
+ * residual correction: the compiler's own expansion without its no-op scaling
+ * wrappers; fit and superposition_vec), variant 1 = div_rn_1nr (one Newton step;
+ * MSE only, not bit-exact). cases 0 = n pseudo-random pairs drawn from seed,
+ * cases 1 = candidates i < n of mdg_division_hard_case (quotients about 2^-53 ulp
+ * from a rounding midpoint). *mismatches receives the pairs whose bits differ,
+ * *tested (may be NULL) the pairs checked. */
+int mdg_check_division(mdg_ctx* ctx, int variant, int cases, uint64_t seed, uint64_t n,
+                       uint64_t* mismatches, uint64_t* tested);
+/* mdg_check_division(ctx, 0, 0, seed, n, mismatches, NULL). */
 int mdg_check_fast_division(mdg_ctx* ctx, uint64_t seed, uint64_t n, uint64_t* mismatches);
+/* Host (no GPU): the i-th constructed near-midpoint operand pair of stream seed
+ * (the generator mdg_check_division runs on the device); MDG_INVALID_ARGUMENT
+ * when candidate i is rejected (its numerator does not fit 53 bits). */
+int mdg_division_hard_case(uint64_t seed, uint64_t i, double* n, double* d);
 
 /* Device synthetic batch: d_x (n, shared axis x_i = xmax - (i*width)/(n-1)) and
  * d_y (b x n): y_s = in-order superposition of mdg_synth_lorentzians(seed0+s) +

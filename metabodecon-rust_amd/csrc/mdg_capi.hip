@@ -57,6 +57,10 @@ struct mdg_ctx {
     Buffer opt[12];
     // replayable pipelines of mdg_deconvolute_batch_device, keyed by every argument
     std::vector<std::pair<std::vector<unsigned char>, hipGraphExec_t>> graphs;
+    // bumped whenever the arena or the chain buffer is reallocated: cached graphs
+    // bake their addresses and layout (ws_B/ws_N strides, counter offsets), so a
+    // new generation drops every one of them before the next replay
+    uint64_t ws_gen = 0, graphs_gen = 0;
     int last_B = 0, last_N = 0;  // shape of the last pipeline run
     bool last_smoothed = false;  // the last run used the moving average
     Workspace w{};
@@ -214,8 +218,23 @@ int ensure_workspace(mdg_ctx* c, int B, int N) {
 
         c->ws_B = nB;
         c->ws_N = nN;
+        ++c->ws_gen;
     }
     return MDG_OK;
+}
+
+// ensure() for the chain smoother buffer, bumping the workspace generation when
+// the buffer moves
+int ensure_chain(mdg_ctx* c, size_t bytes) {
+    const void* old = c->chain.p;
+    const int rc = ensure(c->chain, bytes);
+    if (c->chain.p != old) ++c->ws_gen;
+    return rc;
+}
+
+void drop_graphs(mdg_ctx* c) {
+    for (auto& ge : c->graphs) (void)hipGraphExecDestroy(ge.second);
+    c->graphs.clear();
 }
 
 int validate_common(const mdg_settings* s, size_t n_ignore, const double* ignore) {
@@ -269,7 +288,7 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
         const char* force = std::getenv("MDG_SMOOTH");
         const int P = (int)s->smooth_iterations, ws = (int)s->smooth_window;
         if ((!force || std::string(force) == "chain") && chain_supported(a.B, a.N, P, ws) &&
-            ensure(c->chain, chain_bytes(a.B, a.N, ws, P)) == MDG_OK) {
+            ensure_chain(c, chain_bytes(a.B, a.N, ws, P)) == MDG_OK) {
             const int64_t L = chain_stride_for(a.N, ws);
             char* base = (char*)c->chain.p;
             w.chain_stride = L;
@@ -523,8 +542,7 @@ int mdg_ctx_destroy(mdg_ctx* c) {
             (void)hipEventDestroy(p.b);
         }
         for (auto e : c->free_events) (void)hipEventDestroy(e);
-        for (auto& ge : c->graphs) (void)hipGraphExecDestroy(ge.second);
-        c->graphs.clear();
+        drop_graphs(c);
         for (Buffer& b : c->opt)
             if (b.p) (void)hipFree(b.p);
         for (Buffer* b : {&c->arena, &c->chain, &c->st_x, &c->st_y, &c->st_sb, &c->st_out, &c->st_cnt,
@@ -644,7 +662,11 @@ int run_pipeline_graphed(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     if (rc) return rc;
     if (ma && chain_supported(a.B, a.N, (int)s->smooth_iterations, (int)s->smooth_window) &&
         !(std::getenv("MDG_SMOOTH") && std::string(std::getenv("MDG_SMOOTH")) != "chain"))
-        (void)ensure(c->chain, chain_bytes(a.B, a.N, (int)s->smooth_window, (int)s->smooth_iterations));
+        (void)ensure_chain(c, chain_bytes(a.B, a.N, (int)s->smooth_window, (int)s->smooth_iterations));
+    if (c->graphs_gen != c->ws_gen) {  // buffers moved since these graphs were captured
+        drop_graphs(c);
+        c->graphs_gen = c->ws_gen;
+    }
     std::vector<unsigned char> key(sizeof(BatchArgs) + sizeof(mdg_settings) + 2 * sizeof(void*) +
                                    sizeof(size_t));
     unsigned char* k = key.data();
@@ -848,19 +870,36 @@ int mdg_ordered_sum(mdg_ctx* c, const double* t, size_t n, double acc0, double* 
     return MDG_OK;
 }
 
-int mdg_check_fast_division(mdg_ctx* c, uint64_t seed, uint64_t n, uint64_t* mismatches) {
-    if (!c || !mismatches || n > (uint64_t)INT64_MAX) return MDG_INVALID_ARGUMENT;
+int mdg_check_division(mdg_ctx* c, int variant, int cases, uint64_t seed, uint64_t n,
+                       uint64_t* mismatches, uint64_t* tested) {
+    if (!c || !mismatches || n > (uint64_t)INT64_MAX || (variant != 0 && variant != 1) ||
+        (cases != 0 && cases != 1))
+        return MDG_INVALID_ARGUMENT;
     std::lock_guard<std::mutex> g(c->mu);
     HIPCHK(hipSetDevice(c->device));
     hipStream_t st = c->stream;
     int rc;
     if ((rc = ensure(c->st_flag, 256))) return rc;
-    HIPCHK(hipMemsetAsync(c->st_flag.p, 0, 8, st));
-    launch_division_check(seed, (long long)n, (unsigned long long*)c->st_flag.p, st);
+    HIPCHK(hipMemsetAsync(c->st_flag.p, 0, 16, st));
+    launch_division_check(variant, cases, seed, (long long)n, (unsigned long long*)c->st_flag.p, st);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(mismatches, c->st_flag.p, 8, hipMemcpyDeviceToHost, st));
+    uint64_t res[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(res, c->st_flag.p, 16, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    *mismatches = res[0];
+    if (tested) *tested = res[1];
     return MDG_OK;
+}
+
+int mdg_check_fast_division(mdg_ctx* c, uint64_t seed, uint64_t n, uint64_t* mismatches) {
+    return mdg_check_division(c, 0, 0, seed, n, mismatches, nullptr);
+}
+
+int mdg_division_hard_case(uint64_t seed, uint64_t i, double* n, double* d) {
+    if (!n || !d) return MDG_INVALID_ARGUMENT;
+    bool ok = false;
+    division_hard_case(seed, i, n, d, &ok);
+    return ok ? MDG_OK : MDG_INVALID_ARGUMENT;
 }
 
 int mdg_synth_batch_device(mdg_ctx* c, size_t b, size_t n, double xmax, double width,

@@ -31,19 +31,37 @@ __device__ __forceinline__ double lorentz(double x, double sfhw, double hw2, dou
 }
 
 // Correctly rounded binary64 quotient without the div_scale/div_fmas/div_fixup
-// wrappers. hipcc expands `n / d` to: div_scale x2, rcp, two Newton steps
-// (fma, fma), q0 = n*r, rem = fma(-d, q0, n), div_fmas(rem, r, q0), div_fixup.
-// When div_scale does not scale (|n|, |d| in [2^-200, 2^203], quotient normal)
-// div_fmas is a plain fma and div_fixup returns its input. This sequence also
-// stops after ONE Newton step: the reciprocal then differs from the two-step one
-// in about a third of the cases (by an ulp), but the final residual correction
-// q0 + fma(-d, q0, n) * r gives the quotient of `/` bit for bit -- checked on
-// 4.4e12 random operand pairs over the whole range, mantissas random or with
-// long runs of ones / zeros (tools/ubench/div_check.hip), and by every parity
-// test. 9 instead of 11 issue slots plus the quarter-rate rcp per evaluation.
-// Callers use it only for spectra whose flags prove the operand ranges
-// (peak_fast_ok + x_ok below); everything else takes `/`.
-__device__ __forceinline__ double div_rn_fast(double n, double d) {
+// wrappers. hipcc expands `n / d` (LLVM's AMDGPU f64 fdiv lowering) to
+//   s = div_scale(d), r0 = rcp(s), e0 = fma(-s, r0, 1), r1 = fma(r0, e0, r0),
+//   e1 = fma(-s, r1, 1), r2 = fma(r1, e1, r1), t = div_scale(n), q0 = t * r2,
+//   rem = fma(-s, q0, t), q = div_fmas(rem, r2, q0), div_fixup(q, d, n).
+// When |n|, |d| lie in [2^-200, 2^200] div_scale returns its operand unchanged
+// and clears VCC (no exponent gap >= 768, no denormal operand or quotient, n
+// not below 2^-969), div_fmas is then a plain fma, and div_fixup returns its
+// input for the resulting normal, finite quotient. div_rn is that sequence
+// minus the three no-op wrappers -- the same operations on the same operands
+// in the same order -- so it returns the bits of `/` by construction, not by
+// measurement. Callers use it only for spectra whose flags prove
+// the operand ranges (peak_fast_ok + x_ok below); everything else takes `/`.
+__device__ __forceinline__ double div_rn(double n, double d) {
+    const double r0 = __builtin_amdgcn_rcp(d);
+    const double e0 = __builtin_fma(-d, r0, 1.0);
+    const double r1 = __builtin_fma(r0, e0, r0);
+    const double e1 = __builtin_fma(-d, r1, 1.0);
+    const double r2 = __builtin_fma(r1, e1, r1);
+    const double q0 = n * r2;
+    const double rem = __builtin_fma(-d, q0, n);
+    return __builtin_fma(rem, r2, q0);
+}
+
+// The same without the second Newton step. r1 is within about an ulp of 1/d
+// (it differs from r2 in a third of the cases), so the corrected quotient is off
+// by at most ~2^-52 ulp before its last rounding: it equals `/` except for
+// quotients within that distance of a rounding midpoint. Such operand pairs
+// exist (mdg_check_division's constructed cases hit them), so this variant is
+// NOT bit-exact and is used only by the MSE superposition, whose result the
+// tests compare at 1e-12 relative (one such term moves it by ~1e-16).
+__device__ __forceinline__ double div_rn_1nr(double n, double d) {
     const double r0 = __builtin_amdgcn_rcp(d);
     const double e0 = __builtin_fma(-d, r0, 1.0);
     const double r1 = __builtin_fma(r0, e0, r0);
@@ -66,7 +84,15 @@ template <bool FAST>
 __device__ __forceinline__ double lorentz_t(double x, double sfhw, double hw2, double maxp) {
     const double d = x - maxp;
     const double den = hw2 + d * d;
-    return FAST ? div_rn_fast(sfhw, den) : sfhw / den;
+    return FAST ? div_rn(sfhw, den) : sfhw / den;
+}
+
+// MSE only (see div_rn_1nr): not bit-exact, within the MSE's tolerance
+template <bool FAST>
+__device__ __forceinline__ double lorentz_mse(double x, double sfhw, double hw2, double maxp) {
+    const double d = x - maxp;
+    const double den = hw2 + d * d;
+    return FAST ? div_rn_1nr(sfhw, den) : sfhw / den;
 }
 
 // In-order superposition (lorentzian.rs:606-611) of P wave-uniform Lorentzians.
@@ -143,7 +169,7 @@ __device__ __forceinline__ void sup_group_n(const double (&x)[NPT], double (&acc
                                             const_f64_ptr next, bool load_next) {
     double e[NPT][kSupGP];
 #pragma unroll
-    for (int i = 0; i < NPT; ++i) e[i][0] = lorentz_t<FAST>(x[i], c[0], c[1], c[2]);
+    for (int i = 0; i < NPT; ++i) e[i][0] = lorentz_mse<FAST>(x[i], c[0], c[1], c[2]);
     __builtin_amdgcn_sched_barrier(0);
     if (load_next) {
 #pragma unroll
@@ -152,7 +178,7 @@ __device__ __forceinline__ void sup_group_n(const double (&x)[NPT], double (&acc
 #pragma unroll
     for (int k = 1; k < kSupGP; ++k)
 #pragma unroll
-        for (int i = 0; i < NPT; ++i) e[i][k] = lorentz_t<FAST>(x[i], c[3 * k], c[3 * k + 1], c[3 * k + 2]);
+        for (int i = 0; i < NPT; ++i) e[i][k] = lorentz_mse<FAST>(x[i], c[3 * k], c[3 * k + 1], c[3 * k + 2]);
 #pragma unroll
     for (int i = 0; i < NPT; ++i)
 #pragma unroll
@@ -186,7 +212,7 @@ __device__ __forceinline__ void superpose_n(const double (&x)[NPT], const double
     for (int j = kSupGP * G; j < P; ++j) {
         const_f64_ptr L = params + 3 * j;
 #pragma unroll
-        for (int i = 0; i < NPT; ++i) acc[i] += lorentz_t<FAST>(x[i], L[0], L[1], L[2]);
+        for (int i = 0; i < NPT; ++i) acc[i] += lorentz_mse<FAST>(x[i], L[0], L[1], L[2]);
     }
 }
 
@@ -2011,20 +2037,42 @@ __device__ __forceinline__ double fast_range_operand(unsigned long long h, bool 
     const int e = (int)((h >> 12) % 401) - 200;
     return __longlong_as_double((long long)(((unsigned long long)(e + 1023) << 52) | m));
 }
-__global__ void k_division_check(unsigned long long seed, long long n, unsigned long long* bad) {
-    unsigned long long nb = 0;
+// variant 0: div_rn (fit, superposition_vec), 1: div_rn_1nr (MSE only).
+// cases 0: random pairs, 1: constructed near-midpoint pairs (division_hard_case).
+// out[0] += mismatches, out[1] += pairs tested.
+template <int VARIANT>
+__device__ __forceinline__ double div_variant(double n, double d) {
+    return VARIANT == 0 ? div_rn(n, d) : div_rn_1nr(n, d);
+}
+template <int VARIANT>
+__global__ void k_division_check(unsigned long long seed, long long n, int cases,
+                                 unsigned long long* out) {
+    unsigned long long nb = 0, nt = 0;
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (long long)gridDim.x * blockDim.x) {
-        const unsigned long long h1 = mix64(seed ^ (2 * i)), h2 = mix64(seed ^ (2 * i + 1));
-        const bool runs = (h1 >> 63) & (h2 >> 63);
-        const double num = fast_range_operand(h1, runs), d = fast_range_operand(h2, runs);
-        nb += __double_as_longlong(div_rn_fast(num, d)) != __double_as_longlong(num / d);
+        double num, d;
+        if (cases == 0) {
+            const unsigned long long h1 = mix64(seed ^ (2 * i)), h2 = mix64(seed ^ (2 * i + 1));
+            const bool runs = (h1 >> 63) & (h2 >> 63);
+            num = fast_range_operand(h1, runs);
+            d = fast_range_operand(h2, runs);
+        } else {
+            bool ok;
+            division_hard_case(seed, (uint64_t)i, &num, &d, &ok);
+            if (!ok) continue;
+        }
+        ++nt;
+        nb += __double_as_longlong(div_variant<VARIANT>(num, d)) != __double_as_longlong(num / d);
     }
-    if (nb) atomicAdd(bad, nb);
+    if (nb) atomicAdd(out, nb);
+    atomicAdd(out + 1, nt);
 }
-void launch_division_check(unsigned long long seed, long long n, unsigned long long* bad,
-                           hipStream_t st) {
-    hipLaunchKernelGGL(k_division_check, dim3(4096), dim3(256), 0, st, seed, n, bad);
+void launch_division_check(int variant, int cases, unsigned long long seed, long long n,
+                           unsigned long long* out, hipStream_t st) {
+    if (variant == 0)
+        hipLaunchKernelGGL(k_division_check<0>, dim3(4096), dim3(256), 0, st, seed, n, cases, out);
+    else
+        hipLaunchKernelGGL(k_division_check<1>, dim3(4096), dim3(256), 0, st, seed, n, cases, out);
 }
 
 template <int BS>
@@ -2326,7 +2374,9 @@ __device__ __forceinline__ double fold16_eval_fast(double& acc, double ei, doubl
         "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:5 row_mask:0xf bank_mask:0xf\n"
         "v_fma_f64 %[r], %[r], %[t], %[r]\n"
         "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:6 row_mask:0xf bank_mask:0xf\n"
+        "v_fma_f64 %[t], -%[den], %[r], 1.0\n"
         "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:7 row_mask:0xf bank_mask:0xf\n"
+        "v_fma_f64 %[r], %[r], %[t], %[r]\n"
         "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
         "v_mul_f64 %[q], %[sf], %[r]\n"
         "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:9 row_mask:0xf bank_mask:0xf\n"
@@ -2379,8 +2429,12 @@ __device__ __forceinline__ void fold2_eval_fast(double& accA, double& accB, doub
         "v_fma_f64 %[rB], %[rB], %[tB], %[rB]\n"
         "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:6 row_mask:0xf bank_mask:0xf\n"
         "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:6 row_mask:0xf bank_mask:0xf\n"
+        "v_fma_f64 %[tA], -%[denA], %[rA], 1.0\n"
+        "v_fma_f64 %[tB], -%[denB], %[rB], 1.0\n"
         "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:7 row_mask:0xf bank_mask:0xf\n"
         "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:7 row_mask:0xf bank_mask:0xf\n"
+        "v_fma_f64 %[rA], %[rA], %[tA], %[rA]\n"
+        "v_fma_f64 %[rB], %[rB], %[tB], %[rB]\n"
         "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
         "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
         "v_mul_f64 %[qA], %[sf], %[rA]\n"

@@ -122,9 +122,11 @@ void launch_mse(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t 
 void launch_mse_final(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st);
 // windowed left fold of n <= kWinMax non-negative terms (test support)
 void launch_ordered_sum(const double* t, int n, double acc0, double* out, hipStream_t st);
-// div_rn_fast against IEEE '/' on n pseudo-random FAST-range pairs (test support)
-void launch_division_check(unsigned long long seed, long long n, unsigned long long* bad,
-                           hipStream_t st);
+// fast-range division variants against IEEE '/' (test support): variant 0 div_rn,
+// 1 div_rn_1nr; cases 0 random pairs, 1 constructed near-midpoint pairs;
+// out[0] += mismatches, out[1] += pairs tested
+void launch_division_check(int variant, int cases, unsigned long long seed, long long n,
+                           unsigned long long* out, hipStream_t st);
 void launch_superposition_vec(const double* x, int64_t n, const double* params, int P,
                               double* out, int* flag, hipStream_t st);
 void launch_synth(double* x, double* y, int64_t n, int B, double xmax, double width,

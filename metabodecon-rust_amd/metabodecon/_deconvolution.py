@@ -299,7 +299,10 @@ class Deconvolution:
 # Deconvoluter (bindings/deconvoluter.rs:17-165, deconvoluter.rs:118-905)
 # =====================================================================================
 class Deconvoluter:
-    MAX_IGNORE = 16
+    # merged ignore regions the engine takes per call (kMaxIgnore, mdg_common.hpp);
+    # the reference has no limit -- add_ignore_region refuses the 65th disjoint
+    # region with InvalidIgnoreRegion instead of failing later at deconvolute time
+    MAX_IGNORE = 64
 
     def __init__(self):
         self._s = nat.default_settings()
@@ -359,6 +362,10 @@ class Deconvoluter:
         if st:
             raise exc.InvalidIgnoreRegion(
                 f"ignore region boundaries [{a}, {b}] are invalid")
+        if n.value > self.MAX_IGNORE:
+            raise exc.InvalidIgnoreRegion(
+                f"ignore region [{a}, {b}] would make {n.value} disjoint regions; the GPU "
+                f"engine takes at most {self.MAX_IGNORE}")
         self._ignore = [(float(buf[2 * i]), float(buf[2 * i + 1])) for i in range(n.value)]
 
     def clear_ignore_regions(self) -> None:
@@ -417,6 +424,58 @@ class Deconvoluter:
             for k, i in enumerate(idx):
                 results[i] = (int(status[k]), out[k, : int(counts[k])].copy(), float(mse[k]))
         return results
+
+    def _run_device(self, spectra: list[Spectrum]):
+        """Device-resident variant of ``_run`` for the multi-GPU path: the block's
+        inputs go to HBM once, ``mdg_deconvolute_batch_device`` runs one batched
+        pipeline per distinct length on this process's GPU, and the results stay
+        in HBM as torch tensors for the RCCL gather:
+        (status int32[b], counts int32[b], mse f64[b], tables f64[b, cap, 3]),
+        with cap = the largest count of the block (>= 1)."""
+        import torch
+        dev_index = nat.default_device() if self.device is None else self.device
+        dev = torch.device("cuda", dev_index)
+        b_all = len(spectra)
+        by_n: dict[int, list[int]] = {}
+        for i, sp in enumerate(spectra):
+            if not isinstance(sp, Spectrum):
+                raise TypeError("expected metabodecon.Spectrum")
+            by_n.setdefault(len(sp), []).append(i)
+        ign = self._ignore_array()
+        ctx = nat.context(dev_index)
+        status = torch.zeros(b_all, dtype=torch.int32, device=dev)
+        counts = torch.zeros(b_all, dtype=torch.int32, device=dev)
+        mse = torch.zeros(b_all, dtype=torch.float64, device=dev)
+        parts = []
+        for n, idx in by_n.items():
+            b = len(idx)
+            x = torch.from_numpy(np.stack([spectra[i].chemical_shifts for i in idx])).to(dev)
+            y = torch.from_numpy(np.stack([spectra[i].intensities for i in idx])).to(dev)
+            sb = torch.tensor([spectra[i].signal_boundaries for i in idx], dtype=torch.float64,
+                              device=dev)
+            cap = n // 2 + 2
+            out = torch.empty((b, cap, 3), dtype=torch.float64, device=dev)
+            cnt = torch.zeros(b, dtype=torch.int32, device=dev)
+            m = torch.zeros(b, dtype=torch.float64, device=dev)
+            st = torch.zeros(b, dtype=torch.int32, device=dev)
+            torch.cuda.synchronize(dev)  # inputs written on torch's stream
+            with ctx.lock:
+                rc = nat.lib().mdg_deconvolute_batch_device(
+                    ctx.handle, b, n, x.data_ptr(), n, y.data_ptr(), n, sb.data_ptr(),
+                    ctypes.byref(self._s), nat.ptr(ign) if ign.size else None, ign.size // 2,
+                    out.data_ptr(), cap, cnt.data_ptr(), m.data_ptr(), st.data_ptr())
+                if rc:
+                    raise exc.UnexpectedError(f"GPU engine failure: {nat.strerror(rc)}")
+                ctx.synchronize()
+            ii = torch.tensor(idx, dtype=torch.int64, device=dev)
+            status[ii], counts[ii], mse[ii] = st, cnt, m
+            parts.append((ii, out))
+        width = max(1, int(counts.max().item())) if b_all else 1
+        tables = torch.zeros((b_all, width, 3), dtype=torch.float64, device=dev)
+        for ii, out in parts:
+            w = min(width, out.shape[1])
+            tables[ii, :w] = out[:, :w]
+        return status, counts, mse, tables
 
     def _collect(self, results) -> list[Deconvolution]:
         out = []

@@ -45,6 +45,7 @@ EXPORTS = [
     "mdg_superposition_vec", "mdg_superposition_vec_device", "mdg_synth_batch_device",
     "mdg_ctx_last_peaks", "mdg_ctx_last_smoothed", "mdg_ctx_set_profiling_mask",
     "mdg_optimize_settings", "mdg_ordered_sum", "mdg_check_fast_division",
+    "mdg_check_division", "mdg_division_hard_case",
 ]
 
 
@@ -149,6 +150,9 @@ def _declare(L):
                                         _sz, sp, _dp]
     L.mdg_ordered_sum.argtypes = [_vp, _dp, _sz, ctypes.c_double, _dp]
     L.mdg_check_fast_division.argtypes = [_vp, ctypes.c_uint64, ctypes.c_uint64, _u64p]
+    L.mdg_check_division.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
+                                     ctypes.c_uint64, _u64p, _u64p]
+    L.mdg_division_hard_case.argtypes = [ctypes.c_uint64, ctypes.c_uint64, _dp, _dp]
     L.mdg_synth_batch_device.argtypes = [_vp, _sz, _sz, ctypes.c_double, ctypes.c_double,
                                          ctypes.c_uint64, _sz, ctypes.c_double, ctypes.c_double,
                                          ctypes.c_double, _vp, _vp]
@@ -255,9 +259,12 @@ _ctx_lock = threading.Lock()
 
 
 def default_device() -> int:
-    env = os.environ.get("MDGPU_DEVICE")
-    if env is not None:
-        return int(env)
+    """MDGPU_DEVICE if set; else LOCAL_RANK (one process per GPU under torchrun,
+    so every rank runs on its own device); else 0."""
+    for var in ("MDGPU_DEVICE", "LOCAL_RANK"):
+        env = os.environ.get(var)
+        if env is not None:
+            return int(env)
     return 0
 
 

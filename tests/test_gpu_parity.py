@@ -412,18 +412,37 @@ def test_ordered_sum_window_fold(ctx):
     assert nat.lib().mdg_ordered_sum(ctx.handle, nat.ptr(bad), 2, -0.0, ctypes.byref(out)) != 0
 
 
+def _division_check(ctx, variant, cases, seed, n):
+    bad, tested = ctypes.c_uint64(1), ctypes.c_uint64(0)
+    rc = nat.lib().mdg_check_division(ctx.handle, variant, cases, seed, n, ctypes.byref(bad),
+                                      ctypes.byref(tested))
+    assert rc == 0, nat.strerror(rc)
+    return bad.value, tested.value
+
+
 @pytest.mark.parametrize("seed", [0x9E3779B97F4A7C15, 20261016])
 def test_fast_division_matches_ieee(ctx, seed):
-    """div_rn_fast (reciprocal + one Newton step + one residual correction) is the
-    divider of every FAST-path Lorentzian evaluation. It must round exactly like
-    IEEE '/' on operands in [2^-200, 2^200] (the range the fast flags gate): 2^33
-    seeded pairs per seed, three quarters with uniform mantissas, a quarter with
-    trailing-ones / single-bit mantissas (the usual worst cases for Newton
-    quotients); exponents uniform in [-200, 200]."""
-    bad = ctypes.c_uint64(1)
-    rc = nat.lib().mdg_check_fast_division(ctx.handle, seed, 1 << 33, ctypes.byref(bad))
-    assert rc == 0, nat.strerror(rc)
-    assert bad.value == 0
+    """div_rn (reciprocal + two Newton steps + residual correction: the compiler's
+    own '/' expansion minus its no-op scaling wrappers) is the divider of every
+    FAST-path evaluation in the fit and superposition_vec. On operands in
+    [2^-200, 2^200] (the range the fast flags gate) it must round exactly like
+    IEEE '/': 2^32 seeded random pairs per seed (a quarter with trailing-ones /
+    single-bit mantissas), and 2^31 candidates of the constructed near-midpoint
+    family (quotients 2^-53 ulp from a tie -- the only inputs on which a
+    not-quite-correct reciprocal can misround)."""
+    bad, tested = _division_check(ctx, 0, 0, seed, 1 << 32)
+    assert tested == 1 << 32 and bad == 0
+    bad, tested = _division_check(ctx, 0, 1, seed, 1 << 31)
+    assert tested > (1 << 31) // 3 and bad == 0, (bad, tested)
+
+
+def test_one_newton_division_is_not_exact_on_hard_cases(ctx):
+    """Power check of the hard-case family: the one-Newton-step quotient (kept for
+    the MSE only, which the tests compare at 1e-12 relative) does misround on
+    constructed near-midpoint pairs, while it almost never does on random pairs
+    -- the reason it was retired from the bit-exact paths."""
+    bad_hard, tested = _division_check(ctx, 1, 1, 5, 1 << 28)
+    assert tested > 0 and bad_hard > 0, (bad_hard, tested)
 
 
 def test_device_graph_replay(ctx, monkeypatch):
@@ -542,3 +561,83 @@ def test_jcampdx_and_serde_inputs_through_the_device(tmp_path):
     sf = d.params[:, 0] / hw
     assert np.array_equal(r.params, np.stack([sf * hw, hw * hw, d.params[:, 2]], axis=1))
     assert r.mse == d.mse
+
+
+def test_graph_cache_survives_workspace_growth(ctx):
+    """A cached pipeline graph bakes the workspace layout. Growing the workspace
+    (a larger batch, then a longer spectrum on a fresh context) must drop the cached
+    graphs, so B=1 -> B=2 -> B=1 -> longer N -> B=1 on the same tensors keeps
+    giving the oracle's results (stale graph after reallocation)."""
+    torch = pytest.importorskip("torch")
+    c = nat.Context(0)
+    try:
+        names = ["sim_04", "sim_09"]
+        cases = [load_case(nm) for nm in names]
+        n = cases[0][1].size
+        dev = "cuda"
+        x = torch.from_numpy(np.stack([cc[0] for cc in cases])).to(dev)
+        y = torch.from_numpy(np.stack([cc[1] for cc in cases])).to(dev)
+        sb = torch.tensor([cc[2] for cc in cases], dtype=torch.float64, device=dev)
+        cap = n // 2 + 2
+        out = torch.zeros((2, cap, 3), dtype=torch.float64, device=dev)
+        cnt = torch.zeros(2, dtype=torch.int32, device=dev)
+        mse = torch.zeros(2, dtype=torch.float64, device=dev)
+        status = torch.zeros(2, dtype=torch.int32, device=dev)
+        s = nat.default_settings()
+        refs = [oracle.deconvolute(cc[0], cc[1], cc[2], cc[3]) for cc in cases]
+
+        def run(b):
+            out.zero_(); mse.zero_()
+            torch.cuda.synchronize()
+            rc = nat.lib().mdg_deconvolute_batch_device(
+                c.handle, b, n, x.data_ptr(), n, y.data_ptr(), n, sb.data_ptr(), ctypes.byref(s),
+                None, 0, out.data_ptr(), cap, cnt.data_ptr(), mse.data_ptr(), status.data_ptr())
+            assert rc == 0, nat.strerror(rc)
+            c.synchronize()
+            for k in range(b):
+                o = refs[k]
+                assert int(status[k]) == o.status == 0
+                assert np.array_equal(out[k, : int(cnt[k])].cpu().numpy(), o.params)
+                assert abs(float(mse[k]) - o.mse) <= MSE_RTOL * abs(o.mse), (b, k)
+
+        for b in (1, 2, 1, 2, 1):
+            run(b)
+        # a longer spectrum through the host API grows the arena under the cached graphs
+        bx, by, bsb, bst, _ = load_case("blood_03")
+        gpu_batch(c, bx, by[None, :], [bsb], bst)
+        run(1)
+        run(2)
+    finally:
+        c.close()
+
+
+def test_par_deconvolute_spectra_rccl_world1():
+    """The multi-GPU product path itself (metabodecon.distributed) on the box's GPU:
+    nccl (RCCL) process group of world size 1, the shard run device-resident by
+    Deconvoluter._run_device, tables gathered in HBM; results equal the goldens,
+    and an injected failure raises the first error in order."""
+    import socket
+    import torch
+    import torch.distributed as dist
+    import metabodecon as md
+    from metabodecon import exceptions as mexc
+    from metabodecon.distributed import par_deconvolute_spectra
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        spectra = md.Spectrum.read_bruker_set(os.path.join(GOLDEN, "bruker", "blood"), 10, 10,
+                                              (-2.2, 11.8))[:6]
+        decs = par_deconvolute_spectra(md.Deconvoluter(), spectra)
+        for k, d in enumerate(decs):
+            g = np.load(os.path.join(GOLDEN, "expected", f"blood_{k + 1:02d}.npz"))
+            assert np.array_equal(d.params, g["params"])
+            assert abs(d.mse - float(g["mse"])) <= MSE_RTOL * abs(float(g["mse"]))
+        flat = md.Spectrum(spectra[0].chemical_shifts, np.full(len(spectra[0]), 5.0),
+                           (-2.2, 11.8))
+        with pytest.raises(mexc.NoPeaksDetected):
+            par_deconvolute_spectra(md.Deconvoluter(), [spectra[1], flat, spectra[2]])
+    finally:
+        dist.destroy_process_group()

@@ -174,3 +174,42 @@ def test_no_cpu_fallback_without_device():
     s = Spectrum(x, np.ones(4096), (-2.2, 11.8))
     with pytest.raises(nat.DeviceUnavailableError):
         Deconvoluter().deconvolute_spectrum(s)
+
+
+def test_division_hard_cases_lie_next_to_rounding_midpoints():
+    """mdg_division_hard_case (the generator mdg_check_division runs on the
+    device) yields operand pairs whose exact quotient is within 2^-53 ulp of a
+    rounding midpoint (checked in exact rational arithmetic), inside the
+    fast-division range [2^-200, 2^200]."""
+    import ctypes
+    from fractions import Fraction
+    n, d = ctypes.c_double(), ctypes.c_double()
+    valid = 0
+    for i in range(3000):
+        if nat.lib().mdg_division_hard_case(11, i, ctypes.byref(n), ctypes.byref(d)):
+            continue
+        valid += 1
+        for v in (n.value, d.value):
+            assert 2.0 ** -200 <= abs(v) <= 2.0 ** 200
+        q = Fraction(n.value) / Fraction(d.value)
+        ulp = Fraction(2) ** (math.frexp(float(q))[1] - 53)
+        t = q / ulp  # significand scaled to [2^52, 2^53)
+        dist = abs(t - math.floor(t) - Fraction(1, 2))
+        assert 0 < dist <= Fraction(1, 2 ** 53), (i, float(dist))
+    assert valid > 1000
+
+
+def test_ignore_region_engine_limit_is_reported_at_add_time():
+    """The engine takes up to Deconvoluter.MAX_IGNORE (64) merged regions per call;
+    the next disjoint region is refused by add_ignore_region itself with the
+    reference's InvalidIgnoreRegion kind, leaving the list unchanged."""
+    d = Deconvoluter()
+    for k in range(Deconvoluter.MAX_IGNORE):
+        d.add_ignore_region((0.1 * k, 0.1 * k + 0.05))
+    assert len(d.ignore_regions) == Deconvoluter.MAX_IGNORE
+    before = d.ignore_regions
+    with pytest.raises(exceptions.InvalidIgnoreRegion):
+        d.add_ignore_region((100.0, 100.5))
+    assert d.ignore_regions == before
+    d.add_ignore_region((0.0, 0.12))  # merges with existing ones: still accepted
+    assert len(d.ignore_regions) == Deconvoluter.MAX_IGNORE - 1
