@@ -1,21 +1,30 @@
 """Benchmark: metabodecon Deconvoluter::deconvolute_spectrum on MI355X.
 
 Metric (BASELINE.json): spectra/s for 131072-point spectra with ~2k peaks.
-Workload (configs[1]): synthetic 131072-point f64 spectrum with 2048 injected
-Lorentzians (jittered grid, SURVEY 8d recipe, generated on the device), full
-default Deconvoluter (MA 3x3 smoothing, noise-score selection thr 5, analytical
-fit 10 iterations, MSE). One step = one deconvolution of a batch of --batch
-spectra per GPU (default 1 = configs[1]; --batch 256 = configs[2]); inputs are
-resident in HBM before timing. With --gpus N>1 (torchrun, one process per GPU)
-every rank deconvolutes its own spectra (weak scaling, no data-path
-collective) and the step ends with the RCCL all_gather of the Lorentzian
-tables (the path's only exchange).
+Headline workload (configs[1]): synthetic 131072-point f64 spectra with 2048
+injected Lorentzians (jittered grid, SURVEY 8d recipe, generated on the device),
+full default Deconvoluter (MA 3x3 smoothing, noise-score selection thr 5,
+analytical fit 10 iterations, MSE). One step = one deconvolution of one distinct
+spectrum (--batch 1); inputs are resident in HBM before timing.
 
-Three passes over the same resident inputs: (1) a short profiled pass that
-times every pipeline stage with hipEvents (stages_ms_per_step); (2) the timed
-region, K steps with no events (each step replays the pipeline's cached
-hipGraph) -> value / ms_per_step; (3) the same K steps with hipEvents around the
-dominant stage's launches only -> roofline.avg_launch_ms / achieved.
+Steps are submitted round-robin to --streams engine contexts (one HIP stream and
+one HBM workspace each), the way concurrent callers of the reference's
+`par_deconvolute_spectrum` (Deconvoluter is Send + Sync, deconvoluter.rs:913-917)
+would use one GPU: spectrum k+1's sequential smoother overlaps spectrum k's fit
+and MSE. `value` is that stream's throughput; `latency_ms` is one spectrum alone
+on an idle GPU (one context, steps back to back).
+
+--gpus N: without WORLD_SIZE in the environment, bench.py starts N rank processes
+itself (torch.distributed.run as a child process, before any GPU call) and exits
+with its status. Each rank deconvolutes its own stream of spectra on its own GPU
+(weak scaling, no data-path collective) and the timed region ends with the RCCL
+all_gather of every rank's Lorentzian tables (the path's only exchange).
+
+On one GPU (rank 0, N=1) the same run also measures the other BASELINE configs
+(`configs` block, each with its own roofline): configs[0] blood_01, configs[2]
+256 x 131072 batch, configs[3] 4096 x 65536 batch (one GPU's worth of the
+8-GPU job), configs[4] the 16 blood spectra end to end through the Python
+surface, and the CPU baselines (the C oracle on all host cores, median of 5).
 
 Prints ONE JSON line (rank 0).
 """
@@ -26,6 +35,9 @@ import ctypes
 import glob
 import json
 import os
+import socket
+import statistics
+import subprocess
 import sys
 import time
 
@@ -40,6 +52,9 @@ FLOPS_PER_EVAL = 5        # sub, mul, add, div, accumulate (div counted once)
 CLOCK_GHZ = 2.35          # shader clock measured by tools/ubench/eval_cost.hip (cycles / wall ns)
 CHAIN_FLOOR_CYC = 8.34    # two dependent v_fmac_f64 per smoother tick, one wave (eval_cost.hip)
 WORK_STAGES = ["fit_superposition", "mse_superposition", "smooth", "detect"]
+SB = (11.8, -2.2)         # signal boundaries of the synthetic configs (ppm, Spectrum order)
+BLOOD = os.path.join(ROOT, "tests", "golden", "bruker", "blood")
+CPU_REPS = 5
 
 
 def parse():
@@ -47,19 +62,42 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=1, help="spectra per GPU per step")
+    ap.add_argument("--batch", type=int, default=1, help="spectra per step (headline)")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="engine contexts the steps are spread over (1 = back to back)")
     ap.add_argument("--n", type=int, default=131072)
     ap.add_argument("--peaks", type=int, default=2048)
     ap.add_argument("--cap", type=int, default=4096)
-    ap.add_argument("--cpu-sample", type=int, default=64,
-                    help="spectra in the all-cores CPU sample (~10-15 core-seconds)")
-    ap.add_argument("--cpu-single", type=int, default=8, help="spectra in the 1-core sample")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = len(sched_getaffinity)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-configs", action="store_true", help="headline only")
+    ap.add_argument("--configs", default="0,2,3,4", help="secondary configs to measure")
     ap.add_argument("--no-profile", action="store_true", help="no per-stage HIP events")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: exercise the launcher, rendezvous and gather (gloo)")
     return ap.parse_args()
 
 
+# ------------------------------------------------------------------ launcher
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(args) -> int:
+    """--gpus N without a torchrun environment: start N ranks as a child
+    torch.distributed.run (never an exec of this process; nothing here has touched
+    the GPU) and return its exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+# ------------------------------------------------------------------ helpers
 def sbi_len(x0, step, sb0, sb1):
     import math
     a = max(0, math.floor((sb0 - x0) / step))
@@ -77,202 +115,416 @@ def _cpu_model():
     return "unknown"
 
 
-def cpu_baseline(args, threads):
-    """The oracle (C restatement, -O3, no FMA) timed on this host's cores."""
-    import oracle
-    from metabodecon import _native as nat
-    n, peaks, S = args.n, args.peaks, args.cpu_sample
-    i = np.arange(n, dtype=np.float64)
-    x = 14.8 - (i * 20.0) / (float(n) - 1.0)
-    ys = np.empty((S, n))
-    for s in range(S):
-        p = np.empty((peaks, 3))
-        nat.lib().mdg_synth_lorentzians(s, peaks, -1.8, 11.4, nat.ptr(p))
-        noise = np.empty(n)
-        nat.lib().mdg_synth_noise(s, n, 1.0e3, nat.ptr(noise))
-        ys[s] = oracle.superposition_vec(x, p, threads=threads) + noise
-    sb = np.array([[11.8, -2.2]] * S)
-    # single core: deconvolute_spectrum semantics, one spectrum after another
-    S1 = max(1, min(args.cpu_single, S))
-    t = time.perf_counter()
-    for s in range(S1):
-        assert oracle.deconvolute(x, ys[s], (11.8, -2.2), threads=1).status == 0
-    single = S1 / (time.perf_counter() - t)
-    # all cores: par_deconvolute_spectra semantics (one spectrum per thread)
-    t = time.perf_counter()
-    status, counts, _, _ = oracle.deconvolute_batch(x, ys, sb, threads=threads, cap=args.cap)
-    wall = time.perf_counter() - t
-    assert not status.any()
-    return {
-        "value": S / wall, "unit": "spectra/s", "cores": threads, "kind": "port",
-        "sample": (f"{S} synthetic {n}-pt/{peaks}-peak spectra (seeds 0..{S - 1}), oracle "
-                   f"C restatement -O3 -ffp-contract=off, {threads} threads over spectra "
-                   f"({wall:.2f} s wall, {wall * threads:.1f} core-s); single core {single:.3f} "
-                   f"spectra/s over {S1} spectra; host {_cpu_model()}"),
-        "single_core_value": single,
-    }
+def host_threads(args) -> int:
+    if args.cpu_threads:
+        return args.cpu_threads
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
 
 
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
-    from metabodecon import _native as nat
+def median_rate(fn, units, reps=CPU_REPS):
+    """units / median wall time of `reps` runs of fn() (one untimed warm-up)."""
+    fn()
+    ts = []
+    for _ in range(reps):
+        t = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t)
+    return units / statistics.median(ts), ts
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    ctx = nat.Context(local)
-    stream = torch.cuda.current_stream(dev)
-    ctx.set_stream(stream.cuda_stream)
 
-    B, n = args.batch, args.n
-    x = torch.empty(n, dtype=torch.float64, device=dev)
-    y = torch.empty((B, n), dtype=torch.float64, device=dev)
-    seed0 = rank * B
-    rc = nat.lib().mdg_synth_batch_device(ctx.handle, B, n, 14.8, 20.0, seed0, args.peaks, -1.8,
-                                          11.4, 1.0e3, x.data_ptr(), y.data_ptr())
-    assert rc == 0, nat.strerror(rc)
-    sb = torch.tensor([[11.8, -2.2]] * B, dtype=torch.float64, device=dev)
-    cap = args.cap
-    out = torch.zeros((B, cap, 3), dtype=torch.float64, device=dev)
-    cnt = torch.zeros(B, dtype=torch.int32, device=dev)
-    mse = torch.zeros(B, dtype=torch.float64, device=dev)
-    status = torch.zeros(B, dtype=torch.int32, device=dev)
-    settings = nat.default_settings()
-    if world > 1:
-        g_out = torch.empty((world * B, cap, 3), dtype=torch.float64, device=dev)
-        g_cnt = torch.empty(world * B, dtype=torch.int32, device=dev)
+def pmc_traffic(tag, stage):
+    """HBM bytes per launch of `stage` from the newest committed PMC summary for
+    this workload tag (tools/pmc_summary.py), or (None, None)."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{tag}.json")),
+                       reverse=True):
+        try:
+            return (json.load(open(path))["stages"][stage]["hbm_bytes_per_launch"],
+                    os.path.relpath(path, ROOT))
+        except (OSError, KeyError, ValueError):
+            continue
+    return None, None
 
-    def step():
-        rc = nat.lib().mdg_deconvolute_batch_device(
-            ctx.handle, B, n, x.data_ptr(), 0, y.data_ptr(), n, sb.data_ptr(),
-            ctypes.byref(settings), None, 0, out.data_ptr(), cap, cnt.data_ptr(), mse.data_ptr(),
-            status.data_ptr())
-        if rc:
-            raise RuntimeError(nat.strerror(rc))
-        if world > 1:  # RCCL gather of the Lorentzian tables (weak-scaling exchange)
-            dist.all_gather_into_tensor(g_cnt, cnt)
-            dist.all_gather_into_tensor(g_out, out)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    assert int(status.abs().max()) == 0, status
-    profile = not args.no_profile
-    # (1) profiled pass before the timed region: every stage bracketed by hipEvents
-    prof_steps = min(args.steps, 5)
-    stages = {}
-    if profile:
-        ctx.reset_stage_times()
-        ctx.set_profiling(True)
-        for _ in range(prof_steps):
-            step()
-        torch.cuda.synchronize()
-        stages = ctx.stage_times()
-        ctx.set_profiling(False)
-    dom = max(WORK_STAGES, key=lambda k: stages[k][0]) if profile else None
-    # (2) timed region: no events, so each step replays the pipeline's cached hipGraph
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    # (3) roofline pass: the same K steps again with hipEvents around the dominant
-    # stage's launches only (on the context stream they run on)
-    dom_times = {}
-    if profile:
-        ctx.reset_stage_times()
-        ctx.set_profiling_stages([dom])
-        for _ in range(args.steps):
-            step()
-        torch.cuda.synchronize()
-        dom_times = ctx.stage_times()
-        ctx.set_profiling(False)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t)
+def roofline_from_stages(ctx, stages, work, tag, n):
+    """Roofline of the dominant stage of a profiled pass: `stages` = stage ->
+    (ms, launches) from hipEvents around every launch on the context stream;
+    `work` = stage -> (bound, algorithmic amount per launch, unit); kernel names
+    come from the engine (mdg_ctx_stage_kernel)."""
+    dom = max((k for k in WORK_STAGES if k in work and stages.get(k, (0, 0))[1]),
+              key=lambda k: stages[k][0])
+    ms_total, launches = stages[dom]
+    avg_s = ms_total / launches / 1e3
+    bound, amount, unit = work[dom]
+    if unit == "TFLOP/s":
+        achieved, peak = amount / avg_s / 1e12, FP64_PEAK_TFLOPS
+    else:
+        achieved, peak = amount / avg_s / 1e9, HBM_PEAK_GBS
+    traffic, src = pmc_traffic(tag, dom)
+    limiter = {
+        "smooth": ("sequential running sums (moving_average.rs:69-80): 2 dependent f64 adds "
+                   "per point per pass, one CU per pass; not bandwidth-bound"),
+        "fit_superposition": "FP64 VALU issue (IEEE division sequence per evaluation)",
+        "mse_superposition": "FP64 VALU issue (division sequence per evaluation)",
+        "detect": "launch latency / L2",
+    }[dom]
+    r = {"bound": bound, "kernel": ctx.stage_kernels().get(dom), "stage": dom,
+         "achieved": achieved, "peak": peak, "unit": unit, "frac": achieved / peak,
+         "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": src,
+         "avg_launch_ms": avg_s * 1e3, "launches": launches, "algorithmic_per_launch": amount,
+         "limiter": limiter}
+    if dom == "smooth":
+        # one pass is N ticks of two dependent FP64 adds on one wave; passes pipeline on
+        # separate CUs, so a launch lasts about one pass (tools/ubench/eval_cost.hip floor)
+        cyc = avg_s * CLOCK_GHZ * 1e9 / n
+        r["issue_roofline"] = {"unit": "cycles/tick", "achieved": cyc, "floor": CHAIN_FLOOR_CYC,
+                               "frac": CHAIN_FLOOR_CYC / cyc, "clock_ghz": CLOCK_GHZ,
+                               "source": "tools/ubench/eval_cost.hip ('smoother tick: 2 fmac SGPR')"}
+    return r
 
-    # ---- algorithmic work of the launches (per spectrum, from this rank's results)
-    counts = cnt.cpu().numpy()
+
+def work_per_launch(nat, ctx, B, n, counts, settings, x0, x1, sb):
+    """Algorithmic flops/bytes per launch of each work stage for the last batch run
+    (SURVEY 8d): 5 flops per Lorentzian evaluation; fit 3*P_sel^2 evaluations per
+    spectrum and iteration; MSE L*P_kept evaluations + 3L; smoother 16N bytes;
+    detection 8N + 24 ceil(N/64) bytes."""
     P_sel = []
     for s in range(B):
         c = ctypes.c_size_t(0)
         nat.lib().mdg_ctx_last_peaks(ctx.handle, s, 1, None, None, None, 0, ctypes.byref(c))
         P_sel.append(c.value)
-    xh0, xh1 = 14.8, 14.8 - 20.0 / (n - 1.0)
-    L = sbi_len(xh0, xh1 - xh0, 11.8, -2.2)
-    fit_flops = sum(FLOPS_PER_EVAL * 3 * p * p for p in P_sel)           # per launch (1 iteration)
-    mse_flops = sum((FLOPS_PER_EVAL * int(k) + 3) * L for k in counts)     # per launch
-    smooth_bytes = B * 16 * n  # per launch: y read once, smoothed row written once (passes fused on chip)
-    detect_bytes = B * (8 * n + 3 * ((n + 63) // 64) * 8)
-    ws, iters = settings.smooth_window, settings.smooth_iterations
-    smooth_kernel = (f"k_smooth_chain<{ws}>" if 2 <= ws <= 8 and B * iters <= 2048 and n >= 400
-                     else f"k_smooth_waves<{ws}>" if B > 21 else f"k_smooth_pipe<{ws}>")
-    fit_kernel = ("k_fit_sup_tf" if B <= 2 else "k_fit_sup_dpp" if B <= 8 else "k_fit_sup")
+    L = sbi_len(x0, x1 - x0, sb[0], sb[1])
     work = {
-        "fit_superposition": ("fp64", fit_flops, "TFLOP/s", fit_kernel),
-        "mse_superposition": ("fp64", mse_flops, "TFLOP/s", "k_mse_partial_n<256, 2>"),
-        "smooth": ("hbm", smooth_bytes, "GB/s", smooth_kernel),
-        "detect": ("hbm", detect_bytes, "GB/s", "k_flags+k_peaks_count+k_peaks_write"),
+        "fit_superposition": ("fp64", sum(FLOPS_PER_EVAL * 3 * p * p for p in P_sel), "TFLOP/s"),
+        "mse_superposition": ("fp64", sum((FLOPS_PER_EVAL * int(k) + 3) * L for k in counts),
+                              "TFLOP/s"),
+        "detect": ("hbm", B * (8 * n + 3 * ((n + 63) // 64) * 8), "GB/s"),
     }
-    limiter = {
-        "smooth": ("sequential running sums (moving_average.rs:69-80): 2 dependent f64 adds "
-                   "per point per pass, one CU per pass; not bandwidth-bound"),
-        "fit_superposition": "FP64 VALU issue (IEEE division sequence per evaluation)",
-        "mse_superposition": "FP64 VALU issue (IEEE division sequence per evaluation)",
-        "detect": "launch latency (three short kernels)",
-    }
-    stage_ms_step = {k: v[0] / prof_steps for k, v in stages.items() if v[1]}
-    roofline = None
-    if profile:
-        bound, amount, unit, kname = work[dom]
-        ms_total, launches = dom_times[dom]
-        avg_s = ms_total / launches / 1e3
-        if unit == "TFLOP/s":
-            achieved = amount / avg_s / 1e12
-            peak = FP64_PEAK_TFLOPS
-        else:
-            achieved = amount / avg_s / 1e9
-            peak = HBM_PEAK_GBS
-        # HBM bytes per launch of this stage from the committed PMC passes of the same
-        # batch size (tools/pmc_summary.py; FETCH_SIZE doubled per the gfx950 note)
-        traffic, traffic_src = None, None
-        pmc = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_b{B}.json")))
-        if pmc:
-            try:
-                traffic = json.load(open(pmc[-1]))["stages"][dom]["hbm_bytes_per_launch"]
-                traffic_src = os.path.relpath(pmc[-1], ROOT)
-            except (OSError, KeyError, ValueError):
-                traffic = None
-        roofline = {"bound": bound, "kernel": kname, "stage": dom, "achieved": achieved,
-                    "peak": peak, "unit": unit, "frac": achieved / peak, "traffic": traffic,
-                    "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
-                    "avg_launch_ms": avg_s * 1e3, "algorithmic_per_launch": amount,
-                    "limiter": limiter[dom]}
-        if dom == "smooth":
-            # the bound that does apply: one pass is N ticks of two dependent FP64 adds
-            # on one wave, passes pipelined on separate CUs, so a launch lasts about one
-            # pass. Floor: two dependent VOP2 v_fmac_f64 on SGPR operands per tick,
-            # 8.34 cycles (tools/ubench/eval_cost.hip), at the 2.35 GHz measured there.
-            cyc = avg_s * CLOCK_GHZ * 1e9 / n
-            roofline["issue_roofline"] = {
-                "unit": "cycles/tick", "achieved": cyc, "floor": CHAIN_FLOOR_CYC,
-                "frac": CHAIN_FLOOR_CYC / cyc, "clock_ghz": CLOCK_GHZ,
-                "source": "tools/ubench/eval_cost.hip ('smoother tick: 2 fmac SGPR')"}
+    if settings.smoother == 1:
+        work["smooth"] = ("hbm", B * 16 * n, "GB/s")
+    return work, P_sel
 
-    total_spectra = world * B * args.steps
-    value = total_spectra / elapsed
+
+# ------------------------------------------------------------------ device runs
+class Slot:
+    """One engine context on its own stream with its own input/output rows."""
+
+    def __init__(self, nat, torch, dev, B, n, cap):
+        self.ctx = nat.Context(dev.index)
+        self.stream = torch.cuda.Stream(dev)
+        self.ctx.set_stream(self.stream.cuda_stream)
+        self.y = torch.empty((B, n), dtype=torch.float64, device=dev)
+        # one contiguous result record [out | mse | cnt | status]: a step's results
+        # leave the slot in one copy
+        f64 = B * cap * 3 + B + B  # the int32 pair packs into B doubles
+        self.rec = torch.zeros(f64, dtype=torch.float64, device=dev)
+        self.out = self.rec[: B * cap * 3].view(B, cap, 3)
+        self.mse = self.rec[B * cap * 3: B * cap * 3 + B]
+        ints = self.rec[B * cap * 3 + B:].view(torch.int32)
+        self.cnt = ints[:B]
+        self.status = ints[B:]
+
+
+def run_batch(nat, slot, B, n, x, y, sb, settings, cap, x_stride=0):
+    rc = nat.lib().mdg_deconvolute_batch_device(
+        slot.ctx.handle, B, n, x.data_ptr(), x_stride, y.data_ptr(), n, sb.data_ptr(),
+        ctypes.byref(settings), None, 0, slot.out.data_ptr(), cap, slot.cnt.data_ptr(),
+        slot.mse.data_ptr(), slot.status.data_ptr())
+    if rc:
+        raise RuntimeError(nat.strerror(rc))
+
+
+def profiled_pass(nat, torch, slot, fn, steps):
+    """`steps` calls of fn() with hipEvents around every stage launch (the engine
+    runs un-graphed while timing) -> stage -> (ms, launches)."""
+    slot.ctx.reset_stage_times()
+    slot.ctx.set_profiling(True)
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    st = slot.ctx.stage_times()
+    slot.ctx.set_profiling(False)
+    return st
+
+
+def synth_device(nat, ctx, torch, B, n, peaks, seed0, dev, x=None):
+    x = torch.empty(n, dtype=torch.float64, device=dev) if x is None else x
+    y = torch.empty((B, n), dtype=torch.float64, device=dev)
+    rc = nat.lib().mdg_synth_batch_device(ctx.handle, B, n, 14.8, 20.0, seed0, peaks, -1.8, 11.4,
+                                          1.0e3, x.data_ptr(), y.data_ptr())
+    assert rc == 0, nat.strerror(rc)
+    ctx.synchronize()
+    return x, y
+
+
+def headline(args, nat, torch, dist, dev, rank, world):
+    """configs[1] stream: args.steps distinct spectra over args.streams contexts."""
+    B, n, cap, K, W, S = args.batch, args.n, args.cap, args.steps, args.warmup, args.streams
+    settings = nat.default_settings()
+    slots = [Slot(nat, torch, dev, B, n, cap) for _ in range(S)]
+    R = max(K, W, 1)  # distinct spectra (B each), seeds rank*R*B ...
+    x, Y = synth_device(nat, slots[0].ctx, torch, R * B, n, args.peaks, rank * R * B, dev)
+    Y = Y.view(R, B, n)
+    sb = torch.tensor([SB] * B, dtype=torch.float64, device=dev)
+    res = torch.zeros((K, slots[0].rec.numel()), dtype=torch.float64, device=dev)
+
+    def submit(k, j, nslots):
+        s = slots[k % nslots]
+        with torch.cuda.stream(s.stream):
+            s.y.copy_(Y[j])
+            run_batch(nat, s, B, n, x, s.y, sb, settings, cap)
+            if k < K:
+                res[k].copy_(s.rec)
+
+    for k in range(max(W, S)):  # every context captures its graph
+        submit(K + k, k % R, S)
+    torch.cuda.synchronize()
+    # latency: one context, one spectrum at a time on an otherwise idle GPU
+    lat = []
+    for k in range(min(K, 10)):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        submit(K, k % R, 1)
+        torch.cuda.synchronize()
+        lat.append(time.perf_counter() - t)
+    # timed region
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(K):
+        submit(k, k % R, S)
+    torch.cuda.synchronize()
+    if world > 1:  # RCCL gather of every rank's result records (the weak-scaling exchange)
+        g_res = torch.empty((world * K, res.shape[1]), dtype=torch.float64, device=dev)
+        dist.all_gather_into_tensor(g_res, res)
+        torch.cuda.synchronize()
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    ints = res[:, B * cap * 3 + B:].contiguous().view(torch.int32)
+    res_cnt, res_status = ints[:, :B], ints[:, B:]
+    assert int(res_status.abs().max()) == 0, res_status
+    # profiled pass (stage times, roofline) on slot 0, outside the timed region
+    s0 = slots[0]
+    prof = {}
+    prof_steps = min(K, 5)
+    if not args.no_profile:
+        with torch.cuda.stream(s0.stream):
+            s0.y.copy_(Y[0])
+        prof = profiled_pass(nat, torch, s0, lambda: run_batch(nat, s0, B, n, x, s0.y, sb,
+                                                              settings, cap), prof_steps)
+    s0.ctx.synchronize()
+    counts = s0.cnt.cpu().numpy()
+    work, P_sel = work_per_launch(nat, s0.ctx, B, n, counts, settings, 14.8,
+                                  14.8 - 20.0 / (n - 1.0), SB)
+    roof = (roofline_from_stages(s0.ctx, prof, work, f"b{B}", n) if prof else None)
+    kept = res_cnt.cpu().numpy()
+    out = {
+        "elapsed": elapsed, "spectra": world * K * B, "latency_ms": 1e3 * statistics.median(lat),
+        "roofline": roof,
+        "stages_ms_per_spectrum": {k: v[0] / prof_steps / B for k, v in prof.items() if v[1]},
+        "selected_peaks": P_sel[:4], "kept_peaks": [int(c) for c in kept[:4, 0]],
+    }
+    for s in slots:
+        s.ctx.close()
+    return out
+
+
+def batch_config(args, nat, torch, dev, B, n, peaks, steps, warmup, tag):
+    """One resident batch of B synthetic spectra per step (configs[2], configs[3])."""
+    settings = nat.default_settings()
+    slot = Slot(nat, torch, dev, B, n, args.cap)
+    x, y = synth_device(nat, slot.ctx, torch, B, n, peaks, 0, dev)
+    sb = torch.tensor([SB] * B, dtype=torch.float64, device=dev)
+
+    def step():
+        with torch.cuda.stream(slot.stream):
+            run_batch(nat, slot, B, n, x, y, sb, settings, args.cap)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    assert int(slot.status.abs().max()) == 0
+    prof = profiled_pass(nat, torch, slot, step, 1) if not args.no_profile else {}
+    slot.ctx.synchronize()
+    counts = slot.cnt.cpu().numpy()
+    work, P_sel = work_per_launch(nat, slot.ctx, B, n, counts, settings, 14.8,
+                                  14.8 - 20.0 / (n - 1.0), SB)
+    roof = roofline_from_stages(slot.ctx, prof, work, tag, n) if prof else None
+    r = {"value": B * steps / elapsed, "unit": "spectra/s", "ms_per_step": elapsed / steps * 1e3,
+         "steps": steps, "warmup": warmup, "spectra_per_step": B, "n_points": n,
+         "injected_peaks": peaks, "selected_peaks_mean": float(np.mean(P_sel)),
+         "kept_peaks_mean": float(np.mean(counts)), "roofline": roof,
+         "stages_ms_per_step": {k: v[0] for k, v in prof.items() if v[1]}}
+    slot.ctx.close()
+    del x, y
+    torch.cuda.empty_cache()
+    return r
+
+
+def blood_gpu(args, nat, torch, dev):
+    """configs[0] on the GPU: blood_01 (Bruker 10/10, sb (-2.2, 11.8)), one spectrum
+    per step back to back, host buffers (PCIe inside) through the Python surface."""
+    import metabodecon as md
+    sp = md.Spectrum.read_bruker(os.path.join(BLOOD, "blood_01"), 10, 10, (-2.2, 11.8))
+    dec = md.Deconvoluter()
+    dec.device = dev.index
+    for _ in range(2):
+        d = dec.deconvolute_spectrum(sp)
+    steps = 20
+    t = time.perf_counter()
+    for _ in range(steps):
+        d = dec.deconvolute_spectrum(sp)
+    el = time.perf_counter() - t
+    return sp, {"value": steps / el, "unit": "spectra/s", "ms_per_step": el / steps * 1e3,
+                "steps": steps, "kept_peaks": len(d.lorentzians), "mse": d.mse,
+                "path": "Deconvoluter.deconvolute_spectrum, host buffers (H2D/D2H inside)"}
+
+
+def bruker_set(args, nat, torch, dev):
+    """configs[4]: the 16 blood spectra, Spectrum.read_bruker_set ->
+    Deconvoluter.par_deconvolute_spectra (one batched call, host buffers)."""
+    import metabodecon as md
+    t = time.perf_counter()
+    spectra = md.Spectrum.read_bruker_set(BLOOD, 10, 10, (-2.2, 11.8))
+    read_s = time.perf_counter() - t
+    dec = md.Deconvoluter()
+    dec.device = dev.index
+    for _ in range(2):
+        res = dec.par_deconvolute_spectra(spectra)
+    steps = 10
+    t = time.perf_counter()
+    for _ in range(steps):
+        res = dec.par_deconvolute_spectra(spectra)
+    el = time.perf_counter() - t
+    ctx = nat.context(dev.index)
+    ctx.reset_stage_times()
+    ctx.set_profiling(True)
+    dec.par_deconvolute_spectra(spectra)
+    prof = ctx.stage_times()
+    ctx.set_profiling(False)
+    n = len(spectra[0])
+    x = spectra[0].chemical_shifts
+    counts = [len(d.lorentzians) for d in res]
+    work, P_sel = work_per_launch(nat, ctx, len(spectra), n, counts, dec.settings, x[0], x[1],
+                                  spectra[0].signal_boundaries)
+    roof = roofline_from_stages(ctx, prof, work, "blood16", n)
+    return spectra, {"value": len(spectra) * steps / el, "unit": "spectra/s",
+                     "ms_per_step": el / steps * 1e3, "steps": steps, "spectra_per_step":
+                     len(spectra), "read_s": read_s, "kept_peaks": counts, "roofline": roof,
+                     "path": "Spectrum.read_bruker_set + Deconvoluter.par_deconvolute_spectra, "
+                             "host buffers (PCIe inside the timed region)"}
+
+
+# ------------------------------------------------------------------ CPU baselines
+def cpu_baselines(args, threads, Yh, x, blood_sp, blood_set, c3):
+    """The oracle (C restatement, -O3, no FMA) timed on this host: median of 5."""
+    import oracle
+    n = x.size
+    out = {"threads": threads, "nproc": os.cpu_count(), "cpu": _cpu_model(), "reps": CPU_REPS}
+    # configs[1]/[2]: synthetic spectra, one per worker thread (par_deconvolute_spectra)
+    S = min(Yh.shape[0], 2 * threads)
+    sb = np.array([SB] * S)
+    rate, ts = median_rate(lambda: oracle.deconvolute_batch(x, Yh[:S], sb, threads=threads,
+                                                            cap=args.cap), S)
+    single, ts1 = median_rate(lambda: oracle.deconvolute(x, Yh[0], SB, threads=1), 1)
+    out["synthetic"] = {
+        "value": rate, "unit": "spectra/s", "cores": threads, "kind": "port",
+        "sample": (f"{S} synthetic {n}-pt/{args.peaks}-peak spectra per rep over {threads} "
+                   f"threads (one spectrum per thread at a time), median of {CPU_REPS} reps "
+                   f"({statistics.median(ts):.2f} s); oracle C restatement -O3 "
+                   f"-ffp-contract=off; host {_cpu_model()}, nproc {os.cpu_count()}"),
+        "single_core_value": single}
+    if blood_sp is not None:  # configs[0]: benches/deconvoluter.rs:8-30
+        bx, by = blood_sp.chemical_shifts, blood_sp.intensities
+        bsb = blood_sp.signal_boundaries
+        seq, _ = median_rate(lambda: oracle.deconvolute(bx, by, bsb, threads=1), 1)
+        par, _ = median_rate(lambda: oracle.deconvolute(bx, by, bsb, threads=threads), 1)
+        out["blood_01"] = {"deconvolute_spectrum": seq, "par_deconvolute_spectrum": par,
+                           "unit": "spectra/s", "par_threads": threads}
+    if blood_set is not None:  # configs[4]: par_deconvolute_spectra over the 16 spectra
+        X = np.stack([s.chemical_shifts for s in blood_set])
+        Yb = np.stack([s.intensities for s in blood_set])
+        bsb = np.array([s.signal_boundaries for s in blood_set])
+        outer = min(threads, len(blood_set))
+        inner = max(1, threads // outer)
+        r, _ = median_rate(lambda: oracle.deconvolute_batch(X, Yb, bsb, threads=outer,
+                                                            inner_threads=inner,
+                                                            cap=X.shape[1] // 2 + 2),
+                           len(blood_set))
+        out["blood_set"] = {"value": r, "unit": "spectra/s",
+                            "threads": f"{outer} over spectra x {inner} per spectrum"}
+    if c3 is not None:  # configs[3] shape: 65536 points, 1024 peaks
+        x3, Y3 = c3
+        S3 = min(Y3.shape[0], 2 * threads)
+        r, _ = median_rate(lambda: oracle.deconvolute_batch(x3, Y3[:S3], np.array([SB] * S3),
+                                                            threads=threads, cap=args.cap), S3)
+        out["synthetic_65536"] = {"value": r, "unit": "spectra/s", "spectra_per_rep": S3}
+    return out
+
+
+# ------------------------------------------------------------------ main
+def dry_run(args, world, rank):
+    """No GPU: the launcher, the rendezvous, the max-over-ranks timing and the
+    table gather run exactly as on the GPU path, with gloo and zero tables."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+    t0 = time.perf_counter()
+    tab = torch.zeros((args.steps, 1, 4, 3), dtype=torch.float64)
+    if world > 1:
+        g = torch.empty((world * args.steps, 1, 4, 3), dtype=torch.float64)
+        dist.all_gather_into_tensor(g, tab)
+        dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": "spectra/s (128k pts, ~2k peaks)", "value": None,
+                          "unit": "spectra/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "dry_run": True, "max_elapsed_s": float(el)}),
+              flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if "WORLD_SIZE" in os.environ and args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
+    if args.dry_run:
+        return dry_run(args, world, rank)
+
+    import torch
+    import torch.distributed as dist
+    from metabodecon import _native as nat
+
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    h = headline(args, nat, torch, dist, dev, rank, world)
+    value = h["spectra"] / h["elapsed"]
+    B = args.batch
     line = {
         "metric": "spectra/s (128k pts, ~2k peaks)",
         "value": value,
@@ -280,30 +532,71 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
+        "ms_per_step": h["elapsed"] / args.steps * 1e3,
+        "latency_ms": h["latency_ms"],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (device-generated, seeds rank*B..rank*B+B-1)",
-        "config": {"workload": ("configs[1]: synthetic 131072-pt f64 spectrum, 2048 injected "
-                                "Lorentzians, default Deconvoluter" if B == 1 else
-                                f"configs[2]-shape: batch of {B} synthetic spectra per GPU"),
-                   "n_points": n, "injected_peaks": args.peaks, "spectra_per_gpu_per_step": B,
-                   "selected_peaks": P_sel[:4], "kept_peaks": [int(c) for c in counts[:4]],
+        "data": "synthetic (device-generated, distinct seeds per step and rank)",
+        "config": {"workload": ("configs[1]: synthetic 131072-pt f64 spectra, 2048 injected "
+                                "Lorentzians, default Deconvoluter, one distinct spectrum per "
+                                "step" if B == 1 else
+                                f"batch of {B} synthetic spectra per GPU per step"),
+                   "n_points": args.n, "injected_peaks": args.peaks,
+                   "spectra_per_gpu_per_step": B, "streams": args.streams,
+                   "selected_peaks": h["selected_peaks"], "kept_peaks": h["kept_peaks"],
                    "parallelism": f"dp{world}" if world > 1 else "single"},
-        "roofline": roofline,
-        "stages_ms_per_step": stage_ms_step,
-        "stages_source": f"separate profiled pass of {prof_steps} steps (every stage with hipEvents)",
+        "roofline": h["roofline"],
+        "stages_ms_per_spectrum": h["stages_ms_per_spectrum"],
+        "stages_source": "separate profiled pass on one context (hipEvents around every stage)",
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        line["cpu_baseline"] = cpu_baseline(args, threads)
-        line["speedup_vs_cpu"] = value / line["cpu_baseline"]["value"]
+    if rank == 0 and world == 1:
+        torch.cuda.synchronize()
+        want = set() if args.no_configs else {int(c) for c in args.configs.split(",") if c}
+        configs = {}
+        blood_sp = blood_set = c3 = None
+        if 0 in want:
+            blood_sp, configs["configs[0]"] = blood_gpu(args, nat, torch, dev)
+        if 2 in want:
+            configs["configs[2]"] = batch_config(args, nat, torch, dev, 256, 131072, 2048, 3, 1,
+                                                 "b256")
+            configs["configs[2]"]["workload"] = ("256 synthetic 131072-pt/2048-peak spectra per "
+                                                 "step, one batched pipeline, resident in HBM")
+        if 3 in want:
+            configs["configs[3]"] = batch_config(args, nat, torch, dev, 4096, 65536, 1024, 2, 1,
+                                                 "b4096_n65536")
+            configs["configs[3]"]["workload"] = (
+                "4096 synthetic 65536-pt/1024-peak spectra (hw x2) per step on ONE GPU (the "
+                "8-GPU job's whole batch; sharded it is 512 per rank)")
+        if 4 in want:
+            blood_set, configs["configs[4]"] = bruker_set(args, nat, torch, dev)
+        if configs:
+            line["configs"] = configs
+        if not args.no_cpu_baseline:
+            threads = host_threads(args)
+            # the CPU sample: the same generator (device, bit-identical to the host one)
+            ctx = nat.Context(local)
+            xd, yd = synth_device(nat, ctx, torch, 2 * threads, args.n, args.peaks, 0, dev)
+            xh, Yh = xd.cpu().numpy(), yd.cpu().numpy()
+            if 3 in want:
+                x3, y3 = synth_device(nat, ctx, torch, 2 * threads, 65536, 1024, 0, dev)
+                c3 = (x3.cpu().numpy(), y3.cpu().numpy())
+            ctx.close()
+            del xd, yd
+            cb = cpu_baselines(args, threads, Yh, xh, blood_sp, blood_set, c3)
+            line["cpu_baseline"] = cb["synthetic"]
+            line["cpu_baselines"] = {k: v for k, v in cb.items() if k != "synthetic"}
+            line["speedup_vs_cpu"] = value / cb["synthetic"]["value"]
+            for key, ref in (("configs[0]", ("blood_01", "par_deconvolute_spectrum")),
+                             ("configs[2]", ("synthetic", "value")),
+                             ("configs[3]", ("synthetic_65536", "value")),
+                             ("configs[4]", ("blood_set", "value"))):
+                if key in configs and ref[0] in cb:
+                    configs[key]["speedup_vs_cpu"] = configs[key]["value"] / cb[ref[0]][ref[1]]
     if rank == 0:
         print(json.dumps(line), flush=True)
-    ctx.close()
     if world > 1:
         dist.destroy_process_group()
 

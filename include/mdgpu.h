@@ -120,6 +120,11 @@ int mdg_ctx_set_profiling(mdg_ctx* ctx, int enable);
 int mdg_ctx_set_profiling_mask(mdg_ctx* ctx, uint32_t mask);
 int mdg_ctx_stage_times(mdg_ctx* ctx, double* times_ms, uint64_t* launches, int n_stages);
 int mdg_ctx_reset_stage_times(mdg_ctx* ctx);
+/* Name of the kernel(s) the last pipeline run on this context launched for `stage`
+ * (same numbering; "+"-joined when a stage launches several, NULL when the stage did
+ * not run). The string is static. Lets benchmarks label measurements with what the
+ * engine actually dispatched. */
+int mdg_ctx_stage_kernel(mdg_ctx* ctx, int stage, const char** name);
 
 /* ---- hot path: host buffers ------------------------------------------------
  * x, y: n chemical shifts / intensities of a validated Spectrum

@@ -56,7 +56,13 @@ struct mdg_ctx {
     const int32_t* ovr_fit = nullptr;
     Buffer opt[12];
     // replayable pipelines of mdg_deconvolute_batch_device, keyed by every argument
-    std::vector<std::pair<std::vector<unsigned char>, hipGraphExec_t>> graphs;
+    struct CachedGraph {
+        std::vector<unsigned char> key;
+        hipGraphExec_t exec;
+        const char* kernels[kStages];  // kernel names per stage of the captured pipeline
+    };
+    std::vector<CachedGraph> graphs;
+    const char* stage_kernel[kStages] = {};  // kernels the last pipeline launched, per stage
     // bumped whenever the arena or the chain buffer is reallocated: cached graphs
     // bake their addresses and layout (ws_B/ws_N strides, counter offsets), so a
     // new generation drops every one of them before the next replay
@@ -164,7 +170,7 @@ int ensure_workspace(mdg_ctx* c, int B, int N) {
         const size_t o_params = take(Bs * capD * 24), o_kept = take(Bs * capD * 24);
         const size_t o_st = take(Bs * capD * 48);
         const size_t o_rx = take(Bs * capD * 24), o_ry = take(Bs * capD * 24), o_ratio = take(Bs * capD * 24);
-        const size_t o_msep = take(Bs * 1024 * 8);
+        const size_t o_msep = take(Bs * kMseMaxParts * 8);
         const size_t o_sfr = take(Bs * 16);
         const size_t o_sbi = take(Bs * 16);
         const size_t o_ig = take(Bs * 2 * kMaxIgnore * 8);
@@ -233,7 +239,7 @@ int ensure_chain(mdg_ctx* c, size_t bytes) {
 }
 
 void drop_graphs(mdg_ctx* c) {
-    for (auto& ge : c->graphs) (void)hipGraphExecDestroy(ge.second);
+    for (auto& ge : c->graphs) (void)hipGraphExecDestroy(ge.exec);
     c->graphs.clear();
 }
 
@@ -260,6 +266,8 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     hipStream_t st = c->stream;
     const bool ma = s->smoother == MDG_SMOOTH_MOVING_AVERAGE;
     c->last_smoothed = ma;
+    for (auto& k : c->stage_kernel) k = nullptr;
+    const char** kn = c->stage_kernel;
     if (ma) {
         w.smooth_ptr = w.smooth;
         w.smooth_stride = a.N;
@@ -301,6 +309,7 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     {
         StageTimer t(c, ST_PREP);
         launch_prep(a, w, st);
+        kn[ST_PREP] = "k_prep";
     }
     if (ma) {
         if ((int64_t)(s->smooth_window / 2) > a.N) {
@@ -310,40 +319,43 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
             HIPCHK(hipStreamSynchronize(st));
         } else {
             StageTimer t(c, ST_SMOOTH);
-            launch_smooth(a, w, (int)s->smooth_iterations, (int)s->smooth_window, st);
+            kn[ST_SMOOTH] = launch_smooth(a, w, (int)s->smooth_iterations, (int)s->smooth_window, st);
         }
     }
     {
         StageTimer t(c, ST_DETECT);
         launch_flags(a, w, st);
-        launch_peaks(a, w, det_only, st);
+        kn[ST_DETECT] = launch_peaks(a, w, det_only, st);
     }
     {
         StageTimer t(c, ST_SELECT);
         if (!det_only) launch_scores(a, w, st);
-        launch_select(a, w, det_only, s->threshold, st);
+        kn[ST_SELECT] = launch_select(a, w, det_only, s->threshold, st);
     }
     {
         StageTimer t(c, ST_FIT_INIT);
         launch_fit_init(a, w, gupd, st);
+        kn[ST_FIT_INIT] = "k_fit_init";
     }
     for (uint32_t it = 0; it < s->fit_iterations; ++it) {
         {
             StageTimer t(c, ST_FIT_SUP);
-            launch_fit_sup(a, w, gfit, (int)it, st);
+            kn[ST_FIT_SUP] = launch_fit_sup(a, w, gfit, (int)it, st);
         }
         if (!fused) {
             StageTimer t(c, ST_FIT_UPDATE);
             launch_fit_update(a, w, gupd, (int)it, st);
+            kn[ST_FIT_UPDATE] = "k_fit_update";
         }
     }
     {
         StageTimer t(c, ST_RETAIN);
         launch_retain(a, w, st);
+        kn[ST_RETAIN] = "k_retain<1024>";
     }
     {
         StageTimer t(c, ST_MSE);
-        launch_mse(a, w, nparts, st);
+        kn[ST_MSE] = launch_mse(a, w, nparts, st);
     }
     {
         StageTimer t(c, ST_MSE_REDUCE);
@@ -610,6 +622,13 @@ int mdg_ctx_reset_stage_times(mdg_ctx* c) {
     return MDG_OK;
 }
 
+int mdg_ctx_stage_kernel(mdg_ctx* c, int stage, const char** name) {
+    if (!c || !name || stage < 0 || stage >= kStages) return MDG_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> g(c->mu);
+    *name = c->stage_kernel[stage];
+    return MDG_OK;
+}
+
 int mdg_ctx_last_peaks(mdg_ctx* c, size_t spectrum, int which, int32_t* left, int32_t* center,
                        int32_t* right, size_t cap, size_t* count) {
     if (!c || !count || (which != 0 && which != 1)) return MDG_INVALID_ARGUMENT;
@@ -681,7 +700,10 @@ int run_pipeline_graphed(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     std::memcpy(k, &c->chain.bytes, sizeof(size_t));
     hipGraphExec_t exec = nullptr;
     for (auto& ge : c->graphs)
-        if (ge.first == key) exec = ge.second;
+        if (ge.key == key) {
+            exec = ge.exec;
+            std::memcpy(c->stage_kernel, ge.kernels, sizeof(ge.kernels));
+        }
     if (!exec) {
         hipStream_t user = c->stream;
         c->stream = c->own;
@@ -698,10 +720,14 @@ int run_pipeline_graphed(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
         (void)hipGraphDestroy(graph);
         if (ei != hipSuccess) return hip_fail(ei);
         if (c->graphs.size() >= 8) {
-            (void)hipGraphExecDestroy(c->graphs.front().second);
+            (void)hipGraphExecDestroy(c->graphs.front().exec);
             c->graphs.erase(c->graphs.begin());
         }
-        c->graphs.emplace_back(std::move(key), exec);
+        mdg_ctx::CachedGraph cg;
+        cg.key = std::move(key);
+        cg.exec = exec;
+        std::memcpy(cg.kernels, c->stage_kernel, sizeof(cg.kernels));
+        c->graphs.push_back(std::move(cg));
     } else {
         // host-side state run_pipeline would have set
         c->last_B = a.B;

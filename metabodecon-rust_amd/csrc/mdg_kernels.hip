@@ -816,6 +816,9 @@ static_assert(kChainG % 8 == 0 && kChainCB % kChainG == 0, "checkpoint groups ti
 constexpr int kChainPrefetch = MDG_CHAIN_PF;  // input blocks touched into the scalar cache ahead
 constexpr int kChainL2Ahead = 64;        // pass-0 input blocks pulled into L2 ahead
 constexpr unsigned kChainSpins = 1u << 22;
+// largest chain grid (workgroups, padded to 8 spectra x passes) launched with
+// whole-CU workgroups: 8 spectra x 3 passes at the defaults, 232 CUs left free
+constexpr int kChainExclMax = 24;
 
 int64_t chain_stride_for(int N, int ws) {
     const int64_t span = (int64_t)N + ws / 2 + 2 * kChainCB;
@@ -949,8 +952,19 @@ __device__ __forceinline__ void chain_l2_pull(const double* p, int cnt) {
         : "v20", "v21", "v22", "v23", "v24", "v25", "s40", "scc", "memory");
 }
 
-template <int WS>
+// EXCL: each wave claims the whole register file of its SIMD (256 arch + 256 acc
+// VGPRs), so a chain workgroup owns its CU outright. Small batches only (the
+// launcher requires B * passes <= kChainExclMax): with one workgroup per CU every
+// pass must still find a CU of its own. Concurrent pipelines on other streams
+// then never put waves next to the chain, feeder and scaler waves (which spin
+// and would slow them, and whose neighbours they would slow: a stream's
+// k_fit_sup_tf launch lasts as long as its slowest workgroup).
+template <int WS, bool EXCL>
 __global__ __launch_bounds__(64 * (2 + kChainScalers)) void k_smooth_chain(BatchArgs a, Workspace w, int P) {
+    if constexpr (EXCL) {
+        asm volatile("v_mov_b32 v255, 0" ::: "v255");
+        asm volatile("v_accvgpr_write_b32 a255, 0" ::: "a255");
+    }
     // workgroup id -> (spectrum, pass): the P passes of a spectrum share id % 8
     // (the XCD of round-robin dispatch), so their hand-offs stay in one L2
     const int id = blockIdx.x;
@@ -3074,6 +3088,190 @@ __global__ __launch_bounds__(BS) void k_mse_partial_n(BatchArgs a, Workspace w, 
     }
 }
 
+// ----------------------------------------------------------------------------------
+// MSE superposition with one division per four Lorentzians (k_mse_quad).
+// compute_mse (deconvoluter.rs:828-862) only needs the MSE within the tests'
+// 1e-12 relative tolerance: the summation order inside a point's superposition is
+// free there, and so is the rounding of each term. The retained Lorentzians have
+// sfhw > 0 and hw2 > 0 (fitter_analytical.rs:67-69), so every term is positive and
+// four of them combine without cancellation:
+//   f0/b0 + f1/b1 = (f0 b1 + f1 b0) / (b0 b1),   b = hw2 + (x - maxp)^2 (one fma),
+// two such pairs again into N/D, then one reciprocal with one Newton step and one
+// residual correction. About seven issue slots per term against thirteen for a
+// term with its own division; the relative error of a quad stays within ~8 ulp.
+// Ranges: under the FAST flags (peak_fast_ok, x_ok) b lies in [2^-200, 2^203), so
+// D (four b) in [2^-800, 2^812) and every product stays normal and finite; spectra
+// outside them take the IEEE '/' per term.
+// A workgroup's four waves share its 64 * NPT points and split the Lorentzians into
+// four contiguous ranges (more waves per SIMD to hide the scalar loads at small B);
+// the partial sums meet in LDS, then the residuals, the tree and the last-workgroup
+// fold of k_mse_partial_n.
+// ----------------------------------------------------------------------------------
+__device__ __forceinline__ double quad_term(double x, const double (&c)[12]) {
+    const double d0 = x - c[2], d1 = x - c[5], d2 = x - c[8], d3 = x - c[11];
+    const double b0 = __builtin_fma(d0, d0, c[1]);
+    const double b1 = __builtin_fma(d1, d1, c[4]);
+    const double b2 = __builtin_fma(d2, d2, c[7]);
+    const double b3 = __builtin_fma(d3, d3, c[10]);
+    const double n01 = __builtin_fma(c[3], b0, c[0] * b1);
+    const double n23 = __builtin_fma(c[9], b2, c[6] * b3);
+    const double d01 = b0 * b1, d23 = b2 * b3;
+    const double N = __builtin_fma(n01, d23, n23 * d01);
+    const double D = d01 * d23;
+    const double r0 = __builtin_amdgcn_rcp(D);
+    const double r1 = __builtin_fma(r0, __builtin_fma(-D, r0, 1.0), r0);
+    const double q0 = N * r1;
+    return __builtin_fma(__builtin_fma(-D, q0, N), r1, q0);
+}
+
+// acc[i] += sum over Lorentzians [j0, j1) of point x[i]; FAST: quads (j1 - j0 any)
+template <bool FAST, int NPT>
+__device__ __forceinline__ void sup_range_quad(const double (&x)[NPT], const_f64_ptr params, int j0,
+                                               int j1, double (&acc)[NPT]) {
+    int j = j0;
+    if (FAST && j1 - j0 >= 4) {
+        const int nq = (j1 - j0) / 4;
+        double A[12], B[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) A[k] = params[3 * j + k];
+        int q = 0;
+        for (; q + 2 <= nq; q += 2) {
+            const const_f64_ptr nb = params + 3 * (j + 4);
+#pragma unroll
+            for (int k = 0; k < 12; ++k) B[k] = nb[k];
+            double t[NPT];
+#pragma unroll
+            for (int i = 0; i < NPT; ++i) t[i] = quad_term(x[i], A);
+#pragma unroll
+            for (int i = 0; i < NPT; ++i) acc[i] += t[i];
+            const int jn = (q + 2 < nq) ? j + 8 : j + 4;  // next A (re-read of B's at the end)
+            const const_f64_ptr na = params + 3 * jn;
+#pragma unroll
+            for (int k = 0; k < 12; ++k) A[k] = na[k];
+#pragma unroll
+            for (int i = 0; i < NPT; ++i) t[i] = quad_term(x[i], B);
+#pragma unroll
+            for (int i = 0; i < NPT; ++i) acc[i] += t[i];
+            j += 8;
+        }
+        if (q < nq) {
+#pragma unroll
+            for (int i = 0; i < NPT; ++i) acc[i] += quad_term(x[i], A);
+            j += 4;
+        }
+    }
+    for (; j < j1; ++j) {
+        const const_f64_ptr L = params + 3 * j;
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) acc[i] += lorentz_mse<FAST>(x[i], L[0], L[1], L[2]);
+    }
+}
+
+template <int NPT>
+__global__ __launch_bounds__(256) void k_mse_quad(BatchArgs a, Workspace w, int nparts) {
+    constexpr int BS = 256, NW = 4, PTS = 64 * NPT;
+    const int s = blockIdx.x % a.B, part = blockIdx.x / a.B;
+    __shared__ double psum[NW - 1][PTS];
+    __shared__ int last;
+    if (w.status[s]) return;  // already reported by k_retain
+    if (w.mse_panic[s]) {
+        if (part == 0) mse_panic_out(a, s);
+        return;
+    }
+    const int P = w.kept_count[s];
+    const const_f64_ptr kept = (const_f64_ptr)(w.kept + 3 * (size_t)s * w.capD);
+    const double* x = a.x + (size_t)s * a.x_stride;
+    const double* y = a.y + (size_t)s * a.y_stride;
+    const int nig = w.n_ig[s];
+    int64_t total = 0;
+    for (int r = 0; r <= nig; ++r) {
+        int64_t lo, hi;
+        mse_region(w, s, r, nig, &lo, &hi);
+        total += hi - lo;
+    }
+    const bool fast = w.x_ok[s] && w.unsafe_kept[s] == 0;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    // wave wv's Lorentzians: [j0, j1), quad-aligned split
+    const int per = ((P + 4 * NW - 1) / (4 * NW)) * 4;
+    const int j0 = min(P, wv * per), j1 = min(P, j0 + per);
+    double acc = 0.0;
+    for (int64_t v0 = (int64_t)part * PTS; v0 < total; v0 += (int64_t)nparts * PTS) {
+        double xv[NPT], yv[NPT];
+        bool ok[NPT];
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) {
+            const int64_t v = v0 + lane + 64 * i;
+            ok[i] = v < total;
+            int64_t rem = ok[i] ? v : 0, idx = 0;
+            for (int r = 0; r <= nig; ++r) {
+                int64_t lo, hi;
+                mse_region(w, s, r, nig, &lo, &hi);
+                if (rem < hi - lo) {
+                    idx = lo + rem;
+                    break;
+                }
+                rem -= hi - lo;
+            }
+            xv[i] = x[idx];
+            yv[i] = wv == 0 ? y[idx] : 0.0;
+        }
+        double sup[NPT];
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) sup[i] = 0.0;
+        if (fast) sup_range_quad<true, NPT>(xv, kept, j0, j1, sup);
+        else sup_range_quad<false, NPT>(xv, kept, j0, j1, sup);
+        if (wv > 0) {
+#pragma unroll
+            for (int i = 0; i < NPT; ++i) psum[wv - 1][lane + 64 * i] = sup[i];
+        }
+        __syncthreads();
+        if (wv == 0) {
+#pragma unroll
+            for (int i = 0; i < NPT; ++i) {
+                double t = sup[i];
+#pragma unroll
+                for (int k = 0; k < NW - 1; ++k) t += psum[k][lane + 64 * i];
+                const double d = t - yv[i];
+                if (ok[i]) acc += d * d;
+            }
+        }
+        __syncthreads();
+    }
+    if (wv == 0) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    }
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(w.mse_part + (size_t)s * nparts + part, acc, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int done = __hip_atomic_fetch_add(w.mse_done + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = done == nparts - 1;
+        if (last) __hip_atomic_store(w.mse_done + s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!last) return;
+    __shared__ double parts[kMseMaxParts];
+    for (int k = threadIdx.x; k < nparts; k += BS) parts[k] = ld_sc1(w.mse_part + (size_t)s * nparts + k);
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const int sub = threadIdx.x & 15;
+        const double one = 1.0;
+        double t = 0.0;
+        const int G = nparts / 16;
+        for (int g = 0; g < G; ++g) fold16(t, parts[16 * g + sub], one);
+        const int r = nparts - 16 * G;
+        if (r > 0) {
+            const double v = parts[min(16 * G + sub, nparts - 1)];
+            for (int k = 0; k < r; ++k) t += readlane_f64(v, k);
+        }
+        if (threadIdx.x == 0) {
+            a.out_mse[s] = t / (double)mse_len(w, s);
+            a.out_status[s] = (w.kept_count[s] > a.cap) ? MDG_CAPACITY : MDG_OK;
+        }
+    }
+}
+
 // total length of the MSE regions of spectrum s (the divisor of compute_mse)
 __device__ __forceinline__ int64_t mse_len(const Workspace& w, int s) {
     const int nig = w.n_ig[s];
@@ -3192,26 +3390,50 @@ void launch_prep(const BatchArgs& a, const Workspace& w, hipStream_t st) {
     hipLaunchKernelGGL(k_prep, dim3(cdiv(a.B, 64)), dim3(64), 0, st, a, w);
 }
 template <int WS>
-static void launch_waves(const BatchArgs& a, const Workspace& w, int iters, hipStream_t st) {
+static const char* launch_waves(const BatchArgs& a, const Workspace& w, int iters, hipStream_t st) {
     constexpr int U = WS * ((32 + WS - 1) / WS);
     constexpr int RAWSLOT = ((U * 8 + 255) / 256) * 32;
     const size_t lds = sizeof(double) * (4 * RAWSLOT + (size_t)iters * 4 * U);
     const int waves = (iters + 3) / 4 * 4;
     hipLaunchKernelGGL(k_smooth_waves<WS>, dim3(a.B), dim3(64 * waves), lds, st, a, w, iters);
+    static const char* names[] = {"", "", "k_smooth_waves<2>", "k_smooth_waves<3>", "k_smooth_waves<4>",
+                                  "k_smooth_waves<5>", "k_smooth_waves<6>", "k_smooth_waves<7>",
+                                  "k_smooth_waves<8>", "k_smooth_waves<9>", "", "k_smooth_waves<11>"};
+    return names[WS];
 }
 
 template <int WS>
-static void launch_pipe(const BatchArgs& a, const Workspace& w, int iters, hipStream_t st) {
+static const char* launch_pipe(const BatchArgs& a, const Workspace& w, int iters, hipStream_t st) {
     const int spw = 64 / iters;
     hipLaunchKernelGGL(k_smooth_pipe<WS>, dim3(cdiv(a.B, spw)), dim3(64), 0, st, a, w, iters, spw);
+    static const char* names[] = {"", "", "k_smooth_pipe<2>", "k_smooth_pipe<3>", "k_smooth_pipe<4>",
+                                  "k_smooth_pipe<5>", "k_smooth_pipe<6>", "k_smooth_pipe<7>",
+                                  "k_smooth_pipe<8>", "k_smooth_pipe<9>", "", "k_smooth_pipe<11>"};
+    return names[WS];
 }
 
 template <int WS>
-static void launch_chain(const BatchArgs& a, const Workspace& w, int iters, hipStream_t st) {
+static const char* launch_chain(const BatchArgs& a, const Workspace& w, int iters, hipStream_t st) {
     const unsigned grid = 8u * (unsigned)iters * cdiv(a.B, 8);
-    hipLaunchKernelGGL(k_smooth_chain<WS>, dim3(grid), dim3(64 * (2 + kChainScalers)), 0, st, a, w, iters);
+    const char* excl_env = std::getenv("MDG_CHAIN_EXCL");  // 0 = never (measurements)
+    const bool excl = (int)grid <= kChainExclMax && !(excl_env && excl_env[0] == '0');
+    if (excl) {
+        hipLaunchKernelGGL((k_smooth_chain<WS, true>), dim3(grid), dim3(64 * (2 + kChainScalers)), 0, st,
+                           a, w, iters);
+    } else {
+        hipLaunchKernelGGL((k_smooth_chain<WS, false>), dim3(grid), dim3(64 * (2 + kChainScalers)), 0, st,
+                           a, w, iters);
+    }
+    static const char* names[2][9] = {
+        {"", "", "k_smooth_chain<2, false>", "k_smooth_chain<3, false>", "k_smooth_chain<4, false>",
+         "k_smooth_chain<5, false>", "k_smooth_chain<6, false>", "k_smooth_chain<7, false>",
+         "k_smooth_chain<8, false>"},
+        {"", "", "k_smooth_chain<2, true>", "k_smooth_chain<3, true>", "k_smooth_chain<4, true>",
+         "k_smooth_chain<5, true>", "k_smooth_chain<6, true>", "k_smooth_chain<7, true>",
+         "k_smooth_chain<8, true>"}};
+    return names[excl ? 1 : 0][WS];
 }
-void launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int ws, hipStream_t st) {
+const char* launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int ws, hipStream_t st) {
     // chain kernel (one CU per pass) for windows <= 8 and batches <= 512; then
     // wave-per-pass (B > 21) or lane-pipelined (window fits the register FIFO);
     // the one-lane-per-spectrum kernel otherwise. MDG_SMOOTH = chain | waves |
@@ -3261,30 +3483,34 @@ void launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int ws, hi
         }
     }
     hipLaunchKernelGGL(k_smooth, dim3(cdiv(a.B, 64)), dim3(64), 0, st, a, w, iters, ws);
+    return "k_smooth";
 }
 void launch_flags(const BatchArgs& a, const Workspace& w, hipStream_t st) {
     hipLaunchKernelGGL(k_flags, dim3(cdiv(a.N, 256), a.B), dim3(256), 0, st, a, w);
 }
-void launch_peaks(const BatchArgs& a, const Workspace& w, int detector_only, hipStream_t st) {
+const char* launch_peaks(const BatchArgs& a, const Workspace& w, int detector_only, hipStream_t st) {
     const int nch = cdiv(w.W, kPkWords);
     static_assert(kPkWords == 256, "k_flags clears ceil(W / 256) slots");
     if (std::getenv("MDG_PEAKS_2PASS")) {  // the two-kernel form, for comparison
         hipLaunchKernelGGL(k_peaks_count, dim3(nch, a.B), dim3(kPkWords), 0, st, a, w, detector_only);
         hipLaunchKernelGGL(k_peaks_write, dim3(nch, a.B), dim3(kPkWords), 0, st, a, w, detector_only);
-        return;
+        return "k_flags+k_peaks_count+k_peaks_write";
     }
     hipLaunchKernelGGL(k_peaks, dim3(nch, a.B), dim3(kPkWords), 0, st, a, w, detector_only);
+    return "k_flags+k_peaks";
 }
 void launch_scores(const BatchArgs& a, const Workspace& w, hipStream_t st) {
     const int gx = std::max(1, std::min(64, 4096 / std::max(1, a.B)));
     hipLaunchKernelGGL(k_scores, dim3(gx, a.B), dim3(256), 0, st, a, w);
 }
-void launch_select(const BatchArgs& a, const Workspace& w, int detector_only, double threshold,
-                   hipStream_t st) {
-    if (detector_only)
+const char* launch_select(const BatchArgs& a, const Workspace& w, int detector_only,
+                          double threshold, hipStream_t st) {
+    if (detector_only) {
         hipLaunchKernelGGL(k_select_detector_only, dim3(16, a.B), dim3(256), 0, st, a, w);
-    else
-        hipLaunchKernelGGL(k_select<1024>, dim3(a.B), dim3(1024), 0, st, a, w, threshold);
+        return "k_select_detector_only";
+    }
+    hipLaunchKernelGGL(k_select<1024>, dim3(a.B), dim3(1024), 0, st, a, w, threshold);
+    return "k_scores+k_select<1024>";
 }
 void launch_fit_init(const BatchArgs& a, const Workspace& w, int gx, hipStream_t st) {
     hipLaunchKernelGGL(k_fit_init, dim3(gx, a.B), dim3(256), 0, st, a, w);
@@ -3300,25 +3526,28 @@ static std::string fit_choice(const BatchArgs& a) {
     return a.B <= 2 ? "tf" : a.B <= 8 ? "dpp" : "plain";
 }
 bool fit_sup_fused(const BatchArgs& a) { return fit_choice(a) == "tf"; }
-void launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st) {
+const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st) {
     const std::string f = fit_choice(a);
     if (f == "tf") {
         // 24 points per workgroup: 256 workgroups at P = 2048, grid-stride beyond
         const int g = std::max(2, 256 / a.B);
         hipLaunchKernelGGL(k_fit_sup_tf, dim3(g, a.B), dim3(64 * (kTfEW + 1)), 0, st, a, w, it);
+        return "k_fit_sup_tf";
     } else if (f == "dpp") {
         // 32 points per workgroup: 192 workgroups at P = 2048, grid-stride beyond
         const int g = std::max(64, std::min(512, 1024 / a.B));
         hipLaunchKernelGGL(k_fit_sup_dpp, dim3(g, a.B), dim3(256), 0, st, a, w, it);
+        return "k_fit_sup_dpp";
     } else if (f == "split") {
         // 16 points per 1024-thread workgroup: 3P/16 workgroups per spectrum (384 at
         // P = 2048) keep every CU busy; grid-stride beyond that
         const int g = std::max(64, std::min(1024, 2048 / a.B));
         hipLaunchKernelGGL((k_fit_sup_split<16, 128, 1024>), dim3(g, a.B), dim3(1024), 0, st, a, w, it);
-    } else {
-        // gx 256-thread workgroups per spectrum (24: one point per thread at P = 2048)
-        hipLaunchKernelGGL(k_fit_sup, dim3(gx * a.B), dim3(256), 0, st, a, w, it);
+        return "k_fit_sup_split<16, 128, 1024>";
     }
+    // gx 256-thread workgroups per spectrum (24: one point per thread at P = 2048)
+    hipLaunchKernelGGL(k_fit_sup, dim3(gx * a.B), dim3(256), 0, st, a, w, it);
+    return "k_fit_sup";
 }
 void launch_fit_update(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st) {
     hipLaunchKernelGGL(k_fit_update, dim3(gx, a.B), dim3(256), 0, st, a, w, it);
@@ -3326,24 +3555,44 @@ void launch_fit_update(const BatchArgs& a, const Workspace& w, int gx, int it, h
 void launch_retain(const BatchArgs& a, const Workspace& w, hipStream_t st) {
     hipLaunchKernelGGL(k_retain<1024>, dim3(a.B), dim3(1024), 0, st, a, w);
 }
-// points per thread of the MSE superposition (MDG_MSE_NPT overrides, for tuning)
-static int mse_npt(const BatchArgs& a) {
-    if (const char* e = std::getenv("MDG_MSE_NPT")) return std::atoi(e) == 2 ? 2 : 1;
-    return 2;  // bench: B = 1 124 -> 113 us, B = 256 16.79 -> 16.62 ms
+// MSE kernel: quad (k_mse_quad<NPT>, default) | n (k_mse_partial_n<256, 2>, one
+// division per term) | plain (k_mse_partial + k_mse_final); MDG_MSE overrides
+static std::string mse_kind() {
+    const char* e = std::getenv("MDG_MSE");
+    return (e && *e) ? std::string(e) : std::string("quad");
+}
+static int mse_quad_npt(const BatchArgs& a) {
+    if (const char* e = std::getenv("MDG_MSE_QNPT")) return std::atoi(e) == 2 ? 2 : 1;
+    return 2;
 }
 int mse_nparts(const BatchArgs& a) {
+    const std::string k = mse_kind();
+    if (k == "quad") {
+        // one workgroup per 64 * NPT points (its four waves split the Lorentzians)
+        const int pts = 64 * mse_quad_npt(a);
+        return std::max(1, std::min({kMseMaxParts, (a.N + pts - 1) / pts, std::max(1, 8192 / a.B)}));
+    }
     const int base = std::max(1, std::min({1024, (a.N + 255) / 256, std::max(1, 4096 / a.B)}));
-    const int npt = mse_npt(a);
-    return std::max(1, (base + npt - 1) / npt);
+    return k == "plain" ? base : std::max(1, (base + 1) / 2);  // n: two points per thread
 }
-void launch_mse(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st) {
-    if (mse_npt(a) == 2)
+const char* launch_mse(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st) {
+    if (mse_kind() == "quad") {
+        if (mse_quad_npt(a) == 2) {
+            hipLaunchKernelGGL(k_mse_quad<2>, dim3(nparts * a.B), dim3(256), 0, st, a, w, nparts);
+            return "k_mse_quad<2>";
+        }
+        hipLaunchKernelGGL(k_mse_quad<1>, dim3(nparts * a.B), dim3(256), 0, st, a, w, nparts);
+        return "k_mse_quad<1>";
+    }
+    if (mse_kind() == "n") {
         hipLaunchKernelGGL((k_mse_partial_n<256, 2>), dim3(nparts * a.B), dim3(256), 0, st, a, w, nparts);
-    else
-        hipLaunchKernelGGL(k_mse_partial<256>, dim3(nparts * a.B), dim3(256), 0, st, a, w, nparts);
+        return "k_mse_partial_n<256, 2>";
+    }
+    hipLaunchKernelGGL(k_mse_partial<256>, dim3(nparts * a.B), dim3(256), 0, st, a, w, nparts);
+    return "k_mse_partial<256>+k_mse_final";
 }
 void launch_mse_final(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st) {
-    if (mse_npt(a) == 2) return;  // k_mse_partial_n folded the partials itself
+    if (mse_kind() != "plain") return;  // k_mse_quad / k_mse_partial_n fold the partials
     hipLaunchKernelGGL(k_mse_final, dim3(a.B), dim3(64), 0, st, a, w, nparts);
 }
 void launch_mse_exact(const double* sup, const double* y, int64_t n, const ExactRegions& r,

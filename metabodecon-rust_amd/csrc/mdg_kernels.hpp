@@ -104,21 +104,21 @@ void launch_mse_exact(const double* sup, const double* y, int64_t n, const Exact
                       double* scratch, double* out, hipStream_t st);
 
 void launch_prep(const BatchArgs& a, const Workspace& w, hipStream_t st);
-void launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int ws, hipStream_t st);
+const char* launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int ws, hipStream_t st);
 void launch_flags(const BatchArgs& a, const Workspace& w, hipStream_t st);
-void launch_peaks(const BatchArgs& a, const Workspace& w, int detector_only, hipStream_t st);
+const char* launch_peaks(const BatchArgs& a, const Workspace& w, int detector_only, hipStream_t st);
 void launch_scores(const BatchArgs& a, const Workspace& w, hipStream_t st);
-void launch_select(const BatchArgs& a, const Workspace& w, int detector_only, double threshold,
-                   hipStream_t st);
+const char* launch_select(const BatchArgs& a, const Workspace& w, int detector_only,
+                          double threshold, hipStream_t st);
 void launch_fit_init(const BatchArgs& a, const Workspace& w, int gx, hipStream_t st);
 // returns true when the launched kernel also did the stencil update (no k_fit_update)
 bool fit_sup_fused(const BatchArgs& a);
-void launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st);
+const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st);
 void launch_fit_update(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st);
 void launch_retain(const BatchArgs& a, const Workspace& w, hipStream_t st);
 // MSE partial sums per spectrum for launch_mse / launch_mse_final (<= 1024)
 int mse_nparts(const BatchArgs& a);
-void launch_mse(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st);
+const char* launch_mse(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st);
 void launch_mse_final(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st);
 // windowed left fold of n <= kWinMax non-negative terms (test support)
 void launch_ordered_sum(const double* t, int n, double acc0, double* out, hipStream_t st);

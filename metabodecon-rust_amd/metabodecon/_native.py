@@ -45,7 +45,7 @@ EXPORTS = [
     "mdg_superposition_vec", "mdg_superposition_vec_device", "mdg_synth_batch_device",
     "mdg_ctx_last_peaks", "mdg_ctx_last_smoothed", "mdg_ctx_set_profiling_mask",
     "mdg_optimize_settings", "mdg_ordered_sum", "mdg_check_fast_division",
-    "mdg_check_division", "mdg_division_hard_case",
+    "mdg_check_division", "mdg_division_hard_case", "mdg_ctx_stage_kernel",
 ]
 
 
@@ -136,6 +136,7 @@ def _declare(L):
     L.mdg_ctx_set_profiling_mask.argtypes = [_vp, ctypes.c_uint32]
     L.mdg_ctx_stage_times.argtypes = [_vp, _dp, _u64p, ctypes.c_int]
     L.mdg_ctx_reset_stage_times.argtypes = [_vp]
+    L.mdg_ctx_stage_kernel.argtypes = [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p)]
     L.mdg_deconvolute.argtypes = [_vp, _dp, _dp, _sz, ctypes.c_double, ctypes.c_double, sp, _dp,
                                   _sz, _dp, _sz, _szp, _dp]
     L.mdg_deconvolute_batch.argtypes = [_vp, _sz, _sz, _dp, _sz, _dp, _sz, _dp, sp, _dp, _sz,
@@ -228,6 +229,16 @@ class Context:
         n = np.zeros(N_STAGES, dtype=np.uint64)
         lib().mdg_ctx_stage_times(self.handle, ptr(ms), ptr(n, _u64p), N_STAGES)
         return {STAGE_NAMES[i]: (float(ms[i]), int(n[i])) for i in range(N_STAGES)}
+
+    def stage_kernels(self) -> dict:
+        """Kernel names the last pipeline run launched, per stage (mdg_ctx_stage_kernel)."""
+        out = {}
+        for i, name in enumerate(STAGE_NAMES):
+            p = ctypes.c_char_p()
+            lib().mdg_ctx_stage_kernel(self.handle, i, ctypes.byref(p))
+            if p.value:
+                out[name] = p.value.decode()
+        return out
 
     def last_smoothed(self, spectrum: int, n: int) -> np.ndarray:
         """Smoothed intensities of `spectrum` from the last batch run (diagnostic)."""

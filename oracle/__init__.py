@@ -136,6 +136,7 @@ def _declare(L):
                                         _dp, _dp, ctypes.POINTER(Settings), _dp,
                                         ctypes.c_size_t, _dp, ctypes.c_size_t, _szp, _dp,
                                         ctypes.POINTER(ctypes.c_int), ctypes.c_int]
+    L.mdo_deconvolute_batch_nested.argtypes = L.mdo_deconvolute_batch.argtypes + [ctypes.c_int]
 
 
 def _f64(a) -> np.ndarray:
@@ -307,8 +308,9 @@ def deconvolute(x, y, sb, settings: Settings | None = None, ignore=(), threads: 
 
 
 def deconvolute_batch(x, y, sb, settings: Settings | None = None, ignore=(), threads: int = 1,
-                      cap: int = 4096):
-    """x: (n,) shared axis or (b, n); y: (b, n); sb: (b, 2). Returns (status, counts, params, mse)."""
+                      cap: int = 4096, inner_threads: int = 1):
+    """x: (n,) shared axis or (b, n); y: (b, n); sb: (b, 2). Returns (status, counts, params, mse).
+    ``threads`` workers over spectra, ``inner_threads`` per spectrum's superpositions."""
     y = _f64(y)
     b, n = y.shape
     x = _f64(x)
@@ -321,8 +323,10 @@ def deconvolute_batch(x, y, sb, settings: Settings | None = None, ignore=(), thr
     counts = np.zeros(b, dtype=np.uintp)
     mse = np.zeros(b)
     status = np.zeros(b, dtype=np.int32)
-    lib().mdo_deconvolute_batch(b, n, _ptr(x), x_stride, _ptr(y), _ptr(sbv),
-                                ctypes.byref(settings), _ptr(ign) if ign.size else None,
-                                ign.size // 2, _ptr(out), cap, _ptr(counts, _szp), _ptr(mse),
-                                status.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), threads)
+    lib().mdo_deconvolute_batch_nested(b, n, _ptr(x), x_stride, _ptr(y), _ptr(sbv),
+                                       ctypes.byref(settings), _ptr(ign) if ign.size else None,
+                                       ign.size // 2, _ptr(out), cap, _ptr(counts, _szp),
+                                       _ptr(mse),
+                                       status.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
+                                       threads, inner_threads)
     return status, counts.astype(np.int64), out, mse

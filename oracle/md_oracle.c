@@ -583,6 +583,7 @@ typedef struct {
     int* status;
     size_t next;
     pthread_mutex_t lock;
+    int inner; /* threads per spectrum for its superpositions (rayon's nested par_iter) */
 } batch_job;
 
 static void* batch_worker(void* arg) {
@@ -597,20 +598,24 @@ static void* batch_worker(void* arg) {
         j->status[i] = mdo_deconvolute(j->x + i * j->x_stride, j->y + i * j->n, j->n,
                                        j->sb[2 * i], j->sb[2 * i + 1], j->s, j->ignore,
                                        j->n_ignore, j->out + i * j->cap * 3, j->cap, &cnt, &m,
-                                       1, NULL);
+                                       j->inner, NULL);
         j->counts[i] = cnt;
         j->mse[i] = m;
     }
     return NULL;
 }
 
-/* deconvoluter.rs:651-661 / :700-710 (fail-fast collect is done by the caller) */
-int mdo_deconvolute_batch(size_t b, size_t n, const double* x, size_t x_stride,
-                          const double* y, const double* sb, const mdo_settings* s,
-                          const double* ignore, size_t n_ignore, double* out_params,
-                          size_t cap, size_t* counts, double* mse, int* status, int threads) {
+/* deconvoluter.rs:651-661 / :700-710 (fail-fast collect is done by the caller).
+ * threads workers take spectra one at a time; each spectrum's superpositions use
+ * inner threads (par_deconvolute_spectra maps par_deconvolute_spectrum, whose
+ * par_fit_lorentzian / par_superposition_vec nest inside the outer par_iter). */
+int mdo_deconvolute_batch_nested(size_t b, size_t n, const double* x, size_t x_stride,
+                                 const double* y, const double* sb, const mdo_settings* s,
+                                 const double* ignore, size_t n_ignore, double* out_params,
+                                 size_t cap, size_t* counts, double* mse, int* status,
+                                 int threads, int inner) {
     batch_job j = {b, n, x, x_stride, y, sb, s, ignore, n_ignore, out_params, cap,
-                   counts, mse, status, 0, PTHREAD_MUTEX_INITIALIZER};
+                   counts, mse, status, 0, PTHREAD_MUTEX_INITIALIZER, inner < 1 ? 1 : inner};
     pthread_mutex_init(&j.lock, NULL);
     if (threads < 1) threads = 1;
     if (threads > 256) threads = 256;
@@ -625,4 +630,12 @@ int mdo_deconvolute_batch(size_t b, size_t n, const double* x, size_t x_stride,
     for (size_t i = 0; i < b; ++i)
         if (status[i]) return status[i];
     return MDO_OK;
+}
+
+int mdo_deconvolute_batch(size_t b, size_t n, const double* x, size_t x_stride,
+                          const double* y, const double* sb, const mdo_settings* s,
+                          const double* ignore, size_t n_ignore, double* out_params,
+                          size_t cap, size_t* counts, double* mse, int* status, int threads) {
+    return mdo_deconvolute_batch_nested(b, n, x, x_stride, y, sb, s, ignore, n_ignore,
+                                        out_params, cap, counts, mse, status, threads, 1);
 }

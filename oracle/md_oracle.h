@@ -115,6 +115,10 @@ int mdo_deconvolute_batch(size_t b, size_t n, const double* x, size_t x_stride,
                           const double* y, const double* sb, const mdo_settings* s,
                           const double* ignore, size_t n_ignore, double* out_params,
                           size_t cap, size_t* counts, double* mse, int* status, int threads);
+int mdo_deconvolute_batch_nested(size_t b, size_t n, const double* x, size_t x_stride,
+                          const double* y, const double* sb, const mdo_settings* s,
+                          const double* ignore, size_t n_ignore, double* out_params,
+                          size_t cap, size_t* counts, double* mse, int* status, int threads, int inner);
 
 #ifdef __cplusplus
 }

@@ -2,8 +2,11 @@
 
 The per-rank compute is replaced by the oracle (test infrastructure) so the
 sharding, the padded all_gather of the Lorentzian tables and the fail-fast
-error order can be checked without a GPU. On the GPU box the same module runs
-with the nccl (RCCL) backend and the HIP engine as ``compute``.
+error order can be checked without a GPU. The product path itself
+(``distributed.par_deconvolute_spectra`` with the HIP engine and the nccl/RCCL
+backend) is covered by ``test_gpu_parity.py::test_par_deconvolute_spectra_rccl_world1``
+on the GPU box. The bench launcher (``bench.py --gpus 2``) is covered here with
+its GPU-free dry run.
 """
 import os
 import socket
@@ -13,6 +16,8 @@ import pytest
 import torch.multiprocessing as mp
 
 from metabodecon.distributed import shard_range
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def test_shard_range_partitions():
@@ -90,3 +95,32 @@ def test_gloo_world2_gather_matches_serial():
             assert np.array_equal(np.array(p).reshape(-1, 3), r.params) and m == r.mse
     first_err = next(s for s, _, _ in got[0] if s)
     assert first_err == 1  # fail-fast reports the first failing spectrum in order
+
+
+def test_bench_gpus_2_spawns_two_ranks():
+    """`bench.py --gpus 2` (no torchrun environment) starts 2 rank processes itself
+    as a child torch.distributed.run; --dry-run keeps them off the GPU (gloo), while
+    the launcher, rendezvous, table gather and max-over-ranks timing run as on the
+    GPU path. The rank-0 line reports n_gpus 2."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--dry-run", "--steps", "2"], capture_output=True, text=True,
+                       timeout=240, env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["dry_run"] is True
+
+
+def test_bench_rejects_gpus_world_mismatch():
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--dry-run"], capture_output=True, text=True, timeout=120, env=env)
+    assert p.returncode == 2

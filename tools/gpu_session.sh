@@ -16,8 +16,8 @@ run() {  # run <name> <timeout> <cmd...>
 for step in "$@"; do
   case "$step" in
     smoke) run smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) run pytest_gpu 1200 python -m pytest tests -m gpu -x -q ;;
-    tests_all) run pytest_gpu 1200 python -m pytest tests -m gpu -q ;;
+    tests) run pytest_gpu 1200 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    tests_all) run pytest_gpu 1200 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ;;
     bench) run bench1 600 python bench.py ;;
     bench64) run bench64 600 python bench.py --batch 64 --steps 5 --warmup 1 --no-cpu-baseline ;;
     bench256) run bench256 600 python bench.py --batch 256 --steps 3 --warmup 1 --no-cpu-baseline ;;
