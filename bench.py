@@ -63,7 +63,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1, help="spectra per step (headline)")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=3,
                     help="engine contexts the steps are spread over (1 = back to back)")
     ap.add_argument("--n", type=int, default=131072)
     ap.add_argument("--peaks", type=int, default=2048)
@@ -115,13 +115,27 @@ def _cpu_model():
     return "unknown"
 
 
-def host_threads(args) -> int:
-    if args.cpu_threads:
-        return args.cpu_threads
+def cgroup_cpus():
+    """CPUs the cgroup v2 quota allows this job (cpu.max 'quota period'), or None."""
     try:
-        return len(os.sched_getaffinity(0))
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else max(1, int(int(q) // int(p)))
+    except (OSError, ValueError):
+        return None
+
+
+def host_threads(args):
+    """Worker threads for the CPU baseline: the CPUs this process may run on
+    (affinity), capped by the cgroup CPU quota -- more threads than the quota
+    only time-slice (on the GPU box: 256 CPUs visible, a 16-CPU quota)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
     except AttributeError:
-        return os.cpu_count() or 1
+        aff = os.cpu_count() or 1
+    quota = cgroup_cpus()
+    if args.cpu_threads:
+        return args.cpu_threads, aff, quota
+    return (min(aff, quota) if quota else aff), aff, quota
 
 
 def median_rate(fn, units, reps=CPU_REPS):
@@ -212,9 +226,11 @@ class Slot:
     """One engine context on its own stream with its own input/output rows."""
 
     def __init__(self, nat, torch, dev, B, n, cap):
+        # the context's own stream (no second stream per slot: HIP maps streams onto
+        # GPU_MAX_HW_QUEUES hardware queues round-robin, and two busy streams on one
+        # queue serialise); torch's copies join it as an external stream
         self.ctx = nat.Context(dev.index)
-        self.stream = torch.cuda.Stream(dev)
-        self.ctx.set_stream(self.stream.cuda_stream)
+        self.stream = torch.cuda.ExternalStream(self.ctx.stream(), device=dev)
         self.y = torch.empty((B, n), dtype=torch.float64, device=dev)
         # one contiguous result record [out | mse | cnt | status]: a step's results
         # leave the slot in one copy
@@ -444,7 +460,8 @@ def cpu_baselines(args, threads, Yh, x, blood_sp, blood_set, c3):
         "sample": (f"{S} synthetic {n}-pt/{args.peaks}-peak spectra per rep over {threads} "
                    f"threads (one spectrum per thread at a time), median of {CPU_REPS} reps "
                    f"({statistics.median(ts):.2f} s); oracle C restatement -O3 "
-                   f"-ffp-contract=off; host {_cpu_model()}, nproc {os.cpu_count()}"),
+                   f"-ffp-contract=off; host {_cpu_model()}, nproc {os.cpu_count()}, "
+                   f"threads = min(affinity, cgroup CPU quota)"),
         "single_core_value": single}
     if blood_sp is not None:  # configs[0]: benches/deconvoluter.rs:8-30
         bx, by = blood_sp.chemical_shifts, blood_sp.intensities
@@ -575,7 +592,7 @@ def main():
         if configs:
             line["configs"] = configs
         if not args.no_cpu_baseline:
-            threads = host_threads(args)
+            threads, aff, quota = host_threads(args)
             # the CPU sample: the same generator (device, bit-identical to the host one)
             ctx = nat.Context(local)
             xd, yd = synth_device(nat, ctx, torch, 2 * threads, args.n, args.peaks, 0, dev)
@@ -586,6 +603,7 @@ def main():
             ctx.close()
             del xd, yd
             cb = cpu_baselines(args, threads, Yh, xh, blood_sp, blood_set, c3)
+            cb["affinity_cpus"], cb["cgroup_quota_cpus"] = aff, quota
             line["cpu_baseline"] = cb["synthetic"]
             line["cpu_baselines"] = {k: v for k, v in cb.items() if k != "synthetic"}
             line["speedup_vs_cpu"] = value / cb["synthetic"]["value"]

@@ -110,6 +110,8 @@ int mdg_ctx_create(int device, mdg_ctx** out);
 int mdg_ctx_destroy(mdg_ctx* ctx);
 /* Run subsequent work on this hipStream_t (NULL = the context's own stream). */
 int mdg_ctx_set_stream(mdg_ctx* ctx, void* hip_stream);
+/* The hipStream_t work is enqueued on (the context's own one unless set). */
+int mdg_ctx_get_stream(mdg_ctx* ctx, void** hip_stream);
 int mdg_ctx_synchronize(mdg_ctx* ctx);
 /* Per-stage device timing with hipEvents on the context stream (0 = off).
  * Stages: 0 prep, 1 smooth, 2 detect, 3 select, 4 fit_init, 5 fit_superposition,

@@ -574,6 +574,13 @@ int mdg_ctx_set_stream(mdg_ctx* c, void* stream) {
     return MDG_OK;
 }
 
+int mdg_ctx_get_stream(mdg_ctx* c, void** stream) {
+    if (!c || !stream) return MDG_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> g(c->mu);
+    *stream = (void*)c->stream;
+    return MDG_OK;
+}
+
 int mdg_ctx_synchronize(mdg_ctx* c) {
     if (!c) return MDG_INVALID_ARGUMENT;
     std::lock_guard<std::mutex> g(c->mu);

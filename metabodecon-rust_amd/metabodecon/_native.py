@@ -45,7 +45,7 @@ EXPORTS = [
     "mdg_superposition_vec", "mdg_superposition_vec_device", "mdg_synth_batch_device",
     "mdg_ctx_last_peaks", "mdg_ctx_last_smoothed", "mdg_ctx_set_profiling_mask",
     "mdg_optimize_settings", "mdg_ordered_sum", "mdg_check_fast_division",
-    "mdg_check_division", "mdg_division_hard_case", "mdg_ctx_stage_kernel",
+    "mdg_check_division", "mdg_division_hard_case", "mdg_ctx_stage_kernel", "mdg_ctx_get_stream",
 ]
 
 
@@ -131,6 +131,7 @@ def _declare(L):
     L.mdg_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(_vp)]
     L.mdg_ctx_destroy.argtypes = [_vp]
     L.mdg_ctx_set_stream.argtypes = [_vp, _vp]
+    L.mdg_ctx_get_stream.argtypes = [_vp, ctypes.POINTER(_vp)]
     L.mdg_ctx_synchronize.argtypes = [_vp]
     L.mdg_ctx_set_profiling.argtypes = [_vp, ctypes.c_int]
     L.mdg_ctx_set_profiling_mask.argtypes = [_vp, ctypes.c_uint32]
@@ -208,6 +209,12 @@ class Context:
 
     def set_stream(self, stream_ptr: int | None):
         lib().mdg_ctx_set_stream(self.handle, _vp(stream_ptr or 0))
+
+    def stream(self) -> int:
+        """hipStream_t (as an int) the context enqueues on."""
+        p = _vp()
+        lib().mdg_ctx_get_stream(self.handle, ctypes.byref(p))
+        return p.value or 0
 
     def synchronize(self):
         st = lib().mdg_ctx_synchronize(self.handle)
