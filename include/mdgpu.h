@@ -101,6 +101,9 @@ int mdg_ignore_region_add(double* regions, size_t n, size_t cap, double a, doubl
  * counter-based splitmix64 so host and device draw identical bits. */
 int mdg_synth_lorentzians(uint64_t seed, size_t n_peaks, double lo, double hi,
                           mdg_lorentzian* out);
+/* Same with every half width scaled by hw_scale (configs[3]: 2.0; 1.0 = the above). */
+int mdg_synth_lorentzians_hw(uint64_t seed, size_t n_peaks, double lo, double hi, double hw_scale,
+                             mdg_lorentzian* out);
 /* Irwin-Hall(12) noise, exact in binary64: sigma * (sum of 12 u48 - 6). */
 int mdg_synth_noise(uint64_t seed, size_t n, double sigma, double* out);
 
@@ -220,6 +223,10 @@ int mdg_division_hard_case(uint64_t seed, uint64_t i, double* n, double* d);
 int mdg_synth_batch_device(mdg_ctx* ctx, size_t b, size_t n, double xmax, double width,
                            uint64_t seed0, size_t n_peaks, double lo, double hi, double sigma,
                            double* d_x, double* d_y);
+/* Same with mdg_synth_lorentzians_hw's half-width scale. */
+int mdg_synth_batch_device_hw(mdg_ctx* ctx, size_t b, size_t n, double xmax, double width,
+                              uint64_t seed0, size_t n_peaks, double lo, double hi, double hw_scale,
+                              double sigma, double* d_x, double* d_y);
 
 #ifdef __cplusplus
 }

@@ -491,6 +491,11 @@ int mdg_ignore_region_add(double* r, size_t n, size_t cap, double a, double b, s
 }
 
 int mdg_synth_lorentzians(uint64_t seed, size_t n_peaks, double lo, double hi, mdg_lorentzian* out) {
+    return mdg_synth_lorentzians_hw(seed, n_peaks, lo, hi, 1.0, out);
+}
+
+int mdg_synth_lorentzians_hw(uint64_t seed, size_t n_peaks, double lo, double hi, double hw_scale,
+                             mdg_lorentzian* out) {
     if (!out && n_peaks) return MDG_INVALID_ARGUMENT;
     const uint64_t key = stream_key(seed, kStreamPeaks);
     const double delta = (hi - lo) / (double)n_peaks;
@@ -498,7 +503,7 @@ int mdg_synth_lorentzians(uint64_t seed, size_t n_peaks, double lo, double hi, m
         const double u1 = u53(draw(key, 3 * p)), u2 = u53(draw(key, 3 * p + 1)),
                      u3 = u53(draw(key, 3 * p + 2));
         const double maxp = lo + ((double)p + 0.5) * delta + (u1 - 0.5) * 0.5 * delta;
-        const double hw = 3.0e-4 + u2 * 5.0e-4;
+        const double hw = (3.0e-4 + u2 * 5.0e-4) * hw_scale;  // x 1.0 is exact
         const double amp = std::pow(10.0, 4.5 + 3.5 * u3);
         const double hw2 = hw * hw;
         out[p].sfhw = amp * hw2;
@@ -938,11 +943,19 @@ int mdg_division_hard_case(uint64_t seed, uint64_t i, double* n, double* d) {
 int mdg_synth_batch_device(mdg_ctx* c, size_t b, size_t n, double xmax, double width,
                            uint64_t seed0, size_t n_peaks, double lo, double hi, double sigma,
                            double* d_x, double* d_y) {
+    return mdg_synth_batch_device_hw(c, b, n, xmax, width, seed0, n_peaks, lo, hi, 1.0, sigma, d_x,
+                                     d_y);
+}
+
+int mdg_synth_batch_device_hw(mdg_ctx* c, size_t b, size_t n, double xmax, double width,
+                              uint64_t seed0, size_t n_peaks, double lo, double hi, double hw_scale,
+                              double sigma, double* d_x, double* d_y) {
     if (!c || !d_x || !d_y || n < 2 || b == 0 || n_peaks > (size_t)INT32_MAX) return MDG_INVALID_ARGUMENT;
     std::lock_guard<std::mutex> g(c->mu);
     HIPCHK(hipSetDevice(c->device));
     std::vector<mdg_lorentzian> params(b * n_peaks);
-    for (size_t s = 0; s < b; ++s) mdg_synth_lorentzians(seed0 + s, n_peaks, lo, hi, params.data() + s * n_peaks);
+    for (size_t s = 0; s < b; ++s)
+        mdg_synth_lorentzians_hw(seed0 + s, n_peaks, lo, hi, hw_scale, params.data() + s * n_peaks);
     int rc;
     if ((rc = ensure(c->st_L, std::max<size_t>(1, params.size()) * 24))) return rc;
     HIPCHK(hipMemcpyAsync(c->st_L.p, params.data(), params.size() * 24, hipMemcpyHostToDevice, c->stream));

@@ -46,6 +46,7 @@ EXPORTS = [
     "mdg_ctx_last_peaks", "mdg_ctx_last_smoothed", "mdg_ctx_set_profiling_mask",
     "mdg_optimize_settings", "mdg_ordered_sum", "mdg_check_fast_division",
     "mdg_check_division", "mdg_division_hard_case", "mdg_ctx_stage_kernel", "mdg_ctx_get_stream",
+    "mdg_synth_lorentzians_hw", "mdg_synth_batch_device_hw",
 ]
 
 
@@ -126,6 +127,8 @@ def _declare(L):
     L.mdg_settings_validate.argtypes = [sp]
     L.mdg_ignore_region_add.argtypes = [_dp, _sz, _sz, ctypes.c_double, ctypes.c_double, _szp]
     L.mdg_synth_lorentzians.argtypes = [ctypes.c_uint64, _sz, ctypes.c_double, ctypes.c_double, _dp]
+    L.mdg_synth_lorentzians_hw.argtypes = [ctypes.c_uint64, _sz, ctypes.c_double, ctypes.c_double,
+                                           ctypes.c_double, _dp]
     L.mdg_synth_noise.argtypes = [ctypes.c_uint64, _sz, ctypes.c_double, _dp]
     L.mdg_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
     L.mdg_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(_vp)]
@@ -158,6 +161,9 @@ def _declare(L):
     L.mdg_synth_batch_device.argtypes = [_vp, _sz, _sz, ctypes.c_double, ctypes.c_double,
                                          ctypes.c_uint64, _sz, ctypes.c_double, ctypes.c_double,
                                          ctypes.c_double, _vp, _vp]
+    L.mdg_synth_batch_device_hw.argtypes = [_vp, _sz, _sz, ctypes.c_double, ctypes.c_double,
+                                            ctypes.c_uint64, _sz, ctypes.c_double, ctypes.c_double,
+                                            ctypes.c_double, ctypes.c_double, _vp, _vp]
 
 
 def strerror(status: int) -> str:

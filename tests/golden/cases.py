@@ -20,7 +20,7 @@ def _spectrum(kind: str, idx: int, sb):
 
 def synth_spectrum(seed: int, n: int = 131072, n_peaks: int = 2048, xmax: float = 14.8,
                    width: float = 20.0, lo: float = -1.8, hi: float = 11.4,
-                   sigma: float = 1.0e3):
+                   sigma: float = 1.0e3, hw_scale: float = 1.0, threads: int | None = None):
     """CPU twin of mdg_synth_batch_device (bit-identical): shared axis, in-order
     superposition of mdg_synth_lorentzians(seed) plus mdg_synth_noise(seed)."""
     import ctypes
@@ -29,11 +29,27 @@ def synth_spectrum(seed: int, n: int = 131072, n_peaks: int = 2048, xmax: float 
     i = np.arange(n, dtype=np.float64)
     x = xmax - (i * width) / (float(n) - 1.0)
     params = np.empty((n_peaks, 3))
-    nat.lib().mdg_synth_lorentzians(seed, n_peaks, lo, hi, nat.ptr(params))
+    nat.lib().mdg_synth_lorentzians_hw(seed, n_peaks, lo, hi, hw_scale, nat.ptr(params))
     noise = np.empty(n)
     nat.lib().mdg_synth_noise(seed, n, sigma, nat.ptr(noise))
-    y = oracle.superposition_vec(x, params, threads=os.cpu_count() or 1) + noise
+    y = oracle.superposition_vec(x, params, threads=threads or host_threads()) + noise
     return x, y, params
+
+
+def host_threads() -> int:
+    """CPUs this process may use: affinity, capped by the cgroup v2 CPU quota (the
+    GPU box shows 256 CPUs under a 16-CPU quota)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(q) // int(p)))
+    except (OSError, ValueError):
+        pass
+    return n
 
 
 def _settings(**kw):
