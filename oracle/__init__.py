@@ -21,7 +21,8 @@ from dataclasses import dataclass
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "libmd_oracle.so")
+# MDO_LIB selects another build of the same source (the sanitizer build, tests only)
+_LIB_PATH = os.environ.get("MDO_LIB", os.path.join(_HERE, "libmd_oracle.so"))
 
 STATUS = {
     0: "Ok",
