@@ -2725,6 +2725,68 @@ __global__ void k_fit_sup(BatchArgs a, Workspace w, int it) {
     }
 }
 
+// EXPERIMENT (configs[2] "superposition recast as MFMA outer product", SURVEY
+// 8d): the fit superposition with every denominator hw2 + (x - maxp)^2 taken
+// from v_mfma_f64_16x16x4_f64 as the product [x'^2, x', 1, 0] . [1, -2m', m'^2 +
+// hw2, 0] with x' = x - c, m' = maxp - c centred on the tile's first point (to
+// keep the cancellation near a peak small). A wave owns 16 points (A rows) and
+// walks the peaks 16 at a time (B columns); lane l then holds the denominators
+// of peak 16t + (l & 15) at points (l >> 4) + 4r, r = 0..3, divides sfhw by them
+// (div_rn under the fast flags) and accumulates per lane; the 16 lanes of a DPP
+// row then add their partial sums. NOT bit-identical (the denominators round
+// differently and the sum is reordered): selected only by MDG_FITSUP=mfma, and
+// measured against the oracle in tools/mfma_experiment.py.
+template <bool FAST>
+__device__ __forceinline__ void fit_mfma_tile(const Workspace& w, size_t base, int P, int p0, int npts,
+                                              const double* __restrict__ params) {
+    typedef double v4d __attribute__((ext_vector_type(4)));
+    const int lane = threadIdx.x & 63;
+    const int col = lane & 15, kk = lane >> 4;
+    const double* rx = w.rx + 3 * base;
+    const double c = rx[min(p0, npts - 1)];
+    const double xa = rx[min(p0 + col, npts - 1)] - c;  // A: row = point p0 + col
+    const double a = kk == 0 ? xa * xa : kk == 1 ? xa : kk == 2 ? 1.0 : 0.0;
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int j0 = 0; j0 < P; j0 += 16) {
+        const int j = min(j0 + col, P - 1);
+        const double f = params[3 * j], h = params[3 * j + 1], m = params[3 * j + 2] - c;
+        const double b = kk == 0 ? 1.0 : kk == 1 ? -2.0 * m : kk == 2 ? m * m + h : 0.0;
+        v4d d = {0.0, 0.0, 0.0, 0.0};
+        d = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, d, 0, 0, 0);
+        if (j0 + col < P) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[r] += FAST ? div_rn(f, d[r]) : f / d[r];
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) acc[r] += __shfl_xor(acc[r], o, 16);
+    }
+    if (col == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = p0 + kk + 4 * r;
+            if (i < npts) w.ratio[3 * base + i] = w.ry[3 * base + i] / acc[r];
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_fit_sup_mfma(BatchArgs a, Workspace w, int it) {
+    const int s = blockIdx.x % a.B, part = blockIdx.x / a.B, parts = gridDim.x / a.B;
+    if (w.status[s] || fit_done(w, s, it)) return;
+    const int P = w.sel_count[s];
+    const size_t base = (size_t)s * w.capD;
+    const double* __restrict__ params = w.params + 3 * base;
+    if (part == 0 && threadIdx.x == 0) w.unsafe[4 * s + ((it + 1) & 1)] = 0;
+    const bool fast = w.x_ok[s] && w.unsafe[4 * s + (it & 1)] == 0;
+    const int npts = 3 * P, wv = threadIdx.x >> 6;
+    for (int p0 = (part * 4 + wv) * 16; p0 < npts; p0 += parts * 64) {
+        if (fast) fit_mfma_tile<true>(w, base, P, p0, npts, params);
+        else fit_mfma_tile<false>(w, base, P, p0, npts, params);
+    }
+}
+
 // K6b  fit superposition for small batches (B*3P too small to fill 256 CUs with
 // one thread per point). A 1024-thread workgroup owns Q reduced points; the
 // evaluations of a chunk of J peaks are spread over (point, peak) lane pairs and
@@ -3538,6 +3600,12 @@ const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int i
         const int g = std::max(64, std::min(512, 1024 / a.B));
         hipLaunchKernelGGL(k_fit_sup_dpp, dim3(g, a.B), dim3(256), 0, st, a, w, it);
         return "k_fit_sup_dpp";
+    } else if (f == "mfma") {
+        // experiment only (not bit-exact): 64 points per workgroup
+        const int g = std::max(1, std::min(2048, (3 * (a.N / 2 + 2) + 63) / 64));
+        const int parts = std::max(1, std::min(g, 8192 / a.B));
+        hipLaunchKernelGGL(k_fit_sup_mfma, dim3(parts * a.B), dim3(256), 0, st, a, w, it);
+        return "k_fit_sup_mfma";
     } else if (f == "split") {
         // 16 points per 1024-thread workgroup: 3P/16 workgroups per spectrum (384 at
         // P = 2048) keep every CU busy; grid-stride beyond that
