@@ -67,6 +67,7 @@ def parse():
                     help="engine contexts the steps are spread over (1 = back to back)")
     ap.add_argument("--n", type=int, default=131072)
     ap.add_argument("--peaks", type=int, default=2048)
+    ap.add_argument("--hw-scale", type=float, default=1.0, help="half-width scale (configs[3]: 2)")
     ap.add_argument("--cap", type=int, default=4096)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = len(sched_getaffinity)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -284,7 +285,8 @@ def headline(args, nat, torch, dist, dev, rank, world):
     settings = nat.default_settings()
     slots = [Slot(nat, torch, dev, B, n, cap) for _ in range(S)]
     R = max(K, W, 1)  # distinct spectra (B each), seeds rank*R*B ...
-    x, Y = synth_device(nat, slots[0].ctx, torch, R * B, n, args.peaks, rank * R * B, dev)
+    x, Y = synth_device(nat, slots[0].ctx, torch, R * B, n, args.peaks, rank * R * B, dev,
+                        args.hw_scale)
     Y = Y.view(R, B, n)
     sb = torch.tensor([SB] * B, dtype=torch.float64, device=dev)
     res = torch.zeros((K, slots[0].rec.numel()), dtype=torch.float64, device=dev)

@@ -1,6 +1,7 @@
 """Summarise rocprofv3 runs of bench.py into profiles/ (per round, per batch size).
 
     python tools/pmc_summary.py r01 b1 [b256 ...]
+    python tools/pmc_summary.py r02 calib      (tools/ubench/fetch_calib passes)
 
 Reads gpurun_out/prof_<tag>/run_kernel_stats.csv (kernel trace + stats) and the
 separate PMC passes gpurun_out/prof_<tag>_FETCH_SIZE and _WRITE_SIZE, and writes
@@ -8,7 +9,12 @@ separate PMC passes gpurun_out/prof_<tag>_FETCH_SIZE and _WRITE_SIZE, and writes
   profiles/<round>_pmc_<tag>.json           (HBM bytes per launch, keyed by stage)
 FETCH_SIZE/WRITE_SIZE are in KiB. On gfx950 FETCH_SIZE counts half the bytes of a
 coalesced streaming read (MI355X_MICROARCH.md, HBM/rocprofv3 section), so it is
-doubled; WRITE_SIZE is taken as is.
+doubled; WRITE_SIZE is taken as is. The guide calibrates only 16-B/lane reads;
+tools/ubench/fetch_calib measures every width the engine uses (16-B and 8-B vector
+loads, 8-B sc1 loads, wave-uniform scalar loads; 16-B, 8-B and sc1 stores) on
+1 GiB each, and all read widths came out at FETCH_SIZE = bytes / 2, all store
+widths at WRITE_SIZE = bytes (profiles/r02_fetch_calibration.json), so the one
+factor applies to every kernel here.
 """
 import collections
 import csv
@@ -26,7 +32,7 @@ STAGES = [  # stage -> kernel-name prefixes (after "mdg::")
     ("fit_superposition", ("k_fit_sup",)),
     ("fit_update", ("k_fit_update",)),
     ("retain", ("k_retain",)),
-    ("mse_superposition", ("k_mse_partial",)),
+    ("mse_superposition", ("k_mse_partial", "k_mse_quad")),
     ("mse_reduce", ("k_mse_final",)),
 ]
 
@@ -52,7 +58,26 @@ def per_kernel(path, counter):
     return {k: sum(v) / len(v) for k, v in acc.items()}
 
 
+def calib(rnd):
+    out = {"round": rnd, "source": "tools/ubench/fetch_calib (1 GiB per kernel, read or written once)",
+           "bytes_per_kernel": 1 << 30, "kernels": {}}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        path = os.path.join(ROOT, "gpurun_out", f"prof_calib_{ctr}", "run_counter_collection.csv")
+        for k, kib in per_kernel(path, ctr).items():
+            if not (k.startswith("read") or k.startswith("write")):
+                continue
+            e = out["kernels"].setdefault(k, {})
+            e[ctr.lower() + "_kib"] = kib
+            if kib:
+                e["bytes_per_" + ctr.lower() + "_byte"] = (1 << 30) / (kib * 1024)
+    path = os.path.join(ROOT, "profiles", f"{rnd}_fetch_calibration.json")
+    json.dump(out, open(path, "w"), indent=1)
+    print("wrote", path)
+
+
 def main(rnd, tags):
+    if tags == ["calib"]:
+        return calib(rnd)
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     for tag in tags:
         base = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
@@ -62,8 +87,11 @@ def main(rnd, tags):
             shutil.copy(stats, os.path.join(ROOT, "profiles", f"{rnd}_{tag}_kernel_stats.csv"))
             for r in csv.DictReader(open(stats)):
                 avg_ns[short(r["Name"])] = float(r["AverageNs"])
-        fetch = per_kernel(os.path.join(base + "_FETCH_SIZE", "run_counter_collection.csv"),
-                           "FETCH_SIZE")
+        fpath = os.path.join(base + "_FETCH_SIZE", "run_counter_collection.csv")
+        if not os.path.exists(fpath):
+            print("kernel stats only for", tag)
+            continue
+        fetch = per_kernel(fpath, "FETCH_SIZE")
         write = per_kernel(os.path.join(base + "_WRITE_SIZE", "run_counter_collection.csv"),
                            "WRITE_SIZE")
         kernels = {}
