@@ -3,7 +3,7 @@
  *
  * TEST INFRASTRUCTURE / CPU BASELINE ONLY. Not part of the product: the HIP
  * library (libmdgpu.so) never links it. It is compiled with
- * -O2 -ffp-contract=off -fno-fast-math so that every f64 operation rounds
+ * -O3 -ffp-contract=off -fno-fast-math (oracle/Makefile) so that every f64 operation rounds
  * exactly like the Rust reference (rustc never contracts a*b+c into an FMA).
  *
  * Reference files are cited relative to metabodecon/src/ of
