@@ -8,11 +8,14 @@ analytical fit 10 iterations, MSE). One step = one deconvolution of one distinct
 spectrum (--batch 1); inputs are resident in HBM before timing.
 
 Steps are submitted round-robin to --streams engine contexts (one HIP stream and
-one HBM workspace each), the way concurrent callers of the reference's
+one HBM workspace each; default 16, with GPU_MAX_HW_QUEUES=32 so every stream has
+its own hardware queue), the way concurrent callers of the reference's
 `par_deconvolute_spectrum` (Deconvoluter is Send + Sync, deconvoluter.rs:913-917)
-would use one GPU: spectrum k+1's sequential smoother overlaps spectrum k's fit
-and MSE. `value` is that stream's throughput; `latency_ms` is one spectrum alone
-on an idle GPU (one context, steps back to back).
+would use one GPU: the sequential smoothers of some spectra overlap the fits and
+MSEs of others. `value` is that stream's throughput; `latency_ms` is one
+spectrum alone on an idle GPU (one context, synchronised each step);
+`latency_in_stream_ms` is the time a spectrum spends in flight in the stream
+(streams / throughput, Little's law).
 
 --gpus N: without WORLD_SIZE in the environment, bench.py starts N rank processes
 itself (torch.distributed.run as a child process, before any GPU call) and exits
@@ -60,11 +63,14 @@ CPU_REPS = 5
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=60)
+    ap.add_argument("--steps", type=int, default=240)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1, help="spectra per step (headline)")
-    ap.add_argument("--streams", type=int, default=3,
+    ap.add_argument("--streams", type=int, default=16,
                     help="engine contexts the steps are spread over (1 = back to back)")
+    ap.add_argument("--hw-queues", type=int, default=32,
+                    help="GPU_MAX_HW_QUEUES for this process (HIP maps streams onto that "
+                         "many hardware queues round-robin; <= 32)")
     ap.add_argument("--n", type=int, default=131072)
     ap.add_argument("--peaks", type=int, default=2048)
     ap.add_argument("--hw-scale", type=float, default=1.0, help="half-width scale (configs[3]: 2)")
@@ -317,6 +323,7 @@ def headline(args, nat, torch, dist, dev, rank, world):
     t0 = time.perf_counter()
     for k in range(K):
         submit(k, k % R, S)
+    submit_s = time.perf_counter() - t0  # host time to enqueue the K steps
     torch.cuda.synchronize()
     if world > 1:  # RCCL gather of every rank's result records (the weak-scaling exchange)
         g_res = torch.empty((world * K, res.shape[1]), dtype=torch.float64, device=dev)
@@ -348,6 +355,7 @@ def headline(args, nat, torch, dist, dev, rank, world):
     kept = res_cnt.cpu().numpy()
     out = {
         "elapsed": elapsed, "spectra": world * K * B, "latency_ms": 1e3 * statistics.median(lat),
+        "host_submit_ms_per_step": 1e3 * submit_s / K,
         "roofline": roof,
         "stages_ms_per_spectrum": {k: v[0] / prof_steps / B for k, v in prof.items() if v[1]},
         "selected_peaks": P_sel[:4], "kept_peaks": [int(c) for c in kept[:4, 0]],
@@ -524,6 +532,10 @@ def dry_run(args, world, rank):
 
 def main():
     args = parse()
+    # before anything initialises HIP (torch is imported below, and ranks inherit
+    # the environment): one hardware queue per busy stream, or two streams that
+    # share a queue serialise
+    os.environ["GPU_MAX_HW_QUEUES"] = str(max(1, min(32, args.hw_queues)))
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -556,6 +568,8 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": h["elapsed"] / args.steps * 1e3,
         "latency_ms": h["latency_ms"],
+        "latency_in_stream_ms": args.streams * h["elapsed"] / args.steps * 1e3,
+        "host_submit_ms_per_step": h["host_submit_ms_per_step"],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -567,6 +581,7 @@ def main():
                                 f"batch of {B} synthetic spectra per GPU per step"),
                    "n_points": args.n, "injected_peaks": args.peaks,
                    "spectra_per_gpu_per_step": B, "streams": args.streams,
+                   "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]),
                    "selected_peaks": h["selected_peaks"], "kept_peaks": h["kept_peaks"],
                    "parallelism": f"dp{world}" if world > 1 else "single"},
         "roofline": h["roofline"],
