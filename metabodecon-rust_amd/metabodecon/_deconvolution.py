@@ -298,6 +298,17 @@ class Deconvolution:
 # =====================================================================================
 # Deconvoluter (bindings/deconvoluter.rs:17-165, deconvoluter.rs:118-905)
 # =====================================================================================
+_pool = None
+
+
+def _lane_pool(n: int):
+    global _pool
+    if _pool is None:
+        from concurrent.futures import ThreadPoolExecutor
+        _pool = ThreadPoolExecutor(max_workers=n, thread_name_prefix="mdgpu-lane")
+    return _pool
+
+
 class Deconvoluter:
     # merged ignore regions the engine takes per call (kMaxIgnore, mdg_common.hpp);
     # the reference has no limit -- add_ignore_region refuses the 65th disjoint
@@ -392,9 +403,37 @@ class Deconvoluter:
             raise exc.UnexpectedError(f"more than {self.MAX_IGNORE} ignore regions")
         return np.array(self._ignore, dtype=np.float64).reshape(-1)
 
+    # Spectra of one call deconvoluted concurrently, one per engine context (own
+    # HIP stream and workspace), up to this many; larger groups run as one batched
+    # pipeline. Small sets gain: each spectrum's sequential smoother overlaps the
+    # others' fits; a large batch already fills the GPU.
+    LANES = 16
+
+    def _run_batch(self, ctx, spectra: list[Spectrum], idx: list[int], n: int, ign):
+        b = len(idx)
+        x = np.stack([spectra[i].chemical_shifts for i in idx])
+        y = np.stack([spectra[i].intensities for i in idx])
+        sb = np.array([spectra[i].signal_boundaries for i in idx], dtype=np.float64)
+        cap = n // 2 + 2
+        out = np.empty((b, cap, 3))
+        counts = np.zeros(b, dtype=np.uintp)
+        mse = np.zeros(b)
+        status = np.zeros(b, dtype=np.intc)
+        with ctx.lock:  # ctypes drops the GIL for the call: lanes run concurrently
+            rc = nat.lib().mdg_deconvolute_batch(
+                ctx.handle, b, n, nat.ptr(x), n, nat.ptr(y), n, nat.ptr(sb),
+                ctypes.byref(self._s), nat.ptr(ign) if ign.size else None, ign.size // 2,
+                nat.ptr(out), cap, nat.ptr(counts, nat._szp), nat.ptr(mse),
+                status.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+        if rc >= 100 or rc == nat.INVALID_ARGUMENT:
+            raise exc.UnexpectedError(f"GPU engine failure: {nat.strerror(rc)}")
+        return [(int(status[k]), out[k, : int(counts[k])].copy(), float(mse[k]))
+                for k in range(b)]
+
     def _run(self, spectra: list[Spectrum]) -> list[tuple[int, np.ndarray, float]]:
-        """One batched GPU call per distinct spectrum length; returns per-spectrum
-        (status, params, mse) in input order."""
+        """GPU results per spectrum, (status, params, mse) in input order: spectra of
+        one length run one per context concurrently (up to LANES of them), or as one
+        batched pipeline."""
         results: list = [None] * len(spectra)
         by_n: dict[int, list[int]] = {}
         for i, sp in enumerate(spectra):
@@ -402,27 +441,18 @@ class Deconvoluter:
                 raise TypeError("expected metabodecon.Spectrum")
             by_n.setdefault(len(sp), []).append(i)
         ign = self._ignore_array()
-        ctx = nat.context(self.device)
         for n, idx in by_n.items():
-            b = len(idx)
-            x = np.stack([spectra[i].chemical_shifts for i in idx])
-            y = np.stack([spectra[i].intensities for i in idx])
-            sb = np.array([spectra[i].signal_boundaries for i in idx], dtype=np.float64)
-            cap = n // 2 + 2
-            out = np.empty((b, cap, 3))
-            counts = np.zeros(b, dtype=np.uintp)
-            mse = np.zeros(b)
-            status = np.zeros(b, dtype=np.intc)
-            with ctx.lock:
-                rc = nat.lib().mdg_deconvolute_batch(
-                    ctx.handle, b, n, nat.ptr(x), n, nat.ptr(y), n, nat.ptr(sb),
-                    ctypes.byref(self._s), nat.ptr(ign) if ign.size else None, ign.size // 2,
-                    nat.ptr(out), cap, nat.ptr(counts, nat._szp), nat.ptr(mse),
-                    status.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
-            if rc >= 100 or rc == nat.INVALID_ARGUMENT:
-                raise exc.UnexpectedError(f"GPU engine failure: {nat.strerror(rc)}")
-            for k, i in enumerate(idx):
-                results[i] = (int(status[k]), out[k, : int(counts[k])].copy(), float(mse[k]))
+            if 1 < len(idx) <= self.LANES:
+                lanes = nat.lane_contexts(self.device, len(idx))
+                pool = _lane_pool(self.LANES)
+                futs = [pool.submit(self._run_batch, lanes[k], spectra, [i], n, ign)
+                        for k, i in enumerate(idx)]
+                for i, f in zip(idx, futs):
+                    results[i] = f.result()[0]
+            else:
+                res = self._run_batch(nat.context(self.device), spectra, idx, n, ign)
+                for i, r in zip(idx, res):
+                    results[i] = r
         return results
 
     def _run_device(self, spectra: list[Spectrum]):

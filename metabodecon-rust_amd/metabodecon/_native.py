@@ -301,3 +301,18 @@ def context(device: int | None = None) -> Context:
             c = Context(device)
             _ctx[device] = c
         return c
+
+
+_lanes: dict[int, list[Context]] = {}
+
+
+def lane_contexts(device: int | None, n: int) -> list[Context]:
+    """n engine contexts on `device` (each its own HIP stream and workspace), for
+    spectra deconvoluted concurrently; created on first use and kept."""
+    if device is None:
+        device = default_device()
+    with _ctx_lock:
+        lanes = _lanes.setdefault(device, [])
+        while len(lanes) < n:
+            lanes.append(Context(device))
+        return lanes[:n]
