@@ -9,6 +9,7 @@ the same operation order as lorentzian.rs:546-611.
 from __future__ import annotations
 
 import ctypes
+import os
 import math
 
 import numpy as np
@@ -406,8 +407,10 @@ class Deconvoluter:
     # Spectra of one call deconvoluted concurrently, one per engine context (own
     # HIP stream and workspace), up to this many; larger groups run as one batched
     # pipeline. Small sets gain: each spectrum's sequential smoother overlaps the
-    # others' fits; a large batch already fills the GPU.
-    LANES = 16
+    # others' fits; a large batch already fills the GPU. HIP maps
+    # streams round-robin onto GPU_MAX_HW_QUEUES hardware queues (4 unless set)
+    # and two busy streams on one queue serialise, so the lanes stay below it.
+    LANES = max(1, min(16, int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) - 1))
 
     def _run_batch(self, ctx, spectra: list[Spectrum], idx: list[int], n: int, ign):
         b = len(idx)
