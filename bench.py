@@ -80,6 +80,8 @@ def parse():
     ap.add_argument("--no-configs", action="store_true", help="headline only")
     ap.add_argument("--configs", default="0,2,3,4", help="secondary configs to measure")
     ap.add_argument("--no-profile", action="store_true", help="no per-stage HIP events")
+    ap.add_argument("--fit-iterations", type=int, default=0,
+                    help="diagnostics only: override the analytical fit's iterations (0 = 10)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: exercise the launcher, rendezvous and gather (gloo)")
     return ap.parse_args()
@@ -289,6 +291,8 @@ def headline(args, nat, torch, dist, dev, rank, world):
     """configs[1] stream: args.steps distinct spectra over args.streams contexts."""
     B, n, cap, K, W, S = args.batch, args.n, args.cap, args.steps, args.warmup, args.streams
     settings = nat.default_settings()
+    if args.fit_iterations:
+        settings.fit_iterations = args.fit_iterations
     slots = [Slot(nat, torch, dev, B, n, cap) for _ in range(S)]
     R = max(K, W, 1)  # distinct spectra (B each), seeds rank*R*B ...
     x, Y = synth_device(nat, slots[0].ctx, torch, R * B, n, args.peaks, rank * R * B, dev,
