@@ -2708,6 +2708,119 @@ __global__ __launch_bounds__(64 * (kTfEW + 1)) void k_fit_sup_tf(BatchArgs a, Wo
     else fit_tf_body<false>(w, s, P, it, T);
 }
 
+// K6h  term-fold fit, wide tiles ("tw"): Q = 63 points (21 peaks) per workgroup
+// instead of 24, so the fold wave's LDS reads serve 63 lanes, not 24 (a
+// ds_read_b128 costs its wave 8 cycles of issue whatever EXEC holds,
+// tools/ubench/fold_lds). The PB x PS evaluator waves split a chunk of J = 64 PB
+// peaks into PB blocks (lane = peak, parameters in VGPRs) and the tile's points
+// into PS subsets of Q / PS points (x wave-uniform in SGPRs), so a wave writes
+// Q / PS terms per lane per chunk. Fold, stencil update and parameter versions as
+// in k_fit_sup_tf, so the sums are the same left folds, bit for bit. A spectrum
+// needs 98 workgroups instead of 256 at P = 2048: the same latency on fewer CUs,
+// which is what concurrent pipelines need.
+template <int Q, int PB, int PS>
+struct TwShape {
+    static constexpr int EW = PB * PS, J = 64 * PB, RS = J + kTfPad, QS = Q / PS;
+    static constexpr int LDS = 2 * Q * RS;
+    static_assert(Q % 3 == 0 && Q / 3 <= 64 && Q <= 64 && Q % PS == 0, "tile shape");
+};
+using TwDefault = TwShape<63, 2, 3>;
+
+template <bool FAST, class SH>
+__device__ __forceinline__ void fit_tw_body(const Workspace& w, int s, int P, int it, double* T) {
+    constexpr int QQ = SH::LDS / (2 * SH::RS), EW = SH::EW, J = SH::J, RS = SH::RS, QS = SH::QS;
+    constexpr int PB = J / 64;
+    const size_t base = (size_t)s * w.capD;
+    const int npts = 3 * P;
+    const int tiles = (npts + QQ - 1) / QQ;
+    const int nch = (P + J - 1) / J;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const double* __restrict__ params = params_version(w, base, it);
+    const bool folder = wv == EW;
+    if (folder) __builtin_amdgcn_s_setprio(3);
+    for (int tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+        const int p0 = tile * QQ;
+        if (!folder) {
+            const int pb = wv % PB, ps = wv / PB;
+            // this wave's points: p0 + ps*QS .. +QS-1 (wave-uniform x; a tail tile
+            // reads past 3P into the arena, and those points are never used)
+            const const_f64_ptr rx = (const_f64_ptr)(w.rx + 3 * base + p0 + ps * QS);
+            double xq[QS];
+#pragma unroll
+            for (int q = 0; q < QS; ++q) xq[q] = rx[q];
+            const int jl = pb * 64 + lane;
+            int j = min(jl, P - 1);
+            double f = params[3 * j], h = params[3 * j + 1], m = params[3 * j + 2];
+            for (int c = 0; c <= nch; ++c) {
+                if (c < nch) {
+                    double* Tb = T + (c & 1) * QQ * RS + ps * QS * RS + jl;
+                    const double cf = f, ch = h, cm = m;
+                    j = min((c + 1) * J + jl, P - 1);  // prefetch the next chunk's peak
+                    f = params[3 * j];
+                    h = params[3 * j + 1];
+                    m = params[3 * j + 2];
+#pragma unroll
+                    for (int q = 0; q < QS; ++q) Tb[q * RS] = lorentz_t<FAST>(xq[q], cf, ch, cm);
+                }
+                lds_barrier();
+            }
+        } else {
+            double acc = -0.0;
+            const int q = lane < QQ ? lane : QQ - 1;
+            double one = 1.0;
+            asm volatile("" : "+v"(one));
+            lds_barrier();  // chunk 0 written
+            for (int c = 0; c < nch; ++c) {
+                const double2* row = (const double2*)(T + (c & 1) * QQ * RS + q * RS);
+                const int cn = min(J, P - c * J);
+                if (cn == J) {
+#pragma unroll 16
+                    for (int k = 0; k < J / 2; ++k) {
+                        const double2 v = row[k];
+                        acc = __builtin_fma(v.x, one, acc);
+                        acc = __builtin_fma(v.y, one, acc);
+                    }
+                } else {
+                    const double* r1 = (const double*)row;
+                    for (int k = 0; k < cn; ++k) acc = __builtin_fma(r1[k], one, acc);
+                }
+                lds_barrier();
+            }
+            // stencil update of the tile's peaks: lane k gathers the ratios y/sup of
+            // its peak's three points from lanes 3k..3k+2
+            const double ratio = w.ry[3 * base + min(p0 + q, npts - 1)] / acc;
+            const int k = lane < QQ / 3 ? lane : 0;
+            const double r0 = __shfl(ratio, 3 * k, 64);
+            const double r1 = __shfl(ratio, 3 * k + 1, 64);
+            const double r2 = __shfl(ratio, 3 * k + 2, 64);
+            const int pk = p0 / 3 + lane;
+            if (lane < QQ / 3 && pk < P) {
+                double* st = w.stencil + 6 * base + 6 * (size_t)pk;
+                Stencil sq{st[0], st[1], st[2], st[3], st[4], st[5]};
+                sq.y1 = sq.y1 * r0;
+                sq.y2 = sq.y2 * r1;
+                sq.y3 = sq.y3 * r2;
+                mirror_shoulder(sq);
+                st[0] = sq.x1; st[1] = sq.x2; st[2] = sq.x3; st[3] = sq.y1; st[4] = sq.y2; st[5] = sq.y3;
+                double* L = (((it + 1) & 1) ? w.params_alt : w.params) + 3 * base + 3 * (size_t)pk;
+                solve(sq, L);
+                if (!peak_fast_ok(L[0], L[1], L[2])) atomicAdd(&w.unsafe[4 * s + (it + 1) % 3], 1);
+            }
+        }
+    }
+}
+
+template <class SH>
+__global__ __launch_bounds__(64 * (SH::EW + 1)) void k_fit_sup_tw(BatchArgs a, Workspace w, int it) {
+    __shared__ __attribute__((aligned(16))) double T[SH::LDS];
+    const int s = blockIdx.y;
+    if (w.status[s] || fit_done(w, s, it)) return;
+    const int P = w.sel_count[s];
+    if (blockIdx.x == 0 && threadIdx.x == 0) w.unsafe[4 * s + (it + 2) % 3] = 0;
+    if (w.x_ok[s] && w.unsafe[4 * s + it % 3] == 0) fit_tw_body<true, SH>(w, s, P, it, T);
+    else fit_tw_body<false, SH>(w, s, P, it, T);
+}
+
 // 1-D grid, spectrum = block % B (as k_mse_partial): round-robin dispatch puts the
 // workgroups a CU holds at once on the same spectrum, so they share its Lorentzians
 // in the scalar cache instead of each streaming another spectrum's table
@@ -3581,15 +3694,54 @@ void launch_fit_init(const BatchArgs& a, const Workspace& w, int gx, hipStream_t
 //   B=1 tf 0.215 / dpp 0.277 / plain 0.81;  B=2 tf 0.369 / dpp 0.428;
 //   B=4 dpp 0.589 / tf 0.668;  B=8 dpp 1.37 / plain 1.44 / tf 1.46;
 //   B=12 plain 1.57 / dpp 1.96;  B=256 plain 12.0 / tf 25.4 / dpp 30.6.
-// MDG_FITSUP = tf | dpp | split | plain forces one (tests, tuning).
+// B=1 uses the wide-tile term fold tw<63, 1, 7> (98 workgroups instead of 256):
+// bench spectra/s alone 1021 vs 1007 (tf), 16 concurrent contexts 5715-5742 vs
+// 4555-5139; at B = 2..8 it is slower alone (1607 vs 1648 at B=2, 2249 vs 2624 at
+// B=4) though faster with 16 contexts, so those keep tf / dpp.
+// MDG_FITSUP = tf | tw | tw3 | tw4 | tw7 | tw9 | tw14 | dpp | split | plain forces one.
 static std::string fit_choice(const BatchArgs& a) {
     const char* force = std::getenv("MDG_FITSUP");
     if (force && *force) return force;
-    return a.B <= 2 ? "tf" : a.B <= 8 ? "dpp" : "plain";
+    return a.B == 1 ? "tw7" : a.B <= 2 ? "tf" : a.B <= 8 ? "dpp" : "plain";
 }
-bool fit_sup_fused(const BatchArgs& a) { return fit_choice(a) == "tf"; }
+bool fit_sup_fused(const BatchArgs& a) {
+    const std::string f = fit_choice(a);
+    return f == "tf" || f.rfind("tw", 0) == 0;
+}
 const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st) {
     const std::string f = fit_choice(a);
+    if (f.rfind("tw", 0) == 0) {
+        // 63 points per workgroup: 98 workgroups at P = 2048, grid-stride beyond
+        const int g = std::max(2, 128 / a.B);
+        if (f == "tw4") {  // 4 evaluator waves: 2 peak blocks x 2 point subsets (Q = 60)
+            using SH = TwShape<60, 2, 2>;
+            hipLaunchKernelGGL(k_fit_sup_tw<SH>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
+            return "k_fit_sup_tw<60, 2, 2>";
+        }
+        if (f == "tw7") {  // 7 evaluator waves: 1 peak block x 7 point subsets (Q = 63)
+            using SH = TwShape<63, 1, 7>;
+            hipLaunchKernelGGL(k_fit_sup_tw<SH>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
+            return "k_fit_sup_tw<63, 1, 7>";
+        }
+        if (f == "tw3") {
+            using SH = TwShape<63, 1, 3>;
+            hipLaunchKernelGGL(k_fit_sup_tw<SH>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
+            return "k_fit_sup_tw<63, 1, 3>";
+        }
+        if (f == "tw9") {
+            using SH = TwShape<63, 1, 9>;
+            hipLaunchKernelGGL(k_fit_sup_tw<SH>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
+            return "k_fit_sup_tw<63, 1, 9>";
+        }
+        if (f == "tw14") {  // 2 peak blocks x 7 point subsets
+            using SH = TwShape<63, 2, 7>;
+            hipLaunchKernelGGL(k_fit_sup_tw<SH>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
+            return "k_fit_sup_tw<63, 2, 7>";
+        }
+        using SH = TwDefault;
+        hipLaunchKernelGGL(k_fit_sup_tw<SH>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
+        return "k_fit_sup_tw<63, 2, 3>";
+    }
     if (f == "tf") {
         // 24 points per workgroup: 256 workgroups at P = 2048, grid-stride beyond
         const int g = std::max(2, 256 / a.B);
