@@ -57,9 +57,12 @@ struct mdg_ctx {
     Buffer opt[12];
     // replayable pipelines of mdg_deconvolute_batch_device, keyed by every argument
     struct CachedGraph {
-        std::vector<unsigned char> key;
-        hipGraphExec_t exec;
-        const char* kernels[kStages];  // kernel names per stage of the captured pipeline
+        std::vector<unsigned char> key;  // everything but the caller's array addresses
+        hipGraph_t graph = nullptr;      // kept for its kernel nodes' argument copies
+        hipGraphExec_t exec = nullptr;
+        std::vector<hipGraphNode_t> knodes;  // kernel nodes, all (BatchArgs, Workspace, ...)
+        BatchArgs cur;                   // the arguments the exec's nodes hold now
+        const char* kernels[kStages];    // kernel names per stage of the captured pipeline
     };
     std::vector<CachedGraph> graphs;
     const char* stage_kernel[kStages] = {};  // kernels the last pipeline launched, per stage
@@ -238,8 +241,13 @@ int ensure_chain(mdg_ctx* c, size_t bytes) {
     return rc;
 }
 
+void destroy_graph(mdg_ctx::CachedGraph& ge) {
+    (void)hipGraphExecDestroy(ge.exec);
+    (void)hipGraphDestroy(ge.graph);
+}
+
 void drop_graphs(mdg_ctx* c) {
-    for (auto& ge : c->graphs) (void)hipGraphExecDestroy(ge.exec);
+    for (auto& ge : c->graphs) destroy_graph(ge);
     c->graphs.clear();
 }
 
@@ -306,10 +314,16 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
             w.chain_P = P;
         }
     }
+    // MDG_DIAG_SKIP=smooth,mse: throughput diagnostics only (tools/stream_diag.py);
+    // the skipped stage's outputs are stale, so results are wrong
+    const char* skip = std::getenv("MDG_DIAG_SKIP");
+    const bool skip_smooth = skip && std::strstr(skip, "smooth"), skip_mse = skip && std::strstr(skip, "mse");
     {
         StageTimer t(c, ST_PREP);
         launch_prep(a, w, st);
         kn[ST_PREP] = "k_prep";
+        if (const char* e = std::getenv("MDG_DIAG_PAD"))
+            for (int k = std::atoi(e); k > 0; --k) launch_diag_nop(a, w, st);
     }
     if (ma) {
         if ((int64_t)(s->smooth_window / 2) > a.N) {
@@ -317,7 +331,7 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
             std::vector<int32_t> pan(a.B, MDG_REFERENCE_PANIC);
             HIPCHK(hipMemcpyAsync(w.status, pan.data(), sizeof(int32_t) * a.B, hipMemcpyHostToDevice, st));
             HIPCHK(hipStreamSynchronize(st));
-        } else {
+        } else if (!skip_smooth) {
             StageTimer t(c, ST_SMOOTH);
             kn[ST_SMOOTH] = launch_smooth(a, w, (int)s->smooth_iterations, (int)s->smooth_window, st);
         }
@@ -353,11 +367,11 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
         launch_retain(a, w, st);
         kn[ST_RETAIN] = "k_retain<1024>";
     }
-    {
-        StageTimer t(c, ST_MSE);
-        kn[ST_MSE] = launch_mse(a, w, nparts, st);
-    }
-    {
+    if (!skip_mse) {
+        {
+            StageTimer t(c, ST_MSE);
+            kn[ST_MSE] = launch_mse(a, w, nparts, st);
+        }
         StageTimer t(c, ST_MSE_REDUCE);
         launch_mse_final(a, w, nparts, st);
     }
@@ -675,10 +689,49 @@ int mdg_ctx_last_smoothed(mdg_ctx* c, size_t spectrum, double* out, size_t n) {
     return MDG_OK;
 }
 
-// run_pipeline through a cached hipGraph: the whole launch sequence (about 26
-// kernels at the default settings) replays as one graph launch. Captured on the
-// context's own stream, launched on the current one; keyed by the bytes of every
-// argument, the settings and the workspace addresses (a reallocation re-keys).
+// the caller's array addresses in a BatchArgs (inputs and outputs): not part of a
+// graph's key; a replay with other addresses rewrites them in the graph's nodes
+void clear_io(BatchArgs& a) {
+    a.x = a.y = a.sb = nullptr;
+    a.out = nullptr;
+    a.out_count = nullptr;
+    a.out_mse = nullptr;
+    a.out_status = nullptr;
+}
+
+bool same_io(const BatchArgs& p, const BatchArgs& q) {
+    return p.x == q.x && p.y == q.y && p.sb == q.sb && p.out == q.out && p.out_count == q.out_count &&
+           p.out_mse == q.out_mse && p.out_status == q.out_status;
+}
+
+// Point a cached graph at another call's arrays: every pipeline kernel takes
+// (BatchArgs, Workspace, ...) by value (launch_k, mdg_kernels.hpp; a node whose
+// kernel was not launched that way fails the call over to a new capture), so the
+// node's copy of argument 0 is rewritten, and argument 1's smooth_ptr where it aliased y (the
+// identity smoother), then the node's arguments are pushed into the exec.
+int repoint_graph(mdg_ctx::CachedGraph& ge, const BatchArgs& a) {
+    for (hipGraphNode_t nd : ge.knodes) {
+        hipKernelNodeParams p{};
+        HIPCHK(hipGraphKernelNodeGetParams(nd, &p));
+        if (!is_pipeline_kernel(p.func) || !p.kernelParams || !p.kernelParams[0] || !p.kernelParams[1])
+            return MDG_ERR_HIP;
+        BatchArgs* na = (BatchArgs*)p.kernelParams[0];
+        Workspace* nw = (Workspace*)p.kernelParams[1];
+        if (nw->smooth_ptr == ge.cur.y) nw->smooth_ptr = a.y;
+        std::memcpy(na, &a, sizeof(BatchArgs));
+        HIPCHK(hipGraphExecKernelNodeSetParams(ge.exec, nd, &p));
+    }
+    ge.cur = a;
+    return MDG_OK;
+}
+
+// run_pipeline through a cached hipGraph: the whole launch sequence (about 20
+// kernels at B = 1 and the default settings) replays as one graph launch.
+// Captured on the context's own stream, launched on the current one; keyed by
+// the bytes of every argument except the caller's array addresses, the settings
+// and the workspace addresses (a reallocation re-keys). A call with other arrays
+// rewrites the nodes' arguments (repoint_graph) instead of capturing again, so
+// a stream of calls on distinct device buffers replays one graph.
 // Not used while stages are being timed, or for the reference-panic shape
 // (host-synchronous path); MDG_GRAPHS=0 disables it.
 int run_pipeline_graphed(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
@@ -698,10 +751,12 @@ int run_pipeline_graphed(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
         drop_graphs(c);
         c->graphs_gen = c->ws_gen;
     }
+    BatchArgs ka = a;
+    clear_io(ka);
     std::vector<unsigned char> key(sizeof(BatchArgs) + sizeof(mdg_settings) + 2 * sizeof(void*) +
                                    sizeof(size_t));
     unsigned char* k = key.data();
-    std::memcpy(k, &a, sizeof(BatchArgs));
+    std::memcpy(k, &ka, sizeof(BatchArgs));
     k += sizeof(BatchArgs);
     std::memcpy(k, s, sizeof(mdg_settings));
     k += sizeof(mdg_settings);
@@ -710,42 +765,61 @@ int run_pipeline_graphed(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     std::memcpy(k, &c->chain.p, sizeof(void*));
     k += sizeof(void*);
     std::memcpy(k, &c->chain.bytes, sizeof(size_t));
-    hipGraphExec_t exec = nullptr;
+    mdg_ctx::CachedGraph* hit = nullptr;
     for (auto& ge : c->graphs)
-        if (ge.key == key) {
-            exec = ge.exec;
-            std::memcpy(c->stage_kernel, ge.kernels, sizeof(ge.kernels));
-        }
-    if (!exec) {
-        hipStream_t user = c->stream;
-        c->stream = c->own;
-        HIPCHK(hipStreamBeginCapture(c->own, hipStreamCaptureModeRelaxed));
-        rc = run_pipeline(c, a, s);
-        hipGraph_t graph = nullptr;
-        const hipError_t e = hipStreamEndCapture(c->own, &graph);
-        c->stream = user;
-        if (rc || e != hipSuccess) {
-            if (graph) (void)hipGraphDestroy(graph);
-            return rc ? rc : hip_fail(e);
-        }
-        const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-        (void)hipGraphDestroy(graph);
-        if (ei != hipSuccess) return hip_fail(ei);
-        if (c->graphs.size() >= 8) {
-            (void)hipGraphExecDestroy(c->graphs.front().exec);
-            c->graphs.erase(c->graphs.begin());
-        }
-        mdg_ctx::CachedGraph cg;
-        cg.key = std::move(key);
-        cg.exec = exec;
-        std::memcpy(cg.kernels, c->stage_kernel, sizeof(cg.kernels));
-        c->graphs.push_back(std::move(cg));
-    } else {
+        if (ge.key == key) hit = &ge;
+    if (hit && !same_io(hit->cur, a) && repoint_graph(*hit, a)) {
+        // a graph whose nodes could not be rewritten is captured again
+        destroy_graph(*hit);
+        c->graphs.erase(c->graphs.begin() + (hit - c->graphs.data()));
+        hit = nullptr;
+    }
+    if (hit) {
+        std::memcpy(c->stage_kernel, hit->kernels, sizeof(hit->kernels));
         // host-side state run_pipeline would have set
         c->last_B = a.B;
         c->last_N = a.N;
         c->last_smoothed = ma;
+        HIPCHK(hipGraphLaunch(hit->exec, c->stream));
+        return MDG_OK;
     }
+    hipStream_t user = c->stream;
+    c->stream = c->own;
+    HIPCHK(hipStreamBeginCapture(c->own, hipStreamCaptureModeRelaxed));
+    rc = run_pipeline(c, a, s);
+    hipGraph_t graph = nullptr;
+    const hipError_t e = hipStreamEndCapture(c->own, &graph);
+    c->stream = user;
+    if (rc || e != hipSuccess) {
+        if (graph) (void)hipGraphDestroy(graph);
+        return rc ? rc : hip_fail(e);
+    }
+    mdg_ctx::CachedGraph cg;
+    cg.graph = graph;
+    size_t nn = 0;
+    hipError_t eg = hipGraphGetNodes(graph, nullptr, &nn);
+    std::vector<hipGraphNode_t> nodes(nn);
+    if (eg == hipSuccess && nn) eg = hipGraphGetNodes(graph, nodes.data(), &nn);
+    for (size_t i = 0; eg == hipSuccess && i < nn; ++i) {
+        hipGraphNodeType t;
+        eg = hipGraphNodeGetType(nodes[i], &t);
+        if (eg == hipSuccess && t == hipGraphNodeTypeKernel) cg.knodes.push_back(nodes[i]);
+    }
+    hipGraphExec_t exec = nullptr;
+    if (eg == hipSuccess) eg = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    if (eg != hipSuccess) {
+        (void)hipGraphDestroy(graph);
+        return hip_fail(eg);
+    }
+    if (c->graphs.size() >= 8) {
+        destroy_graph(c->graphs.front());
+        c->graphs.erase(c->graphs.begin());
+    }
+    cg.key = std::move(key);
+    cg.exec = exec;
+    cg.cur = a;
+    std::memcpy(cg.kernels, c->stage_kernel, sizeof(cg.kernels));
+    c->graphs.push_back(std::move(cg));
     HIPCHK(hipGraphLaunch(exec, c->stream));
     return MDG_OK;
 }

@@ -16,6 +16,8 @@
 #include "mdg_chain_asm.inc"
 
 #include <cstdlib>
+#include <mutex>
+#include <vector>
 #include <string>
 #include <type_traits>
 
@@ -3561,8 +3563,36 @@ __global__ void k_synth_y(const double* __restrict__ x, int64_t n,
 // ----------------------------------------------------------------------------------
 static inline unsigned cdiv(int64_t a, int64_t b) { return (unsigned)((a + b - 1) / b); }
 
+namespace {
+std::mutex g_pk_mu;
+std::vector<const void*> g_pk;  // pipeline kernels launched so far (a few dozen)
+}  // namespace
+
+void note_pipeline_kernel(const void* f) {
+    std::lock_guard<std::mutex> g(g_pk_mu);
+    if (std::find(g_pk.begin(), g_pk.end(), f) == g_pk.end()) g_pk.push_back(f);
+}
+
+bool is_pipeline_kernel(const void* f) {
+    std::lock_guard<std::mutex> g(g_pk_mu);
+    return std::find(g_pk.begin(), g_pk.end(), f) != g_pk.end();
+}
+
 void launch_prep(const BatchArgs& a, const Workspace& w, hipStream_t st) {
-    hipLaunchKernelGGL(k_prep, dim3(cdiv(a.B, 64)), dim3(64), 0, st, a, w);
+    launch_k(k_prep, dim3(cdiv(a.B, 64)), dim3(64), 0, st, a, w);
+}
+
+// throughput diagnostic (MDG_DIAG_PAD, mdg_capi.hip): a launch that does nothing,
+// with the pipeline's kernel arguments
+__global__ void k_diag_nop(BatchArgs a, Workspace w) {
+    if (a.B < 0) w.status[0] = 0;
+}
+__global__ void k_diag_nop_small(int32_t* p, int b) {
+    if (b < 0) p[0] = 0;
+}
+void launch_diag_nop(const BatchArgs& a, const Workspace& w, hipStream_t st) {
+    if (std::getenv("MDG_DIAG_PAD_SMALL")) hipLaunchKernelGGL(k_diag_nop_small, dim3(1), dim3(64), 0, st, w.status, a.B);
+    else launch_k(k_diag_nop, dim3(1), dim3(64), 0, st, a, w);
 }
 template <int WS>
 static const char* launch_waves(const BatchArgs& a, const Workspace& w, int iters, hipStream_t st) {
@@ -3570,7 +3600,7 @@ static const char* launch_waves(const BatchArgs& a, const Workspace& w, int iter
     constexpr int RAWSLOT = ((U * 8 + 255) / 256) * 32;
     const size_t lds = sizeof(double) * (4 * RAWSLOT + (size_t)iters * 4 * U);
     const int waves = (iters + 3) / 4 * 4;
-    hipLaunchKernelGGL(k_smooth_waves<WS>, dim3(a.B), dim3(64 * waves), lds, st, a, w, iters);
+    launch_k(k_smooth_waves<WS>, dim3(a.B), dim3(64 * waves), lds, st, a, w, iters);
     static const char* names[] = {"", "", "k_smooth_waves<2>", "k_smooth_waves<3>", "k_smooth_waves<4>",
                                   "k_smooth_waves<5>", "k_smooth_waves<6>", "k_smooth_waves<7>",
                                   "k_smooth_waves<8>", "k_smooth_waves<9>", "", "k_smooth_waves<11>"};
@@ -3580,7 +3610,7 @@ static const char* launch_waves(const BatchArgs& a, const Workspace& w, int iter
 template <int WS>
 static const char* launch_pipe(const BatchArgs& a, const Workspace& w, int iters, hipStream_t st) {
     const int spw = 64 / iters;
-    hipLaunchKernelGGL(k_smooth_pipe<WS>, dim3(cdiv(a.B, spw)), dim3(64), 0, st, a, w, iters, spw);
+    launch_k(k_smooth_pipe<WS>, dim3(cdiv(a.B, spw)), dim3(64), 0, st, a, w, iters, spw);
     static const char* names[] = {"", "", "k_smooth_pipe<2>", "k_smooth_pipe<3>", "k_smooth_pipe<4>",
                                   "k_smooth_pipe<5>", "k_smooth_pipe<6>", "k_smooth_pipe<7>",
                                   "k_smooth_pipe<8>", "k_smooth_pipe<9>", "", "k_smooth_pipe<11>"};
@@ -3593,10 +3623,10 @@ static const char* launch_chain(const BatchArgs& a, const Workspace& w, int iter
     const char* excl_env = std::getenv("MDG_CHAIN_EXCL");  // 0 = never (measurements)
     const bool excl = (int)grid <= kChainExclMax && !(excl_env && excl_env[0] == '0');
     if (excl) {
-        hipLaunchKernelGGL((k_smooth_chain<WS, true>), dim3(grid), dim3(64 * (2 + kChainScalers)), 0, st,
+        launch_k((k_smooth_chain<WS, true>), dim3(grid), dim3(64 * (2 + kChainScalers)), 0, st,
                            a, w, iters);
     } else {
-        hipLaunchKernelGGL((k_smooth_chain<WS, false>), dim3(grid), dim3(64 * (2 + kChainScalers)), 0, st,
+        launch_k((k_smooth_chain<WS, false>), dim3(grid), dim3(64 * (2 + kChainScalers)), 0, st,
                            a, w, iters);
     }
     static const char* names[2][9] = {
@@ -3657,38 +3687,38 @@ const char* launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int
             default: break;
         }
     }
-    hipLaunchKernelGGL(k_smooth, dim3(cdiv(a.B, 64)), dim3(64), 0, st, a, w, iters, ws);
+    launch_k(k_smooth, dim3(cdiv(a.B, 64)), dim3(64), 0, st, a, w, iters, ws);
     return "k_smooth";
 }
 void launch_flags(const BatchArgs& a, const Workspace& w, hipStream_t st) {
-    hipLaunchKernelGGL(k_flags, dim3(cdiv(a.N, 256), a.B), dim3(256), 0, st, a, w);
+    launch_k(k_flags, dim3(cdiv(a.N, 256), a.B), dim3(256), 0, st, a, w);
 }
 const char* launch_peaks(const BatchArgs& a, const Workspace& w, int detector_only, hipStream_t st) {
     const int nch = cdiv(w.W, kPkWords);
     static_assert(kPkWords == 256, "k_flags clears ceil(W / 256) slots");
     if (std::getenv("MDG_PEAKS_2PASS")) {  // the two-kernel form, for comparison
-        hipLaunchKernelGGL(k_peaks_count, dim3(nch, a.B), dim3(kPkWords), 0, st, a, w, detector_only);
-        hipLaunchKernelGGL(k_peaks_write, dim3(nch, a.B), dim3(kPkWords), 0, st, a, w, detector_only);
+        launch_k(k_peaks_count, dim3(nch, a.B), dim3(kPkWords), 0, st, a, w, detector_only);
+        launch_k(k_peaks_write, dim3(nch, a.B), dim3(kPkWords), 0, st, a, w, detector_only);
         return "k_flags+k_peaks_count+k_peaks_write";
     }
-    hipLaunchKernelGGL(k_peaks, dim3(nch, a.B), dim3(kPkWords), 0, st, a, w, detector_only);
+    launch_k(k_peaks, dim3(nch, a.B), dim3(kPkWords), 0, st, a, w, detector_only);
     return "k_flags+k_peaks";
 }
 void launch_scores(const BatchArgs& a, const Workspace& w, hipStream_t st) {
     const int gx = std::max(1, std::min(64, 4096 / std::max(1, a.B)));
-    hipLaunchKernelGGL(k_scores, dim3(gx, a.B), dim3(256), 0, st, a, w);
+    launch_k(k_scores, dim3(gx, a.B), dim3(256), 0, st, a, w);
 }
 const char* launch_select(const BatchArgs& a, const Workspace& w, int detector_only,
                           double threshold, hipStream_t st) {
     if (detector_only) {
-        hipLaunchKernelGGL(k_select_detector_only, dim3(16, a.B), dim3(256), 0, st, a, w);
+        launch_k(k_select_detector_only, dim3(16, a.B), dim3(256), 0, st, a, w);
         return "k_select_detector_only";
     }
-    hipLaunchKernelGGL(k_select<1024>, dim3(a.B), dim3(1024), 0, st, a, w, threshold);
+    launch_k(k_select<1024>, dim3(a.B), dim3(1024), 0, st, a, w, threshold);
     return "k_scores+k_select<1024>";
 }
 void launch_fit_init(const BatchArgs& a, const Workspace& w, int gx, hipStream_t st) {
-    hipLaunchKernelGGL(k_fit_init, dim3(gx, a.B), dim3(256), 0, st, a, w);
+    launch_k(k_fit_init, dim3(gx, a.B), dim3(256), 0, st, a, w);
 }
 // Fit kernel choice by measurement (tools/fit_sweep.sh, P = 2048, ms per 10 launches):
 //   B=1 tf 0.215 / dpp 0.277 / plain 0.81;  B=2 tf 0.369 / dpp 0.428;
@@ -3715,65 +3745,65 @@ const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int i
         const int g = std::max(2, 128 / a.B);
         if (f == "tw4") {  // 4 evaluator waves: 2 peak blocks x 2 point subsets (Q = 60)
             using SH = TwShape<60, 2, 2>;
-            hipLaunchKernelGGL(k_fit_sup_tw<SH>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
+            launch_k(k_fit_sup_tw<SH>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
             return "k_fit_sup_tw<60, 2, 2>";
         }
         if (f == "tw7") {  // 7 evaluator waves: 1 peak block x 7 point subsets (Q = 63)
             using SH = TwShape<63, 1, 7>;
-            hipLaunchKernelGGL(k_fit_sup_tw<SH>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
+            launch_k(k_fit_sup_tw<SH>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
             return "k_fit_sup_tw<63, 1, 7>";
         }
         if (f == "tw3") {
             using SH = TwShape<63, 1, 3>;
-            hipLaunchKernelGGL(k_fit_sup_tw<SH>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
+            launch_k(k_fit_sup_tw<SH>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
             return "k_fit_sup_tw<63, 1, 3>";
         }
         if (f == "tw9") {
             using SH = TwShape<63, 1, 9>;
-            hipLaunchKernelGGL(k_fit_sup_tw<SH>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
+            launch_k(k_fit_sup_tw<SH>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
             return "k_fit_sup_tw<63, 1, 9>";
         }
         if (f == "tw14") {  // 2 peak blocks x 7 point subsets
             using SH = TwShape<63, 2, 7>;
-            hipLaunchKernelGGL(k_fit_sup_tw<SH>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
+            launch_k(k_fit_sup_tw<SH>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
             return "k_fit_sup_tw<63, 2, 7>";
         }
         using SH = TwDefault;
-        hipLaunchKernelGGL(k_fit_sup_tw<SH>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
+        launch_k(k_fit_sup_tw<SH>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
         return "k_fit_sup_tw<63, 2, 3>";
     }
     if (f == "tf") {
         // 24 points per workgroup: 256 workgroups at P = 2048, grid-stride beyond
         const int g = std::max(2, 256 / a.B);
-        hipLaunchKernelGGL(k_fit_sup_tf, dim3(g, a.B), dim3(64 * (kTfEW + 1)), 0, st, a, w, it);
+        launch_k(k_fit_sup_tf, dim3(g, a.B), dim3(64 * (kTfEW + 1)), 0, st, a, w, it);
         return "k_fit_sup_tf";
     } else if (f == "dpp") {
         // 32 points per workgroup: 192 workgroups at P = 2048, grid-stride beyond
         const int g = std::max(64, std::min(512, 1024 / a.B));
-        hipLaunchKernelGGL(k_fit_sup_dpp, dim3(g, a.B), dim3(256), 0, st, a, w, it);
+        launch_k(k_fit_sup_dpp, dim3(g, a.B), dim3(256), 0, st, a, w, it);
         return "k_fit_sup_dpp";
     } else if (f == "mfma") {
         // experiment only (not bit-exact): 64 points per workgroup
         const int g = std::max(1, std::min(2048, (3 * (a.N / 2 + 2) + 63) / 64));
         const int parts = std::max(1, std::min(g, 8192 / a.B));
-        hipLaunchKernelGGL(k_fit_sup_mfma, dim3(parts * a.B), dim3(256), 0, st, a, w, it);
+        launch_k(k_fit_sup_mfma, dim3(parts * a.B), dim3(256), 0, st, a, w, it);
         return "k_fit_sup_mfma";
     } else if (f == "split") {
         // 16 points per 1024-thread workgroup: 3P/16 workgroups per spectrum (384 at
         // P = 2048) keep every CU busy; grid-stride beyond that
         const int g = std::max(64, std::min(1024, 2048 / a.B));
-        hipLaunchKernelGGL((k_fit_sup_split<16, 128, 1024>), dim3(g, a.B), dim3(1024), 0, st, a, w, it);
+        launch_k((k_fit_sup_split<16, 128, 1024>), dim3(g, a.B), dim3(1024), 0, st, a, w, it);
         return "k_fit_sup_split<16, 128, 1024>";
     }
     // gx 256-thread workgroups per spectrum (24: one point per thread at P = 2048)
-    hipLaunchKernelGGL(k_fit_sup, dim3(gx * a.B), dim3(256), 0, st, a, w, it);
+    launch_k(k_fit_sup, dim3(gx * a.B), dim3(256), 0, st, a, w, it);
     return "k_fit_sup";
 }
 void launch_fit_update(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st) {
-    hipLaunchKernelGGL(k_fit_update, dim3(gx, a.B), dim3(256), 0, st, a, w, it);
+    launch_k(k_fit_update, dim3(gx, a.B), dim3(256), 0, st, a, w, it);
 }
 void launch_retain(const BatchArgs& a, const Workspace& w, hipStream_t st) {
-    hipLaunchKernelGGL(k_retain<1024>, dim3(a.B), dim3(1024), 0, st, a, w);
+    launch_k(k_retain<1024>, dim3(a.B), dim3(1024), 0, st, a, w);
 }
 // MSE kernel: quad (k_mse_quad<NPT>, default) | n (k_mse_partial_n<256, 2>, one
 // division per term) | plain (k_mse_partial + k_mse_final); MDG_MSE overrides
@@ -3798,22 +3828,22 @@ int mse_nparts(const BatchArgs& a) {
 const char* launch_mse(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st) {
     if (mse_kind() == "quad") {
         if (mse_quad_npt(a) == 2) {
-            hipLaunchKernelGGL(k_mse_quad<2>, dim3(nparts * a.B), dim3(256), 0, st, a, w, nparts);
+            launch_k(k_mse_quad<2>, dim3(nparts * a.B), dim3(256), 0, st, a, w, nparts);
             return "k_mse_quad<2>";
         }
-        hipLaunchKernelGGL(k_mse_quad<1>, dim3(nparts * a.B), dim3(256), 0, st, a, w, nparts);
+        launch_k(k_mse_quad<1>, dim3(nparts * a.B), dim3(256), 0, st, a, w, nparts);
         return "k_mse_quad<1>";
     }
     if (mse_kind() == "n") {
-        hipLaunchKernelGGL((k_mse_partial_n<256, 2>), dim3(nparts * a.B), dim3(256), 0, st, a, w, nparts);
+        launch_k((k_mse_partial_n<256, 2>), dim3(nparts * a.B), dim3(256), 0, st, a, w, nparts);
         return "k_mse_partial_n<256, 2>";
     }
-    hipLaunchKernelGGL(k_mse_partial<256>, dim3(nparts * a.B), dim3(256), 0, st, a, w, nparts);
+    launch_k(k_mse_partial<256>, dim3(nparts * a.B), dim3(256), 0, st, a, w, nparts);
     return "k_mse_partial<256>+k_mse_final";
 }
 void launch_mse_final(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st) {
     if (mse_kind() != "plain") return;  // k_mse_quad / k_mse_partial_n fold the partials
-    hipLaunchKernelGGL(k_mse_final, dim3(a.B), dim3(64), 0, st, a, w, nparts);
+    launch_k(k_mse_final, dim3(a.B), dim3(64), 0, st, a, w, nparts);
 }
 void launch_mse_exact(const double* sup, const double* y, int64_t n, const ExactRegions& r,
                       double* scratch, double* out, hipStream_t st) {

@@ -5,6 +5,8 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <tuple>
+#include <utility>
 
 #include "../../include/mdgpu.h"
 #include "mdg_common.hpp"
@@ -103,7 +105,31 @@ struct ExactRegions {
 void launch_mse_exact(const double* sup, const double* y, int64_t n, const ExactRegions& r,
                       double* scratch, double* out, hipStream_t st);
 
+// Every pipeline kernel takes (BatchArgs, Workspace, ...) by value and is launched
+// through launch_k, which the compiler holds to that signature and which records
+// the kernel as one whose graph nodes may be re-pointed at another call's arrays
+// (mdg_capi.hip repoint_graph rewrites argument 0 of such nodes only).
+void note_pipeline_kernel(const void* f);
+bool is_pipeline_kernel(const void* f);
+
+template <class K, class T, size_t... I>
+inline void launch_k_tuple(K k, dim3 g, dim3 b, size_t sh, hipStream_t st, const BatchArgs& a,
+                           const Workspace& w, T& t, std::index_sequence<I...>) {
+    void* args[] = {(void*)&a, (void*)&w, (void*)&std::get<I>(t)..., nullptr};
+    (void)hipLaunchKernel((const void*)k, g, b, args, sh, st);
+}
+
+template <typename... P, typename... X>
+inline void launch_k(void (*k)(BatchArgs, Workspace, P...), dim3 g, dim3 b, size_t sh, hipStream_t st,
+                     const BatchArgs& a, const Workspace& w, X... x) {
+    static_assert(sizeof...(P) == sizeof...(X), "kernel argument count");
+    note_pipeline_kernel((const void*)k);
+    std::tuple<P...> t{static_cast<P>(x)...};
+    launch_k_tuple(k, g, b, sh, st, a, w, t, std::index_sequence_for<P...>{});
+}
+
 void launch_prep(const BatchArgs& a, const Workspace& w, hipStream_t st);
+void launch_diag_nop(const BatchArgs& a, const Workspace& w, hipStream_t st);
 const char* launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int ws, hipStream_t st);
 void launch_flags(const BatchArgs& a, const Workspace& w, hipStream_t st);
 const char* launch_peaks(const BatchArgs& a, const Workspace& w, int detector_only, hipStream_t st);

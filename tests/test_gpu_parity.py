@@ -643,6 +643,55 @@ def test_par_deconvolute_spectra_rccl_world1():
         dist.destroy_process_group()
 
 
+def test_graph_repoint_in_flight_bit_exact():
+    """One cached pipeline graph serves calls on distinct device arrays
+    (mdg_capi.hip repoint_graph): every call here passes its own x/y/sb rows and
+    writes straight into its own result rows, and all calls are enqueued on two
+    contexts before any synchronisation, so a graph's node arguments are
+    rewritten while earlier launches of it are still queued or running (the
+    CUDA/HIP contract: launches already enqueued are not affected). Every call
+    must equal the oracle bit for bit, and the MSE within 1e-12."""
+    torch = pytest.importorskip("torch")
+    names = ["blood_02", "blood_05", "blood_07", "blood_11", "blood_13", "blood_16"]
+    cases = [load_case(nm) for nm in names]
+    refs = [oracle.deconvolute(c[0], c[1], c[2], c[3]) for c in cases]
+    dev = torch.device("cuda", 0)
+    n = cases[0][1].size
+    assert all(c[1].size == n for c in cases)
+    cap = n // 2 + 2
+    X = torch.from_numpy(np.stack([c[0] for c in cases])).to(dev)
+    Y = torch.from_numpy(np.stack([c[1] for c in cases])).to(dev)
+    SB = torch.tensor([c[2] for c in cases], dtype=torch.float64, device=dev)
+    ctxs = [nat.Context(0) for _ in range(2)]
+    try:
+        s = nat.default_settings()
+        steps = 5 * len(cases)
+        res_out = torch.zeros((steps, cap, 3), dtype=torch.float64, device=dev)
+        res_cnt = torch.zeros(steps, dtype=torch.int32, device=dev)
+        res_mse = torch.zeros(steps, dtype=torch.float64, device=dev)
+        res_st = torch.full((steps,), -1, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
+        for k in range(steps):
+            c = ctxs[k % 2]
+            j = (k * 5) % len(cases)
+            rc = nat.lib().mdg_deconvolute_batch_device(
+                c.handle, 1, n, X[j].data_ptr(), 0, Y[j].data_ptr(), n, SB[j].data_ptr(),
+                ctypes.byref(s), None, 0, res_out[k].data_ptr(), cap, res_cnt[k].data_ptr(),
+                res_mse[k].data_ptr(), res_st[k].data_ptr())
+            assert rc == 0, nat.strerror(rc)
+        for c in ctxs:
+            c.synchronize()
+        for k in range(steps):
+            o = refs[(k * 5) % len(cases)]
+            assert int(res_st[k]) == o.status == 0, k
+            cnt = int(res_cnt[k])
+            assert np.array_equal(res_out[k, :cnt].cpu().numpy(), o.params), k
+            assert abs(float(res_mse[k]) - o.mse) <= 1e-12 * abs(o.mse), k
+    finally:
+        for c in ctxs:
+            c.close()
+
+
 def test_concurrent_contexts_stream_bit_exact():
     """The bench's stream mode: 6 contexts, each on its own stream,
     replay their captured pipelines on a stream of distinct spectra (input row

@@ -1,6 +1,9 @@
 set -o pipefail
 mkdir -p gpurun_out
-for rep in 1 2; do for F in tf tw7; do
-  MDG_FITSUP=$F timeout -k 10 600 python bench.py --configs 4 --no-cpu-baseline --steps 60 > gpurun_out/c4.log 2>&1 || exit $?
-  python -c "import json;d=json.loads([l for l in open('gpurun_out/c4.log') if l.startswith('{')][0]);v=d['configs']['configs[4]'];print('$F', round(v['value']), round(v['ms_per_step'],3))"
-done; done
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu > gpurun_out/pt_all.log 2>&1 || { tail -30 gpurun_out/pt_all.log; exit 1; }
+tail -2 gpurun_out/pt_all.log
+for io in copy direct copy direct; do
+  F=""; [ $io = copy ] && F="--copy-io"
+  timeout -k 10 300 python bench.py --no-cpu-baseline --no-configs --no-profile --steps 400 $F > gpurun_out/io.log 2>&1 || exit $?
+  python -c "import json;d=json.loads([l for l in open('gpurun_out/io.log') if l.startswith('{')][0]);print('$io', round(d['value']), round(d['latency_ms'],3), round(d['host_submit_ms_per_step'],4))"
+done
