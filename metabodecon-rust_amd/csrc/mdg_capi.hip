@@ -182,7 +182,6 @@ int ensure_workspace(mdg_ctx* c, int B, int N) {
         const size_t o_xok = take(Bs * 4), o_unsafe = take(Bs * 16), o_uk = take(Bs * 4);
         const size_t o_pcnt = take(Bs * 2 * ((W + 255) / 256) * 4);
         const size_t o_mcnt = take(Bs * 4);
-        const size_t o_fitq = take(Bs * 64 * 4);
 
         if (c->arena.p) (void)hipFree(c->arena.p);
         c->arena.p = nullptr;
@@ -223,7 +222,6 @@ int ensure_workspace(mdg_ctx* c, int B, int N) {
         w.unsafe_kept = (int32_t*)(base + o_uk);
         w.peak_cnt = (int32_t*)(base + o_pcnt);
         w.mse_done = (int32_t*)(base + o_mcnt);
-        w.fitq = (int32_t*)(base + o_fitq);
         // k_mse_partial_n's arrival counters start (and are always left) at zero
         HIPCHK(hipMemset(w.mse_done, 0, Bs * 4));
 
@@ -353,10 +351,6 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
         launch_fit_init(a, w, gupd, st);
         kn[ST_FIT_INIT] = "k_fit_init";
     }
-    if (fused && fit_sup_single_launch(a) && s->fit_iterations > 0) {
-        StageTimer t(c, ST_FIT_SUP);
-        kn[ST_FIT_SUP] = launch_fit_all(a, w, (int)s->fit_iterations, st);
-    } else
     for (uint32_t it = 0; it < s->fit_iterations; ++it) {
         {
             StageTimer t(c, ST_FIT_SUP);

@@ -400,8 +400,6 @@ __global__ void k_prep(BatchArgs a, Workspace w) {
     w.det_count[s] = 0;
     w.sel_count[s] = 0;
     w.kept_count[s] = 0;
-    __hip_atomic_store(&w.fitq[64 * s], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&w.fitq[64 * s + 32], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (int p = 0; p < w.chain_P; ++p) w.chain_flags[((size_t)s * w.chain_P + p) * 32] = 0;
 }
 
@@ -2825,170 +2823,6 @@ __global__ __launch_bounds__(64 * (SH::EW + 1)) void k_fit_sup_tw(BatchArgs a, W
     else fit_tw_body<false, SH>(w, s, P, it, T);
 }
 
-// K6i  term-fold fit, every iteration in ONE launch ("twq"): the (iteration,
-// tile) items of a spectrum, in order, go to the resident workgroups through an
-// atomic head counter; an item of iteration it starts once `done` (items
-// finished) reaches it * tiles, which it first does when every item of the
-// earlier iterations is finished, since none of iteration it can have started
-// before. A workgroup only waits for items claimed before its own, by running
-// workgroups, so the queue cannot deadlock whatever is resident beside it (other
-// streams' kernels included). The arithmetic is fit_tw_body's, bit for bit.
-// Hand-offs across workgroups and XCDs (MI355X_MICROARCH.md, visibility table
-// row 1): the parameters and stencils an item writes are sc1 (write-through)
-// stores, drained by the storing (fold) wave's vmcnt(0) before its lane 0 adds to
-// `done`; a consumer's lane polls `done` with sc1 loads, the workgroup joins a
-// barrier, and every load of those bytes is an sc1 load. Saves the 9 launches
-// (and their command-processor time) of a per-iteration fit.
-__device__ __forceinline__ void st_sc1(double* p, double v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-constexpr int kTwqSpin = 1 << 22;  // polls of `done` (with s_sleep) before giving up
-
-template <bool FAST, class SH, int D>
-__device__ __forceinline__ void twq_item(const Workspace& w, int s, int P, int it, int tile,
-                                         double* T, int32_t* done) {
-    constexpr int QQ = SH::LDS / (2 * SH::RS), J = SH::J, RS = SH::RS, QS = SH::QS, EW = SH::EW;
-    constexpr int PB = J / 64;
-    const size_t base = (size_t)s * w.capD;
-    const int npts = 3 * P;
-    const int nch = (P + J - 1) / J;
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const double* params = params_version(w, base, it);
-    const int p0 = tile * QQ;
-    if (wv != EW) {
-        const int pb = wv % PB, ps = wv / PB;
-        const const_f64_ptr rx = (const_f64_ptr)(w.rx + 3 * base + p0 + ps * QS);
-        double xq[QS];
-#pragma unroll
-        for (int q = 0; q < QS; ++q) xq[q] = rx[q];
-        const int jl = pb * 64 + lane;
-        // the parameters of D chunks in flight: their sc1 loads are served from
-        // beyond this XCD's L2 and take far longer than one chunk's evaluations
-        double f[D], h[D], m[D];
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-            const int j = min(d * J + jl, P - 1);
-            f[d] = ld_sc1(params + 3 * j);
-            h[d] = ld_sc1(params + 3 * j + 1);
-            m[d] = ld_sc1(params + 3 * j + 2);
-        }
-        for (int c0 = 0; c0 < nch; c0 += D) {
-#pragma unroll
-            for (int d = 0; d < D; ++d) {
-                const int c = c0 + d;
-                if (c < nch) {
-                    double* Tb = T + (c & 1) * QQ * RS + ps * QS * RS + jl;
-                    const double cf = f[d], ch = h[d], cm = m[d];
-                    const int j = min((c + D) * J + jl, P - 1);
-                    f[d] = ld_sc1(params + 3 * j);
-                    h[d] = ld_sc1(params + 3 * j + 1);
-                    m[d] = ld_sc1(params + 3 * j + 2);
-#pragma unroll
-                    for (int q = 0; q < QS; ++q) Tb[q * RS] = lorentz_t<FAST>(xq[q], cf, ch, cm);
-                    lds_barrier();
-                }
-            }
-        }
-        lds_barrier();
-    } else {
-        double acc = -0.0;
-        const int q = lane < QQ ? lane : QQ - 1;
-        double one = 1.0;
-        asm volatile("" : "+v"(one));
-        lds_barrier();
-        for (int c = 0; c < nch; ++c) {
-            const double2* row = (const double2*)(T + (c & 1) * QQ * RS + q * RS);
-            const int cn = min(J, P - c * J);
-            if (cn == J) {
-#pragma unroll 16
-                for (int k = 0; k < J / 2; ++k) {
-                    const double2 v = row[k];
-                    acc = __builtin_fma(v.x, one, acc);
-                    acc = __builtin_fma(v.y, one, acc);
-                }
-            } else {
-                const double* r1 = (const double*)row;
-                for (int k = 0; k < cn; ++k) acc = __builtin_fma(r1[k], one, acc);
-            }
-            lds_barrier();
-        }
-        const double ratio = w.ry[3 * base + min(p0 + q, npts - 1)] / acc;
-        const int k = lane < QQ / 3 ? lane : 0;
-        const double r0 = __shfl(ratio, 3 * k, 64);
-        const double r1 = __shfl(ratio, 3 * k + 1, 64);
-        const double r2 = __shfl(ratio, 3 * k + 2, 64);
-        const int pk = p0 / 3 + lane;
-        if (lane < QQ / 3 && pk < P) {
-            double* st = w.stencil + 6 * base + 6 * (size_t)pk;
-            Stencil sq{ld_sc1(st), ld_sc1(st + 1), ld_sc1(st + 2), ld_sc1(st + 3), ld_sc1(st + 4), ld_sc1(st + 5)};
-            sq.y1 = sq.y1 * r0;
-            sq.y2 = sq.y2 * r1;
-            sq.y3 = sq.y3 * r2;
-            mirror_shoulder(sq);
-            st_sc1(st, sq.x1); st_sc1(st + 1, sq.x2); st_sc1(st + 2, sq.x3);
-            st_sc1(st + 3, sq.y1); st_sc1(st + 4, sq.y2); st_sc1(st + 5, sq.y3);
-            double Lv[3];
-            solve(sq, Lv);
-            double* L = (((it + 1) & 1) ? w.params_alt : w.params) + 3 * base + 3 * (size_t)pk;
-            st_sc1(L, Lv[0]); st_sc1(L + 1, Lv[1]); st_sc1(L + 2, Lv[2]);
-            if (!peak_fast_ok(Lv[0], Lv[1], Lv[2]))
-                __hip_atomic_fetch_add(&w.unsafe[4 * s + (it + 1) % 3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        // version it+2's range counter (read by iteration it-1, finished) for iteration it+1
-        if (tile == 0 && lane == 0)
-            __hip_atomic_store(&w.unsafe[4 * s + (it + 2) % 3], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-template <class SH, int D>
-__global__ __launch_bounds__(64 * (SH::EW + 1)) void k_fit_twq(BatchArgs a, Workspace w, int iters_launched) {
-    __shared__ __attribute__((aligned(16))) double T[SH::LDS];
-    __shared__ int s_item[2];
-    __shared__ int s_abort;
-    constexpr int QQ = SH::LDS / (2 * SH::RS);
-    const int s = blockIdx.y;
-    if (w.status[s]) return;
-    const int P = w.sel_count[s];
-    const int iters = w.fit_iters_s ? min(w.fit_iters_s[s], iters_launched) : iters_launched;
-    const int tiles = (3 * P + QQ - 1) / QQ;
-    const int total = iters * tiles;
-    int32_t* head = w.fitq + 64 * s;
-    int32_t* done = head + 32;
-    if (threadIdx.x >> 6 == SH::EW) __builtin_amdgcn_s_setprio(3);
-    if (threadIdx.x == 0) {
-        s_item[0] = __hip_atomic_fetch_add(head, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_abort = 0;
-    }
-    __syncthreads();
-    int buf = 0;
-    int q = __builtin_amdgcn_readfirstlane(s_item[0]);
-    while (q < total) {
-        const int it = q / tiles, tile = q - it * tiles;
-        if (threadIdx.x == 0) {
-            s_item[buf ^ 1] = __hip_atomic_fetch_add(head, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            int spins = 0;
-            while (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < it * tiles) {
-                __builtin_amdgcn_s_sleep(2);
-                if (++spins == kTwqSpin) {
-                    s_abort = 1;
-                    atomicCAS(&w.status[s], 0, (int)MDG_ERR_HIP);
-                    break;
-                }
-            }
-        }
-        __syncthreads();
-        if (__builtin_amdgcn_readfirstlane(s_abort)) break;
-        const int nu = __builtin_amdgcn_readfirstlane(
-            __hip_atomic_load(&w.unsafe[4 * s + it % 3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        if (w.x_ok[s] && nu == 0) twq_item<true, SH, D>(w, s, P, it, tile, T, done);
-        else twq_item<false, SH, D>(w, s, P, it, tile, T, done);
-        q = __builtin_amdgcn_readfirstlane(s_item[buf ^ 1]);
-        buf ^= 1;
-    }
-}
-
 // 1-D grid, spectrum = block % B (as k_mse_partial): round-robin dispatch puts the
 // workgroups a CU holds at once on the same spectrum, so they share its Lorentzians
 // in the scalar cache instead of each streaming another spectrum's table
@@ -3903,24 +3737,6 @@ static std::string fit_choice(const BatchArgs& a) {
 bool fit_sup_fused(const BatchArgs& a) {
     const std::string f = fit_choice(a);
     return f == "tf" || f.rfind("tw", 0) == 0;
-}
-bool fit_sup_single_launch(const BatchArgs& a) { return fit_choice(a) == "twq"; }
-const char* launch_fit_all(const BatchArgs& a, const Workspace& w, int iters, hipStream_t st) {
-    using SH = TwShape<63, 1, 7>;
-    // one workgroup per item of an iteration at P <= 2688 (128 at B = 1)
-    const int g = std::max(2, 128 / a.B);
-    const char* e = std::getenv("MDG_TWQ_D");  // parameter chunks in flight (tuning)
-    const int d = e ? std::atoi(e) : 8;
-    if (d == 2) {
-        launch_k(k_fit_twq<SH, 2>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, iters);
-        return "k_fit_twq<63, 1, 7, 2>";
-    }
-    if (d == 4) {
-        launch_k(k_fit_twq<SH, 4>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, iters);
-        return "k_fit_twq<63, 1, 7, 4>";
-    }
-    launch_k(k_fit_twq<SH, 8>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, iters);
-    return "k_fit_twq<63, 1, 7, 8>";
 }
 const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st) {
     const std::string f = fit_choice(a);

@@ -79,7 +79,6 @@ struct Workspace {
                               // (k_fit_update path: version & 1; fused k_fit_sup_tf: version % 3)
     int32_t* unsafe_kept;     // B: same for the retained Lorentzians
     int32_t* mse_done;        // B: k_mse_partial_n workgroups finished (the last one folds, resets)
-    int32_t* fitq;            // B x 64: k_fit_twq work queue {head at 0, done at 32} (k_prep zeroes)
     int32_t* peak_cnt;        // B x ceil(W/256) u64: k_peaks slots {valid, bordered, kept} per mask chunk
     // k_smooth_chain (allocated on first use; null otherwise)
     double* chain_raw;        // P x B x chain_stride: raw running sums of every pass
@@ -140,9 +139,6 @@ const char* launch_select(const BatchArgs& a, const Workspace& w, int detector_o
 void launch_fit_init(const BatchArgs& a, const Workspace& w, int gx, hipStream_t st);
 // returns true when the launched kernel also did the stencil update (no k_fit_update)
 bool fit_sup_fused(const BatchArgs& a);
-// the whole fit (every iteration) as one launch (k_fit_twq)
-bool fit_sup_single_launch(const BatchArgs& a);
-const char* launch_fit_all(const BatchArgs& a, const Workspace& w, int iters, hipStream_t st);
 const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st);
 void launch_fit_update(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st);
 void launch_retain(const BatchArgs& a, const Workspace& w, hipStream_t st);
