@@ -355,9 +355,16 @@ def test_fit_superposition_kernels_batch(ctx, path, monkeypatch):
         assert abs(mse[s] - o.mse) <= MSE_RTOL * abs(o.mse), s
 
 
-def test_mse_cases(ctx):
+@pytest.mark.parametrize("kernel,near_cap", [("local", None), ("local", "8"), ("local", "0"),
+                                             ("quad", None), ("n", None), ("plain", None)])
+def test_mse_cases(ctx, kernel, near_cap, monkeypatch):
     """The MSE against the oracle: ignore regions (two in one spectrum), a short
-    signal region (sim) and a batch whose spectra differ in peak count."""
+    signal region (sim) and a batch whose spectra differ in peak count -- on every
+    MSE kernel; for k_mse_local also with a tiny near-list capacity (crowded tiles
+    take the direct sum) and none at all (every tile direct)."""
+    monkeypatch.setenv("MDG_MSE", kernel)
+    if near_cap is not None:
+        monkeypatch.setenv("MDG_MSE_NEARCAP", near_cap)
     for name in ["blood_01_water", "blood_02_two_regions_increasing", "sim_05", "synth_128k_2k_s0"]:
         x, y, sb, st, ign = load_case(name)
         o = oracle.deconvolute(x, y, sb, st, ignore=ign)

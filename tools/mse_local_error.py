@@ -1,0 +1,89 @@
+"""Accuracy of the local-expansion MSE (k_mse_local) restated in
+numpy, against a long-double direct sum of the Lorentzians.
+
+    python tools/mse_local_error.py [case ...]
+
+For each golden case (oracle parameters from tests/golden/expected/*.npz) and
+for the synthetic configs[1] spectrum it prints the largest relative error of
+the superposition over the signal region and the relative error of the MSE,
+for the kernel's tile shape (256 points, R = 5, 20 terms) and neighbours.
+"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "metabodecon-rust_amd"), os.path.join(ROOT, "tests", "golden")]
+
+
+def local_sup(xs, P, TP=256, R=5.0, p=20):
+    """The kernel's arithmetic per tile: near Lorentzians direct, far ones as the
+    imaginary parts of -sum_k [sum_j a_j w_j (r w_j)^k] u^k."""
+    f, h, m = P[:, 0], P[:, 1], P[:, 2]
+    sig = np.sqrt(h)
+    a = f / sig
+    out = np.zeros(xs.size)
+    for t0 in range(0, xs.size, TP):
+        xt = xs[t0:t0 + TP]
+        lo, hi = xt.min(), xt.max()
+        t, r = 0.5 * lo + 0.5 * hi, 0.5 * hi - 0.5 * lo
+        dz = (m - t) + 1j * sig
+        far = np.abs(dz) > R * r
+        w = 1.0 / dz[far]
+        c, q = a[far] * w, r * w
+        L = np.zeros(p)
+        for k in range(p):
+            L[k] = -np.sum(c.imag)
+            c = c * q
+        u = (xt - t) / r if r > 0 else np.zeros_like(xt)
+        S = np.zeros(xt.size)
+        for k in range(p - 1, -1, -1):
+            S = S * u + L[k]
+        for j in np.nonzero(~far)[0]:
+            d = xt - m[j]
+            S += f[j] / (h[j] + d * d)
+        out[t0:t0 + TP] = S
+    return out
+
+
+def direct(xv, P, dtype):
+    xv = xv.astype(dtype)
+    acc = np.zeros(xv.size, dtype=dtype)
+    for j in range(P.shape[0]):
+        d = xv - dtype(P[j, 2])
+        acc += dtype(P[j, 0]) / (dtype(P[j, 1]) + d * d)
+    return acc
+
+
+def report(name, xs, ys, P, shapes):
+    ref = direct(xs, P, np.longdouble)
+    mref = float(np.mean((ref - ys) ** 2))
+    d64 = direct(xs, P, np.float64)
+    print(f"{name}: P={P.shape[0]} L={xs.size}  direct f64: MSE rel {float(np.mean((d64 - ys) ** 2)) / mref - 1:+.2e}")
+    for TP, R, p in shapes:
+        s = local_sup(xs, P, TP, R, p)
+        e = float(np.max(np.abs((s - ref) / ref)))
+        print(f"   tile {TP} R={R} terms {p}: sup rel {e:.2e}  MSE rel {float(np.mean((s - ys) ** 2)) / mref - 1:+.2e}")
+
+
+def main():
+    from cases import load_case, synth_spectrum
+    import oracle
+    shapes = [(256, 5.0, 20), (256, 5.0, 16), (256, 4.0, 20), (128, 5.0, 20)]
+    names = sys.argv[1:] or ["blood_01", "blood_05", "blood_09", "sim_01", "synth"]
+    for nm in names:
+        if nm == "synth":
+            x, y, _ = synth_spectrum(0)
+            o = oracle.deconvolute(x, y, (11.8, -2.2), threads=8)
+            P, (lo, hi) = o.params, o.sbi
+        else:
+            x, y, *_ = load_case(nm)
+            g = np.load(os.path.join(ROOT, "tests", "golden", "expected", f"{nm}.npz"))
+            P, (lo, hi) = g["params"], (int(v) for v in g["sbi"])
+        x, y = np.asarray(x), np.asarray(y)
+        report(nm, x[lo:hi], y[lo:hi], P, shapes)
+
+
+if __name__ == "__main__":
+    main()
