@@ -318,9 +318,14 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     // the skipped stage's outputs are stale, so results are wrong
     const char* skip = std::getenv("MDG_DIAG_SKIP");
     const bool skip_smooth = skip && std::strstr(skip, "smooth"), skip_mse = skip && std::strstr(skip, "mse");
+    // MDG_DIAG_DUP=prep,smooth,detect,scores,select,fitinit,retain,mse: launch those
+    // stages twice (each is idempotent; smooth adds a k_prep), for their marginal
+    // cost in stream mode
+    const char* dup_env = std::getenv("MDG_DIAG_DUP");
+    auto reps = [&](const char* stage) { return dup_env && std::strstr(dup_env, stage) ? 2 : 1; };
     {
         StageTimer t(c, ST_PREP);
-        launch_prep(a, w, st);
+        for (int r = reps("prep"); r > 0; --r) launch_prep(a, w, st);
         kn[ST_PREP] = "k_prep";
         if (const char* e = std::getenv("MDG_DIAG_PAD"))
             for (int k = std::atoi(e); k > 0; --k) launch_diag_nop(a, w, st);
@@ -333,20 +338,27 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
             HIPCHK(hipStreamSynchronize(st));
         } else if (!skip_smooth) {
             StageTimer t(c, ST_SMOOTH);
+            if (reps("smooth") == 2) {  // the chain's progress counters are reset by k_prep
+                launch_smooth(a, w, (int)s->smooth_iterations, (int)s->smooth_window, st);
+                launch_prep(a, w, st);
+            }
             kn[ST_SMOOTH] = launch_smooth(a, w, (int)s->smooth_iterations, (int)s->smooth_window, st);
         }
     }
     {
         StageTimer t(c, ST_DETECT);
-        launch_flags(a, w, st);
-        kn[ST_DETECT] = launch_peaks(a, w, det_only, st);
+        for (int r = reps("detect"); r > 0; --r) {
+            launch_flags(a, w, st);
+            kn[ST_DETECT] = launch_peaks(a, w, det_only, st);
+        }
     }
     {
         StageTimer t(c, ST_SELECT);
-        if (!det_only) launch_scores(a, w, st);
-        kn[ST_SELECT] = launch_select(a, w, det_only, s->threshold, st);
+        if (!det_only)
+            for (int r = reps("scores"); r > 0; --r) launch_scores(a, w, st);
+        for (int r = reps("select"); r > 0; --r) kn[ST_SELECT] = launch_select(a, w, det_only, s->threshold, st);
     }
-    {
+    if (reps("fitinit") == 2) {  // the selection kernels already initialised the fit
         StageTimer t(c, ST_FIT_INIT);
         launch_fit_init(a, w, gupd, st);
         kn[ST_FIT_INIT] = "k_fit_init";
@@ -362,7 +374,7 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
             kn[ST_FIT_UPDATE] = "k_fit_update";
         }
     }
-    {
+    if (!mse_fuses_retain() || skip_mse || reps("retain") == 2) {
         StageTimer t(c, ST_RETAIN);
         launch_retain(a, w, st);
         kn[ST_RETAIN] = "k_retain<1024>";
@@ -370,7 +382,7 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     if (!skip_mse) {
         {
             StageTimer t(c, ST_MSE);
-            kn[ST_MSE] = launch_mse(a, w, nparts, st);
+            for (int r = reps("mse"); r > 0; --r) kn[ST_MSE] = launch_mse(a, w, nparts, st);
         }
         StageTimer t(c, ST_MSE_REDUCE);
         launch_mse_final(a, w, nparts, st);

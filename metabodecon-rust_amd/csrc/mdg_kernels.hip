@@ -2091,6 +2091,9 @@ void launch_division_check(int variant, int cases, unsigned long long seed, long
         hipLaunchKernelGGL(k_division_check<1>, dim3(4096), dim3(256), 0, st, seed, n, cases, out);
 }
 
+__device__ __forceinline__ void fit_init_peak(const BatchArgs& a, const Workspace& w, int s, size_t base,
+                                              int p, int l, int c, int r);
+
 template <int BS>
 __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double threshold) {
     const int s = blockIdx.x;
@@ -2215,9 +2218,11 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
     for (int q = q0; q < q1; ++q) {
         if (scores[q] >= thr) {
             const size_t o = base + out;
-            w.sel_l[o] = pl[q];
-            w.sel_c[o] = pc[q];
-            w.sel_r[o] = pr[q];
+            const int l = pl[q], c = pc[q], r = pr[q];
+            w.sel_l[o] = l;
+            w.sel_c[o] = c;
+            w.sel_r[o] = r;
+            fit_init_peak(a, w, s, base, out, l, c, r);
             ++out;
         }
     }
@@ -2236,9 +2241,11 @@ __global__ void k_select_detector_only(BatchArgs a, Workspace w) {
     if (blockIdx.x == 0 && threadIdx.x == 0) w.sel_count[s] = P;
     const size_t base = (size_t)s * w.capD;
     for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
-        w.sel_l[base + p] = w.det_l[base + p];
-        w.sel_c[base + p] = w.det_c[base + p];
-        w.sel_r[base + p] = w.det_r[base + p];
+        const int l = w.det_l[base + p], c = w.det_c[base + p], r = w.det_r[base + p];
+        w.sel_l[base + p] = l;
+        w.sel_c[base + p] = c;
+        w.sel_r[base + p] = r;
+        fit_init_peak(a, w, s, base, p, l, c, r);
     }
 }
 
@@ -2279,27 +2286,35 @@ __device__ __forceinline__ void solve(const Stencil& q, double* out3) {
     out3[2] = m;
 }
 
+// selected peak p of spectrum s with borders (l, c, r): its reduced points, the
+// mirrored stencil and the initial parameters (version 0)
+__device__ __forceinline__ void fit_init_peak(const BatchArgs& a, const Workspace& w, int s, size_t base,
+                                              int p, int l, int c, int r) {
+    const double* x = a.x + (size_t)s * a.x_stride;
+    const double* y = a.y + (size_t)s * a.y_stride;
+    Stencil q{x[l], x[c], x[r], y[l], y[c], y[r]};
+    double* rx = w.rx + 3 * base + 3 * (size_t)p;
+    double* ry = w.ry + 3 * base + 3 * (size_t)p;
+    rx[0] = q.x1; rx[1] = q.x2; rx[2] = q.x3;
+    ry[0] = q.y1; ry[1] = q.y2; ry[2] = q.y3;
+    mirror_shoulder(q);
+    double* st = w.stencil + 6 * base + 6 * (size_t)p;
+    st[0] = q.x1; st[1] = q.x2; st[2] = q.x3; st[3] = q.y1; st[4] = q.y2; st[5] = q.y3;
+    double* L = w.params + 3 * base + 3 * (size_t)p;
+    solve(q, L);
+    if (!peak_fast_ok(L[0], L[1], L[2])) atomicAdd(&w.unsafe[4 * s], 1);
+}
+
+// The selection kernels initialise each selected peak's fit as they write it
+// (fit_init_peak), so the pipeline has no separate launch for it; k_fit_init is
+// the stand-alone form (MDG_DIAG_DUP=fitinit re-runs it).
 __global__ void k_fit_init(BatchArgs a, Workspace w) {
     const int s = blockIdx.y;
     if (w.status[s]) return;
     const int P = w.sel_count[s];
     const size_t base = (size_t)s * w.capD;
-    const double* x = a.x + (size_t)s * a.x_stride;
-    const double* y = a.y + (size_t)s * a.y_stride;
-    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
-        const int l = w.sel_l[base + p], c = w.sel_c[base + p], r = w.sel_r[base + p];
-        Stencil q{x[l], x[c], x[r], y[l], y[c], y[r]};
-        double* rx = w.rx + 3 * base + 3 * (size_t)p;
-        double* ry = w.ry + 3 * base + 3 * (size_t)p;
-        rx[0] = q.x1; rx[1] = q.x2; rx[2] = q.x3;
-        ry[0] = q.y1; ry[1] = q.y2; ry[2] = q.y3;
-        mirror_shoulder(q);
-        double* st = w.stencil + 6 * base + 6 * (size_t)p;
-        st[0] = q.x1; st[1] = q.x2; st[2] = q.x3; st[3] = q.y1; st[4] = q.y2; st[5] = q.y3;
-        double* L = w.params + 3 * base + 3 * (size_t)p;
-        solve(q, L);
-        if (!peak_fast_ok(L[0], L[1], L[2])) atomicAdd(&w.unsafe[4 * s], 1);
-    }
+    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x)
+        fit_init_peak(a, w, s, base, p, w.sel_l[base + p], w.sel_c[base + p], w.sel_r[base + p]);
 }
 
 // K6  fit superposition at the 3P reduced points + ratio (fitter_analytical.rs:40-47)
@@ -3014,6 +3029,21 @@ __global__ void k_fit_update(BatchArgs a, Workspace w, int it) {
 
 // K8  retain sfhw > CHECK_PRECISION && hw2 > CHECK_PRECISION, order preserving
 // (fitter_analytical.rs:67-69); copies min(count, cap) rows to the caller's output.
+// the fitted parameters of spectrum s: k_fit_sup_tf / _tw leave version
+// min(iterations) in the buffer of its parity; the k_fit_update path updates in place
+__device__ __forceinline__ const double* final_params(const Workspace& w, int s, size_t base) {
+    const int ver = w.params_alt ? (w.fit_iters_s ? min(w.fit_iters_s[s], w.fit_iters) : w.fit_iters) : 0;
+    return params_version(w, base, ver);
+}
+
+// retain predicate (fitter_analytical.rs:67-69)
+__device__ __forceinline__ bool retained(double sfhw, double hw2) {
+    return sfhw > kCheckPrecision && hw2 > kCheckPrecision;
+}
+
+template <int BS>
+__device__ __forceinline__ void retain_body(const BatchArgs& a, const Workspace& w, int s, int* lds_i);
+
 template <int BS>
 __global__ __launch_bounds__(BS) void k_retain(BatchArgs a, Workspace w) {
     const int s = blockIdx.x;
@@ -3026,12 +3056,16 @@ __global__ __launch_bounds__(BS) void k_retain(BatchArgs a, Workspace w) {
         }
         return;
     }
+    retain_body<BS>(a, w, s, lds_i);
+}
+
+// ordered compaction of the retained Lorentzians into kept and the caller's rows
+// (k_retain; k_mse_local's first workgroup of each spectrum)
+template <int BS>
+__device__ __forceinline__ void retain_body(const BatchArgs& a, const Workspace& w, int s, int* lds_i) {
     const int P = w.sel_count[s];
     const size_t base = (size_t)s * w.capD;
-    // k_fit_sup_tf leaves version min(iterations) of the parameters in the buffer of
-    // its parity; the k_fit_update path updates them in place
-    const int ver = w.params_alt ? (w.fit_iters_s ? min(w.fit_iters_s[s], w.fit_iters) : w.fit_iters) : 0;
-    const double* params = params_version(w, base, ver);
+    const double* params = final_params(w, s, base);
     const int per = (P + BS - 1) / BS;
     const int p0 = threadIdx.x * per, p1 = min(P, p0 + per);
     double* kept = w.kept + 3 * base;
@@ -3168,7 +3202,7 @@ __global__ __launch_bounds__(BS) void k_mse_partial(BatchArgs a, Workspace w, in
 __device__ __forceinline__ int64_t mse_len(const Workspace& w, int s);
 template <int BS>
 __device__ __forceinline__ void mse_publish_fold(const BatchArgs& a, const Workspace& w, int s, int part,
-                                                 int nparts, double acc, double* parts);
+                                                 int nparts, double acc, int kept_n, double* parts);
 __device__ __forceinline__ void mse_panic_out(const BatchArgs& a, int s);
 
 // The last workgroup of a spectrum to finish (arrival counter, acq_rel at agent
@@ -3421,7 +3455,7 @@ __global__ __launch_bounds__(256) void k_mse_quad(BatchArgs a, Workspace w, int 
         for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
     }
     __shared__ double parts[kMseMaxParts];
-    mse_publish_fold<BS>(a, w, s, part, nparts, acc, parts);
+    mse_publish_fold<BS>(a, w, s, part, nparts, acc, w.kept_count[s], parts);
 }
 
 // Thread 0's acc is this workgroup's partial of spectrum s: publish it, count the
@@ -3429,7 +3463,7 @@ __global__ __launch_bounds__(256) void k_mse_quad(BatchArgs a, Workspace w, int 
 // to right from +0.0 (fixed order: deterministic) into out_mse / out_status.
 template <int BS>
 __device__ __forceinline__ void mse_publish_fold(const BatchArgs& a, const Workspace& w, int s, int part,
-                                                 int nparts, double acc, double* parts) {
+                                                 int nparts, double acc, int kept_n, double* parts) {
     __shared__ int last;
     if (threadIdx.x == 0) {
         __hip_atomic_store(w.mse_part + (size_t)s * nparts + part, acc, __ATOMIC_RELAXED,
@@ -3456,7 +3490,7 @@ __device__ __forceinline__ void mse_publish_fold(const BatchArgs& a, const Works
         }
         if (threadIdx.x == 0) {
             a.out_mse[s] = t / (double)mse_len(w, s);
-            a.out_status[s] = (w.kept_count[s] > a.cap) ? MDG_CAPACITY : MDG_OK;
+            a.out_status[s] = (kept_n > a.cap) ? MDG_CAPACITY : MDG_OK;
         }
     }
 }
@@ -3494,6 +3528,18 @@ __device__ __forceinline__ double rcp_nr2(double d) {
     return __builtin_fma(r1, __builtin_fma(-d, r1, 1.0), r1);
 }
 
+// sum over the retained Lorentzians among params[0, P) at x, every term
+// (wave-uniform parameters: scalar loads); FAST: div_rn_1nr, else '/'
+template <bool FAST>
+__device__ __forceinline__ double sup_retained_direct(double x, const_f64_ptr prm, int P) {
+    double acc = 0.0;
+    for (int j = 0; j < P; ++j) {
+        const double f = prm[3 * j], h = prm[3 * j + 1], m = prm[3 * j + 2];
+        if (retained(f, h)) acc += lorentz_mse<FAST>(x, f, h, m);
+    }
+    return acc;
+}
+
 __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int nparts, int near_cap) {
     constexpr int BS = 256, NW = BS / 64, TP = kLocTP, PK = kLocP, PH = PK / 2;
     static_assert(TP == BS && PK % 2 == 0 && PH * 16 <= BS, "tile shape");
@@ -3506,14 +3552,27 @@ __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int
     __shared__ double nearp[3 * kLocNear];
     __shared__ double wmin[NW], wmax[NW], wacc[NW];
     __shared__ int wcnt[NW];
-    if (w.status[s]) return;  // already reported by k_retain
+    __shared__ int lds_i[NW + 1];
+    const int tid = threadIdx.x, wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    // k_retain's work, fused: the first workgroup of each spectrum reports a failed
+    // spectrum or compacts its retained Lorentzians into the caller's rows
+    if (w.status[s]) {
+        if (part == 0 && tid == 0) {
+            a.out_count[s] = 0;
+            a.out_mse[s] = 0.0;
+            a.out_status[s] = w.status[s];
+        }
+        return;
+    }
+    if (part == 0) retain_body<BS>(a, w, s, lds_i);
     if (w.mse_panic[s]) {
         if (part == 0) mse_panic_out(a, s);
         return;
     }
-    const int P = w.kept_count[s];
-    const const_f64_ptr kept = (const_f64_ptr)(w.kept + 3 * (size_t)s * w.capD);
-    const double* __restrict__ keptv = w.kept + 3 * (size_t)s * w.capD;
+    const int P = w.sel_count[s];
+    const size_t pbase = (size_t)s * w.capD;
+    const double* __restrict__ prmv = final_params(w, s, pbase);
+    const const_f64_ptr prm = (const_f64_ptr)prmv;
     const double* x = a.x + (size_t)s * a.x_stride;
     const double* y = a.y + (size_t)s * a.y_stride;
     const int nig = w.n_ig[s];
@@ -3523,8 +3582,18 @@ __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int
         mse_region(w, s, r, nig, &lo, &hi);
         total += hi - lo;
     }
-    const bool fast = w.x_ok[s] && w.unsafe_kept[s] == 0;
-    const int tid = threadIdx.x, wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    // every workgroup counts the retained Lorentzians (the last one reports the
+    // capacity status) and checks their fast ranges (k_retain's unsafe_kept)
+    int cnt = 0, uns = 0;
+    for (int j = tid; j < P; j += BS) {
+        const double f = prmv[3 * j], h = prmv[3 * j + 1], m = prmv[3 * j + 2];
+        const bool r = retained(f, h);
+        cnt += r;
+        uns |= r && !peak_fast_ok(f, h, m);
+    }
+    int kept_n;
+    (void)block_exclusive_scan<BS>(cnt, lds_i, &kept_n);
+    const bool fast = w.x_ok[s] && !__syncthreads_or(uns);
     double acc = 0.0;
     for (int64_t v0 = (int64_t)part * TP; v0 < total; v0 += (int64_t)nparts * TP) {
         const int64_t v = v0 + tid;
@@ -3540,10 +3609,9 @@ __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int
             rem -= hi - lo;
         }
         const double xv = x[idx], yv = y[idx];
-        double sup[1] = {0.0};
-        const double xa[1] = {xv};
+        double sup;
         if (!fast) {
-            sup_range_quad<false, 1>(xa, kept, 0, P, sup);
+            sup = sup_retained_direct<false>(xv, prm, P);
         } else {
             // tile centre and half range over its valid points
             double lo = ok ? xv : INFINITY, hi = ok ? xv : -INFINITY;
@@ -3574,9 +3642,9 @@ __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int
             int nnear = 0;
             for (int j0 = 0; j0 < P; j0 += BS) {
                 const int j = j0 + tid;
-                const bool have = j < P;
-                const int jj = have ? j : P - 1;
-                const double f = keptv[3 * jj], h = keptv[3 * jj + 1], m = keptv[3 * jj + 2];
+                const int jj = j < P ? j : P - 1;
+                const double f = prmv[3 * jj], h = prmv[3 * jj + 1], m = prmv[3 * jj + 2];
+                const bool have = j < P && retained(f, h);
                 const double dm = m - t;
                 const double d2 = __builtin_fma(dm, dm, h);  // |z - t|^2
                 const bool nr = have && !(d2 > lim2);
@@ -3637,7 +3705,7 @@ __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int
                 __syncthreads();
             }
             if (nnear > near_cap) {
-                sup_range_quad<true, 1>(xa, kept, 0, P, sup);
+                sup = sup_retained_direct<true>(xv, prm, P);
             } else {
                 const double u = rt > 0.0 ? (xv - t) / rt : 0.0;
                 double S = coef[PK - 1];
@@ -3654,10 +3722,10 @@ __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int
                 }
                 for (; j < nnear; ++j)
                     nsum += lorentz_mse<true>(xv, nearp[3 * j], nearp[3 * j + 1], nearp[3 * j + 2]);
-                sup[0] = nsum + S;
+                sup = nsum + S;
             }
         }
-        const double d = sup[0] - yv;
+        const double d = sup - yv;
         if (ok) acc += d * d;
         __syncthreads();  // LDS reuse by the next tile
     }
@@ -3670,7 +3738,7 @@ __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int
 #pragma unroll
         for (int k = 0; k < NW; ++k) tot += wacc[k];
     }
-    mse_publish_fold<BS>(a, w, s, part, nparts, tot, red);
+    mse_publish_fold<BS>(a, w, s, part, nparts, tot, kept_n, red);
 }
 
 // total length of the MSE regions of spectrum s (the divisor of compute_mse)
@@ -4041,6 +4109,8 @@ static int mse_quad_npt(const BatchArgs& a) {
     if (const char* e = std::getenv("MDG_MSE_QNPT")) return std::atoi(e) == 2 ? 2 : 1;
     return 2;
 }
+// k_mse_local compacts the retained Lorentzians itself (no k_retain launch)
+bool mse_fuses_retain() { return mse_kind() == "local"; }
 int mse_nparts(const BatchArgs& a) {
     const std::string k = mse_kind();
     if (k == "local")

@@ -27,7 +27,7 @@ def main():
         x, y, _ = synth_spectrum(seed)
         o = oracle.deconvolute(x, y, (11.8, -2.2), threads=16)
         cases.append((f"synth_{seed}", x, y, (11.8, -2.2), oracle.default_settings(), (), o.mse))
-    for kind in ("quad", "n", "plain"):
+    for kind in ("local", "quad", "n", "plain"):
         os.environ["MDG_MSE"] = kind
         worst, wname = 0.0, None
         for name, x, y, sb, st, ign, ref in cases:
