@@ -8,8 +8,9 @@ analytical fit 10 iterations, MSE). One step = one deconvolution of one distinct
 spectrum (--batch 1); inputs are resident in HBM before timing.
 
 Steps are submitted round-robin to --streams engine contexts (one HIP stream and
-one HBM workspace each; default 16, with GPU_MAX_HW_QUEUES=32 so every stream has
-its own hardware queue), the way concurrent callers of the reference's
+one HBM workspace each; default 20, with GPU_MAX_HW_QUEUES=32 so every stream has
+its own hardware queue; from 24 streams on the queues are oversubscribed and the
+throughput drops by a quarter), the way concurrent callers of the reference's
 `par_deconvolute_spectrum` (Deconvoluter is Send + Sync, deconvoluter.rs:913-917)
 would use one GPU: the sequential smoothers of some spectra overlap the fits and
 MSEs of others. `value` is that stream's throughput; `latency_ms` is one
@@ -66,7 +67,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=240)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1, help="spectra per step (headline)")
-    ap.add_argument("--streams", type=int, default=16,
+    ap.add_argument("--streams", type=int, default=20,
                     help="engine contexts the steps are spread over (1 = back to back)")
     ap.add_argument("--hw-queues", type=int, default=32,
                     help="GPU_MAX_HW_QUEUES for this process (HIP maps streams onto that "

@@ -2093,6 +2093,9 @@ void launch_division_check(int variant, int cases, unsigned long long seed, long
 
 __device__ __forceinline__ void fit_init_peak(const BatchArgs& a, const Workspace& w, int s, size_t base,
                                               int p, int l, int c, int r);
+__device__ __forceinline__ void fit_init_pair(const BatchArgs& a, const Workspace& w, int s, size_t base,
+                                              int p1, int l1, int c1, int r1, int p2, int l2, int c2,
+                                              int r2);
 
 template <int BS>
 __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double threshold) {
@@ -2218,11 +2221,9 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
     for (int q = q0; q < q1; ++q) {
         if (scores[q] >= thr) {
             const size_t o = base + out;
-            const int l = pl[q], c = pc[q], r = pr[q];
-            w.sel_l[o] = l;
-            w.sel_c[o] = c;
-            w.sel_r[o] = r;
-            fit_init_peak(a, w, s, base, out, l, c, r);
+            w.sel_l[o] = pl[q];
+            w.sel_c[o] = pc[q];
+            w.sel_r[o] = pr[q];
             ++out;
         }
     }
@@ -2231,6 +2232,15 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
         if (total == 0) w.status[s] = MDG_EMPTY_SIGNAL_REGION;
     }
     KSTAMP(14);
+    // the fit's initial state (k_fit_init's work), spread evenly over the block:
+    // selected peaks p and p + BS per thread, their loads in flight together
+    __syncthreads();  // the selection above, written by other threads of the block
+    for (int p = threadIdx.x; p < total; p += 2 * BS) {
+        const int p2 = p + BS < total ? p + BS : p;
+        const int l1 = w.sel_l[base + p], c1 = w.sel_c[base + p], r1 = w.sel_r[base + p];
+        const int l2 = w.sel_l[base + p2], c2 = w.sel_c[base + p2], r2 = w.sel_r[base + p2];
+        fit_init_pair(a, w, s, base, p, l1, c1, r1, p2, l2, c2, r2);
+    }
 }
 
 // DetectorOnly: the detector output is the selection (detector_only.rs:17-39)
@@ -2305,9 +2315,35 @@ __device__ __forceinline__ void fit_init_peak(const BatchArgs& a, const Workspac
     if (!peak_fast_ok(L[0], L[1], L[2])) atomicAdd(&w.unsafe[4 * s], 1);
 }
 
-// The selection kernels initialise each selected peak's fit as they write it
-// (fit_init_peak), so the pipeline has no separate launch for it; k_fit_init is
-// the stand-alone form (MDG_DIAG_DUP=fitinit re-runs it).
+// two peaks (p2 == p1 for one): both stencils' loads in flight together
+__device__ __forceinline__ void fit_init_pair(const BatchArgs& a, const Workspace& w, int s, size_t base,
+                                              int p1, int l1, int c1, int r1, int p2, int l2, int c2,
+                                              int r2) {
+    const double* x = a.x + (size_t)s * a.x_stride;
+    const double* y = a.y + (size_t)s * a.y_stride;
+    const double xa[6] = {x[l1], x[c1], x[r1], x[l2], x[c2], x[r2]};
+    const double ya[6] = {y[l1], y[c1], y[r1], y[l2], y[c2], y[r2]};
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        if (k == 1 && p2 == p1) break;
+        const int p = k ? p2 : p1;
+        Stencil q{xa[3 * k], xa[3 * k + 1], xa[3 * k + 2], ya[3 * k], ya[3 * k + 1], ya[3 * k + 2]};
+        double* rx = w.rx + 3 * base + 3 * (size_t)p;
+        double* ry = w.ry + 3 * base + 3 * (size_t)p;
+        rx[0] = q.x1; rx[1] = q.x2; rx[2] = q.x3;
+        ry[0] = q.y1; ry[1] = q.y2; ry[2] = q.y3;
+        mirror_shoulder(q);
+        double* st = w.stencil + 6 * base + 6 * (size_t)p;
+        st[0] = q.x1; st[1] = q.x2; st[2] = q.x3; st[3] = q.y1; st[4] = q.y2; st[5] = q.y3;
+        double* L = w.params + 3 * base + 3 * (size_t)p;
+        solve(q, L);
+        if (!peak_fast_ok(L[0], L[1], L[2])) atomicAdd(&w.unsafe[4 * s], 1);
+    }
+}
+
+// The selection kernels initialise the fit of the peaks they select
+// (fit_init_peak / fit_init_pair), so the pipeline has no separate launch for it;
+// k_fit_init is the stand-alone form (MDG_DIAG_DUP=fitinit re-runs it).
 __global__ void k_fit_init(BatchArgs a, Workspace w) {
     const int s = blockIdx.y;
     if (w.status[s]) return;
@@ -3070,7 +3106,9 @@ __device__ __forceinline__ void retain_body(const BatchArgs& a, const Workspace&
     const int p0 = threadIdx.x * per, p1 = min(P, p0 + per);
     double* kept = w.kept + 3 * base;
     double* out = a.out + 3 * (size_t)s * a.cap;
-    constexpr int R = 4;  // up to R parameters per thread stay in registers (one load round)
+    // up to R parameters per thread stay in registers (one load round): 4096
+    // Lorentzians at 1024 threads, 2048 at 256
+    constexpr int R = BS >= 1024 ? 4 : 8;
     if (per <= R) {
         double v[R][3];
         int keep = 0;
@@ -3554,17 +3592,22 @@ __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int
     __shared__ int wcnt[NW];
     __shared__ int lds_i[NW + 1];
     const int tid = threadIdx.x, wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-    // k_retain's work, fused: the first workgroup of each spectrum reports a failed
-    // spectrum or compacts its retained Lorentzians into the caller's rows
-    if (w.status[s]) {
-        if (part == 0 && tid == 0) {
-            a.out_count[s] = 0;
-            a.out_mse[s] = 0.0;
-            a.out_status[s] = w.status[s];
+    // k_retain's work, fused: one extra workgroup per spectrum (part == nparts)
+    // reports a failed spectrum or compacts its retained Lorentzians into the
+    // caller's rows, beside the tiles; the last tile workgroup reports the MSE
+    if (part == nparts) {
+        if (w.status[s]) {
+            if (tid == 0) {
+                a.out_count[s] = 0;
+                a.out_mse[s] = 0.0;
+                a.out_status[s] = w.status[s];
+            }
+            return;
         }
+        retain_body<BS>(a, w, s, lds_i);
         return;
     }
-    if (part == 0) retain_body<BS>(a, w, s, lds_i);
+    if (w.status[s]) return;
     if (w.mse_panic[s]) {
         if (part == 0) mse_panic_out(a, s);
         return;
@@ -4129,7 +4172,8 @@ const char* launch_mse(const BatchArgs& a, const Workspace& w, int nparts, hipSt
         // direct fallback of crowded tiles
         int cap = kLocNear;
         if (const char* e = std::getenv("MDG_MSE_NEARCAP")) cap = std::max(0, std::min(kLocNear, std::atoi(e)));
-        launch_k(k_mse_local, dim3(nparts * a.B), dim3(256), 0, st, a, w, nparts, cap);
+        // nparts tile workgroups per spectrum plus its retain workgroup
+        launch_k(k_mse_local, dim3((nparts + 1) * a.B), dim3(256), 0, st, a, w, nparts, cap);
         return "k_mse_local";
     }
     if (mse_kind() == "quad") {

@@ -32,7 +32,7 @@ STAGES = [  # stage -> kernel-name prefixes (after "mdg::")
     ("fit_superposition", ("k_fit_sup",)),
     ("fit_update", ("k_fit_update",)),
     ("retain", ("k_retain",)),
-    ("mse_superposition", ("k_mse_partial", "k_mse_quad")),
+    ("mse_superposition", ("k_mse_partial", "k_mse_quad", "k_mse_local")),
     ("mse_reduce", ("k_mse_final",)),
 ]
 

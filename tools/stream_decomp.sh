@@ -22,8 +22,6 @@ for v in "$@"; do
     nomse) one nomse MDG_DIAG_SKIP=mse -- ;;
     fit1) one fit1 -- --fit-iterations 1 ;;
     noexcl) one noexcl MDG_CHAIN_EXCL=0 -- ;;
-    s24) one s24 -- --streams 24 ;;
-    s32) one s32 -- --streams 32 ;;
     b2) one b2 -- --batch 2 --streams 16 --steps 240 ;;
     b4) one b4 -- --batch 4 --streams 16 --steps 120 ;;
     b16) one b16 -- --batch 16 --streams 16 --steps 32 ;;
@@ -32,9 +30,7 @@ for v in "$@"; do
     pad10s) one pad10s MDG_DIAG_PAD=10 MDG_DIAG_PAD_SMALL=1 -- ;;
     nograph) one nograph MDG_GRAPHS=0 -- ;;
     tf) one tf MDG_FITSUP=tf -- ;;
-    s8) one s8 -- --streams 8 ;;
-    s12) one s12 -- --streams 12 ;;
-    s20) one s20 -- --streams 20 ;;
+    s[0-9]*) one "$v" -- --streams "${v#s}" ;;
     dup_*) one "$v" MDG_DIAG_DUP="${v#dup_}" -- ;;
     noexcl_dup_smooth) one "$v" MDG_CHAIN_EXCL=0 MDG_DIAG_DUP=smooth -- ;;
     *) echo "unknown $v" ;;
