@@ -765,8 +765,19 @@ int run_pipeline_graphed(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     }
     BatchArgs ka = a;
     clear_io(ka);
+    // the kernel-choice overrides (tests, diagnostics) select other kernels, so
+    // they are part of the key too
+    std::string envs;
+    for (const char* e : {"MDG_SMOOTH", "MDG_CHAIN_EXCL", "MDG_FITSUP", "MDG_GFIT", "MDG_MSE", "MDG_MSE_QNPT",
+                          "MDG_MSE_NEARCAP", "MDG_PEAKS_2PASS", "MDG_DIAG_SKIP", "MDG_DIAG_DUP", "MDG_DIAG_PAD",
+                          "MDG_DIAG_PAD_SMALL"}) {
+        const char* v = std::getenv(e);
+        envs += v ? v : "\x01";
+        envs += '\0';
+    }
     std::vector<unsigned char> key(sizeof(BatchArgs) + sizeof(mdg_settings) + 2 * sizeof(void*) +
                                    sizeof(size_t));
+    key.insert(key.end(), envs.begin(), envs.end());
     unsigned char* k = key.data();
     std::memcpy(k, &ka, sizeof(BatchArgs));
     k += sizeof(BatchArgs);

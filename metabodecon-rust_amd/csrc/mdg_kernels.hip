@@ -3628,6 +3628,7 @@ __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int
     // every workgroup counts the retained Lorentzians (the last one reports the
     // capacity status) and checks their fast ranges (k_retain's unsafe_kept)
     int cnt = 0, uns = 0;
+#pragma unroll 4
     for (int j = tid; j < P; j += BS) {
         const double f = prmv[3 * j], h = prmv[3 * j + 1], m = prmv[3 * j + 2];
         const bool r = retained(f, h);
@@ -3683,10 +3684,18 @@ __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int
 #pragma unroll
             for (int k = 0; k < PK; ++k) L[k] = 0.0;
             int nnear = 0;
+            // the next round's Lorentzian is loaded while this one is expanded
+            double fn = prmv[3 * min(tid, P - 1)], hn = prmv[3 * min(tid, P - 1) + 1],
+                   mn = prmv[3 * min(tid, P - 1) + 2];
             for (int j0 = 0; j0 < P; j0 += BS) {
                 const int j = j0 + tid;
-                const int jj = j < P ? j : P - 1;
-                const double f = prmv[3 * jj], h = prmv[3 * jj + 1], m = prmv[3 * jj + 2];
+                const double f = fn, h = hn, m = mn;
+                {
+                    const int jn = min(j + BS, P - 1);
+                    fn = prmv[3 * jn];
+                    hn = prmv[3 * jn + 1];
+                    mn = prmv[3 * jn + 2];
+                }
                 const bool have = j < P && retained(f, h);
                 const double dm = m - t;
                 const double d2 = __builtin_fma(dm, dm, h);  // |z - t|^2

@@ -501,6 +501,44 @@ def test_device_graph_replay(ctx, monkeypatch):
         assert s1 == s2 and np.array_equal(p1, p2) and m1 == m2
 
 
+def test_graph_key_follows_kernel_overrides(monkeypatch):
+    """A cached pipeline graph is keyed by the kernel-choice overrides too: the
+    same device buffers with MDG_MSE / MDG_FITSUP switched between calls launch
+    the newly chosen kernels (reported by the engine), each call equal to the
+    oracle."""
+    torch = pytest.importorskip("torch")
+    cx, cy, csb, cst, _ = load_case("blood_03")
+    n = cy.size
+    c = nat.Context(0)
+    x = torch.from_numpy(cx).cuda()
+    y = torch.from_numpy(cy).cuda()
+    sb = torch.tensor([csb], dtype=torch.float64, device="cuda")
+    cap = n // 2 + 2
+    out = torch.zeros((1, cap, 3), dtype=torch.float64, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    mse = torch.zeros(1, dtype=torch.float64, device="cuda")
+    status = torch.zeros(1, dtype=torch.int32, device="cuda")
+    s = nat.default_settings()
+    o = oracle.deconvolute(cx, cy, csb, cst)
+    seen = []
+    for mse_k, fit_k in [("local", "tw7"), ("quad", "tw7"), ("local", "dpp"), ("local", "tw7")]:
+        monkeypatch.setenv("MDG_MSE", mse_k)
+        monkeypatch.setenv("MDG_FITSUP", fit_k)
+        rc = nat.lib().mdg_deconvolute_batch_device(
+            c.handle, 1, n, x.data_ptr(), 0, y.data_ptr(), n, sb.data_ptr(), ctypes.byref(s), None,
+            0, out.data_ptr(), cap, cnt.data_ptr(), mse.data_ptr(), status.data_ptr())
+        assert rc == 0
+        c.synchronize()
+        k = c.stage_kernels()
+        seen.append((k["mse_superposition"], k["fit_superposition"]))
+        assert int(status[0]) == 0
+        assert np.array_equal(out[0, : int(cnt[0])].cpu().numpy(), o.params)
+        assert abs(float(mse[0]) - o.mse) <= MSE_RTOL * abs(o.mse)
+    c.close()
+    assert seen[0][0] == "k_mse_local" and seen[1][0].startswith("k_mse_quad")
+    assert seen[2][1] == "k_fit_sup_dpp" and seen[3] == seen[0]
+
+
 @pytest.mark.parametrize("name", ["sim_01", "sim_07"])
 def test_optimize_settings_matches_exhaustive_oracle(name):
     """Deconvoluter.optimize_settings (GPU: 27 batched pipelines + exact tie
