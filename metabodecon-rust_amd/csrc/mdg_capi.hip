@@ -354,8 +354,7 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     }
     {
         StageTimer t(c, ST_SELECT);
-        if (!det_only)
-            for (int r = reps("scores"); r > 0; --r) launch_scores(a, w, st);
+        if (!det_only && (!peaks_score() || reps("scores") == 2)) launch_scores(a, w, st);
         for (int r = reps("select"); r > 0; --r) kn[ST_SELECT] = launch_select(a, w, det_only, s->threshold, st);
     }
     if (reps("fitinit") == 2) {  // the selection kernels already initialised the fit
@@ -769,7 +768,7 @@ int run_pipeline_graphed(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     // they are part of the key too
     std::string envs;
     for (const char* e : {"MDG_SMOOTH", "MDG_CHAIN_EXCL", "MDG_FITSUP", "MDG_GFIT", "MDG_MSE", "MDG_MSE_QNPT",
-                          "MDG_MSE_NEARCAP", "MDG_PEAKS_2PASS", "MDG_DIAG_SKIP", "MDG_DIAG_DUP", "MDG_DIAG_PAD",
+                          "MDG_MSE_NEARCAP", "MDG_PEAKS_2PASS", "MDG_PEAKS_NOSCORE", "MDG_DIAG_SKIP", "MDG_DIAG_DUP", "MDG_DIAG_PAD",
                           "MDG_DIAG_PAD_SMALL"}) {
         const char* v = std::getenv(e);
         envs += v ? v : "\x01";

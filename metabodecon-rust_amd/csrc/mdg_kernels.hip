@@ -1428,6 +1428,29 @@ __device__ __forceinline__ int word_peaks(const BatchArgs& a, const Workspace& w
     return kept;
 }
 
+// ScorerMinimumSum::score_peak (scorer.rs:65-75): min(sum |D[l..=c]|, sum
+// |D[c..=r]|) with D[k] = (y[k-1] - 2 y[k]) + y[k+1] of the smoothed row, both
+// sums left folds in k order. The values of a chunk of 8 ticks are loaded
+// together (clamped addresses): one memory latency per 8 ticks, not per tick.
+__device__ __forceinline__ double score_peak(const double* __restrict__ sm, int N, int l, int c, int r) {
+    double left = -0.0, right = -0.0;
+    for (int k0 = l; k0 <= r; k0 += 8) {
+        double y[10];  // y[k0-1 .. k0+8]
+#pragma unroll
+        for (int u = 0; u < 10; ++u) y[u] = sm[min(max(k0 - 1 + u, 0), N - 1)];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int k = k0 + u;
+            if (k <= r) {
+                const double d = fabs((y[u] - 2.0 * y[u + 1]) + y[u + 2]);
+                if (k <= c) left += d;
+                if (k >= c) right += d;
+            }
+        }
+    }
+    return fmin(left, right);
+}
+
 // K3a per chunk of kPkWords mask words (one word per thread): kept and bordered
 // peak counts. K3b re-scans its chunk, places it after the kept peaks of the chunks
 // before it and compacts in centre order; chunk 0 publishes det_count, or
@@ -1458,7 +1481,7 @@ __global__ __launch_bounds__(kPkWords) void k_peaks_count(BatchArgs a, Workspace
 // chunks before it. Replaces k_peaks_count + k_peaks_write (one launch and one
 // word scan fewer).
 constexpr unsigned long long kPkValid = 1ull << 62;
-__global__ __launch_bounds__(kPkWords) void k_peaks(BatchArgs a, Workspace w, int detector_only) {
+__global__ __launch_bounds__(kPkWords) void k_peaks(BatchArgs a, Workspace w, int detector_only, int score) {
     const int s = blockIdx.y, chunk = blockIdx.x;
     __shared__ int lds_i[kPkWords / 64 + 1];
     __shared__ long long lds_l[kPkWords / 64 + 1];
@@ -1504,7 +1527,14 @@ __global__ __launch_bounds__(kPkWords) void k_peaks(BatchArgs a, Workspace w, in
         return;
     }
     if (chunk == 0 && threadIdx.x == 0) w.det_count[s] = (int32_t)k_all;
-    if (kept) word_peaks<true>(a, w, s, wd, detector_only, &bordered, (size_t)s * w.capD + before + o);
+    const size_t b0 = (size_t)s * w.capD + before;
+    if (kept) word_peaks<true>(a, w, s, wd, detector_only, &bordered, b0 + o);
+    if (detector_only || !score) return;
+    // k_scores' work for this chunk's peaks, spread evenly over the block
+    __syncthreads();  // the peaks above, written by other threads of the block
+    const double* __restrict__ sm = w.smooth_ptr + (size_t)s * w.smooth_stride;
+    for (int p = threadIdx.x; p < total; p += kPkWords)
+        w.scores[b0 + p] = score_peak(sm, a.N, w.det_l[b0 + p], w.det_c[b0 + p], w.det_r[b0 + p]);
 }
 
 __global__ __launch_bounds__(kPkWords) void k_peaks_write(BatchArgs a, Workspace w, int detector_only) {
@@ -1552,25 +1582,8 @@ __global__ void k_scores(BatchArgs a, Workspace w) {
     const size_t base = (size_t)s * w.capD;
     const double* __restrict__ sm = w.smooth_ptr + (size_t)s * w.smooth_stride;
     const int N = a.N;
-    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
-        const int l = w.det_l[base + p], c = w.det_c[base + p], r = w.det_r[base + p];
-        double left = -0.0, right = -0.0;
-        for (int k0 = l; k0 <= r; k0 += 8) {
-            double y[10];  // y[k0-1 .. k0+8]
-#pragma unroll
-            for (int u = 0; u < 10; ++u) y[u] = sm[min(max(k0 - 1 + u, 0), N - 1)];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int k = k0 + u;
-                if (k <= r) {
-                    const double d = fabs((y[u] - 2.0 * y[u + 1]) + y[u + 2]);
-                    if (k <= c) left += d;
-                    if (k >= c) right += d;
-                }
-            }
-        }
-        w.scores[base + p] = fmin(left, right);
-    }
+    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x)
+        w.scores[base + p] = score_peak(sm, N, w.det_l[base + p], w.det_c[base + p], w.det_r[base + p]);
 }
 
 // Left fold over the signal-free-region scores peaks[..left] ++ peaks[right..P]
@@ -4037,6 +4050,7 @@ const char* launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int
 void launch_flags(const BatchArgs& a, const Workspace& w, hipStream_t st) {
     launch_k(k_flags, dim3(cdiv(a.N, 256), a.B), dim3(256), 0, st, a, w);
 }
+bool peaks_score() { return !std::getenv("MDG_PEAKS_NOSCORE") && !std::getenv("MDG_PEAKS_2PASS"); }
 const char* launch_peaks(const BatchArgs& a, const Workspace& w, int detector_only, hipStream_t st) {
     const int nch = cdiv(w.W, kPkWords);
     static_assert(kPkWords == 256, "k_flags clears ceil(W / 256) slots");
@@ -4045,7 +4059,8 @@ const char* launch_peaks(const BatchArgs& a, const Workspace& w, int detector_on
         launch_k(k_peaks_write, dim3(nch, a.B), dim3(kPkWords), 0, st, a, w, detector_only);
         return "k_flags+k_peaks_count+k_peaks_write";
     }
-    launch_k(k_peaks, dim3(nch, a.B), dim3(kPkWords), 0, st, a, w, detector_only);
+    // k_peaks scores the peaks it writes (no k_scores launch) unless MDG_PEAKS_NOSCORE
+    launch_k(k_peaks, dim3(nch, a.B), dim3(kPkWords), 0, st, a, w, detector_only, peaks_score() ? 1 : 0);
     return "k_flags+k_peaks";
 }
 void launch_scores(const BatchArgs& a, const Workspace& w, hipStream_t st) {

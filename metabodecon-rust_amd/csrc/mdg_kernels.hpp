@@ -137,6 +137,7 @@ void launch_scores(const BatchArgs& a, const Workspace& w, hipStream_t st);
 const char* launch_select(const BatchArgs& a, const Workspace& w, int detector_only,
                           double threshold, hipStream_t st);
 bool mse_fuses_retain();
+bool peaks_score();
 void launch_fit_init(const BatchArgs& a, const Workspace& w, int gx, hipStream_t st);
 // returns true when the launched kernel also did the stencil update (no k_fit_update)
 bool fit_sup_fused(const BatchArgs& a);

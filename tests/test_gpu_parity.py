@@ -86,13 +86,21 @@ def test_blood_batch_all_16(ctx):
         assert np.array_equal(ctx.last_peaks(k, "selected").astype(np.int64), g["selected"])
 
 
-def test_detected_peaks_match_oracle(ctx):
+@pytest.mark.parametrize("path", ["fused", "MDG_PEAKS_NOSCORE", "MDG_PEAKS_2PASS"])
+def test_detected_peaks_match_oracle(ctx, path, monkeypatch):
+    """Detected triples equal the oracle's; the selection (which reads the noise
+    scores) equals the golden on every detection path: scores computed by k_peaks
+    itself (default), by a separate k_scores, and the two-kernel peak list."""
+    if path != "fused":
+        monkeypatch.setenv(path, "1")
     x, y, sb, st, ign = load_case("blood_01")
     gpu_batch(ctx, x, y[None, :], [sb], st)
     det = ctx.last_peaks(0, "detected").astype(np.int64)
     sm = oracle.moving_average(y, 3, 3)
     l, c, r = oracle.detect_peaks(oracle.second_derivative(sm))
     assert np.array_equal(det, np.stack([l, c, r], axis=1))
+    g = np.load(os.path.join(GOLDEN, "expected", "blood_01.npz"))
+    assert np.array_equal(ctx.last_peaks(0, "selected").astype(np.int64), g["selected"])
 
 
 def test_python_api_end_to_end():
