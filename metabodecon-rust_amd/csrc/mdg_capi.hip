@@ -51,6 +51,10 @@ struct mdg_ctx {
     Buffer arena;
     int ws_B = 0, ws_N = 0;
     Buffer chain;  // k_smooth_chain buffers (allocated on first use)
+    // k_smooth_chain progress counters: one 128-byte slot per (spectrum, pass) at
+    // a fixed place for every (B, P) the chain supports (B * P <= 2048), zeroed
+    // once and left at zero by every run (k_flags), so no run has to clear them
+    Buffer chain_flags;
     // optimize_settings: per-spectrum overrides for the next run_pipeline, buffers
     const double* ovr_thr = nullptr;
     const int32_t* ovr_fit = nullptr;
@@ -236,8 +240,13 @@ int ensure_workspace(mdg_ctx* c, int B, int N) {
 // the buffer moves
 int ensure_chain(mdg_ctx* c, size_t bytes) {
     const void* old = c->chain.p;
-    const int rc = ensure(c->chain, bytes);
+    int rc = ensure(c->chain, bytes);
     if (c->chain.p != old) ++c->ws_gen;
+    if (rc == MDG_OK && !c->chain_flags.p) {
+        rc = ensure(c->chain_flags, (size_t)2048 * 128);
+        if (rc == MDG_OK) HIPCHK(hipMemsetAsync(c->chain_flags.p, 0, c->chain_flags.bytes, c->stream));
+        ++c->ws_gen;
+    }
     return rc;
 }
 
@@ -310,7 +319,7 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
             w.chain_stride = L;
             w.chain_raw = (double*)base;
             w.chain_tmp = w.chain_raw + (size_t)P * a.B * L;
-            w.chain_flags = (int32_t*)(base + (size_t)(2 * P - 1) * a.B * L * 8);
+            w.chain_flags = (int32_t*)c->chain_flags.p;
             w.chain_P = P;
         }
     }
@@ -323,26 +332,32 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     // cost in stream mode
     const char* dup_env = std::getenv("MDG_DIAG_DUP");
     auto reps = [&](const char* stage) { return dup_env && std::strstr(dup_env, stage) ? 2 : 1; };
-    {
+    const int sm_it = (int)s->smooth_iterations, sm_ws = (int)s->smooth_window;
+    const bool panic_shape = ma && (int64_t)(s->smooth_window / 2) > a.N;
+    // the chain smoother does k_prep's work itself (MDG_PREP=separate: not)
+    const char* prep_env = std::getenv("MDG_PREP");
+    const bool fused_prep = ma && !panic_shape && !skip_smooth && !(prep_env && std::string(prep_env) == "separate") &&
+                            reps("prep") == 1 && smooth_uses_chain(a, w, sm_it, sm_ws);
+    if (!fused_prep) {
         StageTimer t(c, ST_PREP);
         for (int r = reps("prep"); r > 0; --r) launch_prep(a, w, st);
         kn[ST_PREP] = "k_prep";
-        if (const char* e = std::getenv("MDG_DIAG_PAD"))
-            for (int k = std::atoi(e); k > 0; --k) launch_diag_nop(a, w, st);
     }
+    if (const char* e = std::getenv("MDG_DIAG_PAD"))
+        for (int k = std::atoi(e); k > 0; --k) launch_diag_nop(a, w, st);
     if (ma) {
-        if ((int64_t)(s->smooth_window / 2) > a.N) {
+        if (panic_shape) {
             // moving_average.rs:63 `values_len - self.right` underflows: reference panics
             std::vector<int32_t> pan(a.B, MDG_REFERENCE_PANIC);
             HIPCHK(hipMemcpyAsync(w.status, pan.data(), sizeof(int32_t) * a.B, hipMemcpyHostToDevice, st));
             HIPCHK(hipStreamSynchronize(st));
         } else if (!skip_smooth) {
             StageTimer t(c, ST_SMOOTH);
-            if (reps("smooth") == 2) {  // the chain's progress counters are reset by k_prep
-                launch_smooth(a, w, (int)s->smooth_iterations, (int)s->smooth_window, st);
-                launch_prep(a, w, st);
+            if (reps("smooth") == 2) {  // k_flags resets the chain's progress counters
+                launch_smooth(a, w, sm_it, sm_ws, st, fused_prep ? 1 : 0);
+                launch_flags(a, w, st);
             }
-            kn[ST_SMOOTH] = launch_smooth(a, w, (int)s->smooth_iterations, (int)s->smooth_window, st);
+            kn[ST_SMOOTH] = launch_smooth(a, w, sm_it, sm_ws, st, fused_prep ? 1 : 0);
         }
     }
     {
@@ -587,7 +602,7 @@ int mdg_ctx_destroy(mdg_ctx* c) {
         drop_graphs(c);
         for (Buffer& b : c->opt)
             if (b.p) (void)hipFree(b.p);
-        for (Buffer* b : {&c->arena, &c->chain, &c->st_x, &c->st_y, &c->st_sb, &c->st_out, &c->st_cnt,
+        for (Buffer* b : {&c->arena, &c->chain, &c->chain_flags, &c->st_x, &c->st_y, &c->st_sb, &c->st_out, &c->st_cnt,
                           &c->st_mse, &c->st_status, &c->st_L, &c->st_sup, &c->st_flag})
             if (b->p) (void)hipFree(b->p);
         if (c->own) (void)hipStreamDestroy(c->own);
@@ -769,7 +784,7 @@ int run_pipeline_graphed(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     std::string envs;
     for (const char* e : {"MDG_SMOOTH", "MDG_CHAIN_EXCL", "MDG_FITSUP", "MDG_GFIT", "MDG_MSE", "MDG_MSE_QNPT",
                           "MDG_MSE_NEARCAP", "MDG_PEAKS_2PASS", "MDG_PEAKS_NOSCORE", "MDG_DIAG_SKIP", "MDG_DIAG_DUP", "MDG_DIAG_PAD",
-                          "MDG_DIAG_PAD_SMALL"}) {
+                          "MDG_DIAG_PAD_SMALL", "MDG_PREP"}) {
         const char* v = std::getenv(e);
         envs += v ? v : "\x01";
         envs += '\0';

@@ -347,9 +347,11 @@ __device__ __forceinline__ int find_prev_bit(const uint64_t* __restrict__ m, int
 // K0  prep: signal-boundary indices, ignore-region indices, MSE regions
 // spectrum.rs:633-635,741-746 ; deconvoluter.rs:828-904
 // ----------------------------------------------------------------------------------
-__global__ void k_prep(BatchArgs a, Workspace w) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= a.B) return;
+// Per-spectrum set-up of a pipeline run: signal boundary indices, ignore-region
+// indices, MSE-region checks, range flags, counters and status. k_prep runs it for
+// every spectrum; with the chain smoother the pass-0 workgroup of each spectrum
+// runs it instead (one launch fewer), no other kernel of that launch reading it.
+__device__ __forceinline__ void prep_spectrum(const BatchArgs& a, const Workspace& w, int s) {
     const double* x = a.x + (size_t)s * a.x_stride;
     const double x0 = x[0];
     const double step = x[1] - x[0];
@@ -400,6 +402,13 @@ __global__ void k_prep(BatchArgs a, Workspace w) {
     w.det_count[s] = 0;
     w.sel_count[s] = 0;
     w.kept_count[s] = 0;
+}
+
+__global__ void k_prep(BatchArgs a, Workspace w) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= a.B) return;
+    prep_spectrum(a, w, s);
+    // the chain smoother's progress counters start at zero (k_flags leaves them so)
     for (int p = 0; p < w.chain_P; ++p) w.chain_flags[((size_t)s * w.chain_P + p) * 32] = 0;
 }
 
@@ -962,7 +971,8 @@ __device__ __forceinline__ void chain_l2_pull(const double* p, int cnt) {
 // and would slow them, and whose neighbours they would slow: a stream's
 // k_fit_sup_tf launch lasts as long as its slowest workgroup).
 template <int WS, bool EXCL>
-__global__ __launch_bounds__(64 * (2 + kChainScalers)) void k_smooth_chain(BatchArgs a, Workspace w, int P) {
+__global__ __launch_bounds__(64 * (2 + kChainScalers)) void k_smooth_chain(BatchArgs a, Workspace w, int P,
+                                                                            int fused_prep) {
     if constexpr (EXCL) {
         asm volatile("v_mov_b32 v255, 0" ::: "v255");
         asm volatile("v_accvgpr_write_b32 a255, 0" ::: "a255");
@@ -973,7 +983,13 @@ __global__ __launch_bounds__(64 * (2 + kChainScalers)) void k_smooth_chain(Batch
     const int x8 = id & 7, j8 = id >> 3;
     const int p = j8 % P, s = (j8 / P) * 8 + x8;
     if (s >= a.B) return;
-    if (w.status[s]) return;  // uniform per spectrum
+    if (fused_prep) {
+        // k_prep's work; its status is 0 (N >= 2 is checked on the host), so no
+        // pass of this launch needs to read it
+        if (p == 0 && threadIdx.x == 0) prep_spectrum(a, w, s);
+    } else if (w.status[s]) {
+        return;  // uniform per spectrum
+    }
     constexpr int R = WS / 2;
     constexpr int CB = kChainCB;
     const int N = a.N;
@@ -1338,6 +1354,10 @@ __global__ void k_smooth(BatchArgs a, Workspace w, int iters, int ws) {
 // ----------------------------------------------------------------------------------
 __global__ void k_flags(BatchArgs a, Workspace w) {
     const int s = blockIdx.y;
+    // the smoother has finished: its progress counters go back to zero for the
+    // next run (whatever this spectrum's status)
+    if (blockIdx.x == 0 && (int)threadIdx.x < w.chain_P)
+        w.chain_flags[((size_t)s * w.chain_P + threadIdx.x) * 32] = 0;
     if (w.status[s]) return;
     const int N = a.N;
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -3975,16 +3995,17 @@ static const char* launch_pipe(const BatchArgs& a, const Workspace& w, int iters
 }
 
 template <int WS>
-static const char* launch_chain(const BatchArgs& a, const Workspace& w, int iters, hipStream_t st) {
+static const char* launch_chain(const BatchArgs& a, const Workspace& w, int iters, hipStream_t st,
+                                int fused_prep) {
     const unsigned grid = 8u * (unsigned)iters * cdiv(a.B, 8);
     const char* excl_env = std::getenv("MDG_CHAIN_EXCL");  // 0 = never (measurements)
     const bool excl = (int)grid <= kChainExclMax && !(excl_env && excl_env[0] == '0');
     if (excl) {
         launch_k((k_smooth_chain<WS, true>), dim3(grid), dim3(64 * (2 + kChainScalers)), 0, st,
-                           a, w, iters);
+                           a, w, iters, fused_prep);
     } else {
         launch_k((k_smooth_chain<WS, false>), dim3(grid), dim3(64 * (2 + kChainScalers)), 0, st,
-                           a, w, iters);
+                           a, w, iters, fused_prep);
     }
     static const char* names[2][9] = {
         {"", "", "k_smooth_chain<2, false>", "k_smooth_chain<3, false>", "k_smooth_chain<4, false>",
@@ -3995,22 +4016,30 @@ static const char* launch_chain(const BatchArgs& a, const Workspace& w, int iter
          "k_smooth_chain<8, true>"}};
     return names[excl ? 1 : 0][WS];
 }
-const char* launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int ws, hipStream_t st) {
-    // chain kernel (one CU per pass) for windows <= 8 and batches <= 512; then
-    // wave-per-pass (B > 21) or lane-pipelined (window fits the register FIFO);
-    // the one-lane-per-spectrum kernel otherwise. MDG_SMOOTH = chain | waves |
-    // pipe | generic forces one (tests); an unsupported shape falls through.
+// chain kernel (one CU per pass) for windows <= 8 and batches <= 512 (B * iters
+// <= 2048) when its buffers are set up and MDG_SMOOTH does not force another
+bool smooth_uses_chain(const BatchArgs& a, const Workspace& w, int iters, int ws) {
     const char* force = std::getenv("MDG_SMOOTH");
     const bool chain = force ? std::string(force) == "chain" : true;
-    if (chain && w.chain_P >= iters && chain_supported(a.B, a.N, iters, ws)) {
+    return chain && w.chain_P >= iters && chain_supported(a.B, a.N, iters, ws);
+}
+const char* launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int ws, hipStream_t st,
+                          int fused_prep) {
+    // the chain kernel; then wave-per-pass (B > 21) or lane-pipelined (window
+    // fits the register FIFO); the one-lane-per-spectrum kernel otherwise.
+    // MDG_SMOOTH = chain | waves | pipe | generic forces one (tests); an
+    // unsupported shape falls through. fused_prep (chain only): the chain kernel
+    // runs k_prep's work itself.
+    const char* force = std::getenv("MDG_SMOOTH");
+    if (smooth_uses_chain(a, w, iters, ws)) {
         switch (ws) {
-            case 2: return launch_chain<2>(a, w, iters, st);
-            case 3: return launch_chain<3>(a, w, iters, st);
-            case 4: return launch_chain<4>(a, w, iters, st);
-            case 5: return launch_chain<5>(a, w, iters, st);
-            case 6: return launch_chain<6>(a, w, iters, st);
-            case 7: return launch_chain<7>(a, w, iters, st);
-            case 8: return launch_chain<8>(a, w, iters, st);
+            case 2: return launch_chain<2>(a, w, iters, st, fused_prep);
+            case 3: return launch_chain<3>(a, w, iters, st, fused_prep);
+            case 4: return launch_chain<4>(a, w, iters, st, fused_prep);
+            case 5: return launch_chain<5>(a, w, iters, st, fused_prep);
+            case 6: return launch_chain<6>(a, w, iters, st, fused_prep);
+            case 7: return launch_chain<7>(a, w, iters, st, fused_prep);
+            case 8: return launch_chain<8>(a, w, iters, st, fused_prep);
             default: break;
         }
     }

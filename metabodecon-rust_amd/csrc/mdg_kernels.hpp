@@ -130,7 +130,9 @@ inline void launch_k(void (*k)(BatchArgs, Workspace, P...), dim3 g, dim3 b, size
 
 void launch_prep(const BatchArgs& a, const Workspace& w, hipStream_t st);
 void launch_diag_nop(const BatchArgs& a, const Workspace& w, hipStream_t st);
-const char* launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int ws, hipStream_t st);
+bool smooth_uses_chain(const BatchArgs& a, const Workspace& w, int iters, int ws);
+const char* launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int ws, hipStream_t st,
+                          int fused_prep = 0);
 void launch_flags(const BatchArgs& a, const Workspace& w, hipStream_t st);
 const char* launch_peaks(const BatchArgs& a, const Workspace& w, int detector_only, hipStream_t st);
 void launch_scores(const BatchArgs& a, const Workspace& w, hipStream_t st);

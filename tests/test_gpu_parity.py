@@ -149,6 +149,34 @@ def test_reference_unit_superposition(ctx):
     assert abs(md.Lorentzian.superposition_vec(np.array([5.0]), trip)[0] - 51.466992) <= 1e-6
 
 
+def test_fused_prep_after_failures_and_other_smoothers(monkeypatch):
+    """The chain smoother runs k_prep's work itself and never reads the status the
+    previous run left; k_flags returns its progress counters to zero. On one
+    context: a failing spectrum (NoPeaksDetected), then a good one, the same on
+    the wave smoother, with k_prep launched separately, and the chain again --
+    every result equal to the oracle."""
+    c = nat.Context(0)
+    st = oracle.default_settings()
+    n = 4096
+    xf = np.linspace(14.0, -6.0, n)
+    flat = np.full(n, 7.0)
+    x, y, sb, cst, _ = load_case("blood_07")
+    o = oracle.deconvolute(x, y, sb, cst)
+    for smooth, prep in [("chain", None), ("waves", None), ("chain", "separate"), ("chain", None)]:
+        monkeypatch.setenv("MDG_SMOOTH", smooth)
+        if prep:
+            monkeypatch.setenv("MDG_PREP", prep)
+        else:
+            monkeypatch.delenv("MDG_PREP", raising=False)
+        status, *_ = gpu_batch(c, xf, flat[None, :], [(11.8, -2.2)], st)
+        assert status[0] == 1, (smooth, prep)
+        status, counts, out, mse = gpu_batch(c, x, y[None, :], [sb], cst)
+        assert status[0] == 0, (smooth, prep)
+        assert np.array_equal(out[0, : counts[0]], o.params), (smooth, prep)
+        assert abs(mse[0] - o.mse) <= MSE_RTOL * abs(o.mse)
+    c.close()
+
+
 def test_error_statuses(ctx):
     import metabodecon as md
     from metabodecon import exceptions as ex
