@@ -1501,25 +1501,29 @@ __global__ __launch_bounds__(kPkWords) void k_peaks_count(BatchArgs a, Workspace
 // chunks before it. Replaces k_peaks_count + k_peaks_write (one launch and one
 // word scan fewer).
 constexpr unsigned long long kPkValid = 1ull << 62;
-__global__ __launch_bounds__(kPkWords) void k_peaks(BatchArgs a, Workspace w, int detector_only, int score) {
+// kPkThreads threads per chunk: the first kPkWords own one mask word each; all of
+// them score the chunk's peaks afterwards (four times the threads for that part)
+constexpr int kPkThreads = 1024;
+__global__ __launch_bounds__(kPkThreads) void k_peaks(BatchArgs a, Workspace w, int detector_only, int score) {
+    constexpr int BS = kPkThreads;
     const int s = blockIdx.y, chunk = blockIdx.x;
-    __shared__ int lds_i[kPkWords / 64 + 1];
-    __shared__ long long lds_l[kPkWords / 64 + 1];
+    __shared__ int lds_i[BS / 64 + 1];
+    __shared__ long long lds_l[BS / 64 + 1];
     if (w.status[s]) return;  // uniform per spectrum: no chunk waits for a returned one
     const int nch = (w.W + kPkWords - 1) / kPkWords;
     unsigned long long* slot = (unsigned long long*)w.peak_cnt + (size_t)s * nch;
     const int wd = chunk * kPkWords + threadIdx.x;
     int bordered = 0, kept = 0;
-    if (wd < w.W) kept = word_peaks<false>(a, w, s, wd, detector_only, &bordered, 0);
+    if ((int)threadIdx.x < kPkWords && wd < w.W) kept = word_peaks<false>(a, w, s, wd, detector_only, &bordered, 0);
     int total;
-    const int o = block_exclusive_scan<kPkWords>(kept, lds_i, &total);
-    const long long b_tot = block_sum_ll<kPkWords>(bordered, lds_l);
+    const int o = block_exclusive_scan<BS>(kept, lds_i, &total);
+    const long long b_tot = block_sum_ll<BS>(bordered, lds_l);
     if (threadIdx.x == 0)
         __hip_atomic_store(slot + chunk, kPkValid | ((unsigned long long)b_tot << 31) | (unsigned)total,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     long long before = 0, k_all = 0, b_all = 0;
     bool ok = true;
-    for (int k = threadIdx.x; k < nch; k += kPkWords) {
+    for (int k = threadIdx.x; k < nch; k += BS) {
         unsigned long long v;
         unsigned spins = 0;
         while (!((v = __hip_atomic_load(slot + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & kPkValid)) {
@@ -1534,10 +1538,10 @@ __global__ __launch_bounds__(kPkWords) void k_peaks(BatchArgs a, Workspace w, in
         k_all += kk;
         b_all += bb;
     }
-    before = block_sum_ll<kPkWords>(before, lds_l);
-    k_all = block_sum_ll<kPkWords>(k_all, lds_l);
-    b_all = block_sum_ll<kPkWords>(b_all, lds_l);
-    const long long bad = block_sum_ll<kPkWords>(ok ? 0 : 1, lds_l);
+    before = block_sum_ll<BS>(before, lds_l);
+    k_all = block_sum_ll<BS>(k_all, lds_l);
+    b_all = block_sum_ll<BS>(b_all, lds_l);
+    const long long bad = block_sum_ll<BS>(ok ? 0 : 1, lds_l);
     if (bad) {
         if (threadIdx.x == 0) w.status[s] = MDG_ERR_HIP;
         return;
@@ -1553,7 +1557,7 @@ __global__ __launch_bounds__(kPkWords) void k_peaks(BatchArgs a, Workspace w, in
     // k_scores' work for this chunk's peaks, spread evenly over the block
     __syncthreads();  // the peaks above, written by other threads of the block
     const double* __restrict__ sm = w.smooth_ptr + (size_t)s * w.smooth_stride;
-    for (int p = threadIdx.x; p < total; p += kPkWords)
+    for (int p = threadIdx.x; p < total; p += BS)
         w.scores[b0 + p] = score_peak(sm, a.N, w.det_l[b0 + p], w.det_c[b0 + p], w.det_r[b0 + p]);
 }
 
@@ -4089,7 +4093,7 @@ const char* launch_peaks(const BatchArgs& a, const Workspace& w, int detector_on
         return "k_flags+k_peaks_count+k_peaks_write";
     }
     // k_peaks scores the peaks it writes (no k_scores launch) unless MDG_PEAKS_NOSCORE
-    launch_k(k_peaks, dim3(nch, a.B), dim3(kPkWords), 0, st, a, w, detector_only, peaks_score() ? 1 : 0);
+    launch_k(k_peaks, dim3(nch, a.B), dim3(kPkThreads), 0, st, a, w, detector_only, peaks_score() ? 1 : 0);
     return "k_flags+k_peaks";
 }
 void launch_scores(const BatchArgs& a, const Workspace& w, hipStream_t st) {
