@@ -317,8 +317,8 @@ def headline(args, nat, torch, dist, dev, rank, world):
 
     def submit(k, j, nslots):
         # the engine reads spectrum j where it lies and writes step k's results
-        # straight into res[k]: a cached pipeline graph is re-pointed at each
-        # call's arrays (mdg_capi.hip repoint_graph), no staging copies
+        # straight into res[k]: no staging copies (with MDG_GRAPHS=1 a cached
+        # pipeline graph is re-pointed at each call's arrays, repoint_graph)
         s = slots[k % nslots]
         if args.copy_io:  # the round-2 form: stage through the slot's own rows
             with torch.cuda.stream(s.stream):
@@ -329,7 +329,7 @@ def headline(args, nat, torch, dist, dev, rank, world):
             return
         run_batch(nat, s, B, n, x, Y[j], sb, settings, cap, rec=res[k] if k < K else None)
 
-    for k in range(max(W, S)):  # every context captures its graph
+    for k in range(max(W, S)):  # every context sizes its workspace (and captures its graph)
         submit(K + k, k % R, S)
     torch.cuda.synchronize()
     if world > 1:  # RCCL connections are set up by the first collectives, not in the timing

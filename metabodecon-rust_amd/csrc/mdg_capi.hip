@@ -759,11 +759,15 @@ int repoint_graph(mdg_ctx::CachedGraph& ge, const BatchArgs& a) {
 // rewrites the nodes' arguments (repoint_graph) instead of capturing again, so
 // a stream of calls on distinct device buffers replays one graph.
 // Not used while stages are being timed, or for the reference-panic shape
-// (host-synchronous path); MDG_GRAPHS=0 disables it.
+// (host-synchronous path). Opt-in (MDG_GRAPHS=1): on ROCm 7 a replayed graph
+// costs the GPU more per node than the same launches made directly -- 20
+// concurrent B = 1 pipelines ran 7514-7576 spectra/s replayed against
+// 7740-7766 launched directly, one spectrum alone 0.97-0.98 ms against 0.95
+// (DESIGN.md §8); the host saves ≈10 µs per call.
 int run_pipeline_graphed(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     const char* env = std::getenv("MDG_GRAPHS");
     const bool ma = s->smoother == MDG_SMOOTH_MOVING_AVERAGE;
-    if ((env && std::string(env) == "0") || c->profile_mask ||
+    if (!(env && std::string(env) == "1") || c->profile_mask ||
         (ma && (int64_t)(s->smooth_window / 2) > a.N))
         return run_pipeline(c, a, s);
     // size every buffer first: the capture must not allocate, and the key needs the

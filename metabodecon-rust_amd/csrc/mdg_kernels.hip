@@ -3973,7 +3973,11 @@ __global__ void k_diag_nop_small(int32_t* p, int b) {
 }
 void launch_diag_nop(const BatchArgs& a, const Workspace& w, hipStream_t st) {
     if (std::getenv("MDG_DIAG_PAD_SMALL")) hipLaunchKernelGGL(k_diag_nop_small, dim3(1), dim3(64), 0, st, w.status, a.B);
-    else launch_k(k_diag_nop, dim3(1), dim3(64), 0, st, a, w);
+    else {
+        // MDG_DIAG_PAD_WGS: workgroups of the no-op (the cost of workgroup dispatch)
+        const char* g = std::getenv("MDG_DIAG_PAD_WGS");
+        launch_k(k_diag_nop, dim3(g ? std::max(1, std::atoi(g)) : 1), dim3(g ? 256 : 64), 0, st, a, w);
+    }
 }
 template <int WS>
 static const char* launch_waves(const BatchArgs& a, const Workspace& w, int iters, hipStream_t st) {

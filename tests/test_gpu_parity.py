@@ -489,11 +489,12 @@ def test_one_newton_division_is_not_exact_on_hard_cases(ctx):
 
 
 def test_device_graph_replay(ctx, monkeypatch):
-    """mdg_deconvolute_batch_device replays a cached hipGraph for repeated argument
-    sets: refilling the same device buffers with other spectra must still give the
-    oracle's results on the replayed launch, and the same bits as the uncaptured
-    pipeline (MDG_GRAPHS=0)."""
+    """With MDG_GRAPHS=1 mdg_deconvolute_batch_device replays a cached hipGraph for
+    repeated argument sets: refilling the same device buffers with other spectra
+    must still give the oracle's results on the replayed launch, and the same bits
+    as the uncaptured pipeline (MDG_GRAPHS=0, the default)."""
     torch = pytest.importorskip("torch")
+    monkeypatch.setenv("MDG_GRAPHS", "1")
     names = [["blood_02", "blood_04"], ["blood_09", "blood_11"], ["blood_02", "blood_04"]]
     n = load_case("blood_02")[1].size
     b = 2
@@ -543,6 +544,7 @@ def test_graph_key_follows_kernel_overrides(monkeypatch):
     the newly chosen kernels (reported by the engine), each call equal to the
     oracle."""
     torch = pytest.importorskip("torch")
+    monkeypatch.setenv("MDG_GRAPHS", "1")
     cx, cy, csb, cst, _ = load_case("blood_03")
     n = cy.size
     c = nat.Context(0)
@@ -644,12 +646,13 @@ def test_jcampdx_and_serde_inputs_through_the_device(tmp_path):
     assert r.mse == d.mse
 
 
-def test_graph_cache_survives_workspace_growth(ctx):
+def test_graph_cache_survives_workspace_growth(ctx, monkeypatch):
     """A cached pipeline graph bakes the workspace layout. Growing the workspace
     (a larger batch, then a longer spectrum on a fresh context) must drop the cached
     graphs, so B=1 -> B=2 -> B=1 -> longer N -> B=1 on the same tensors keeps
     giving the oracle's results (stale graph after reallocation)."""
     torch = pytest.importorskip("torch")
+    monkeypatch.setenv("MDG_GRAPHS", "1")
     c = nat.Context(0)
     try:
         names = ["sim_04", "sim_09"]
@@ -724,7 +727,7 @@ def test_par_deconvolute_spectra_rccl_world1():
         dist.destroy_process_group()
 
 
-def test_graph_repoint_in_flight_bit_exact():
+def test_graph_repoint_in_flight_bit_exact(monkeypatch):
     """One cached pipeline graph serves calls on distinct device arrays
     (mdg_capi.hip repoint_graph): every call here passes its own x/y/sb rows and
     writes straight into its own result rows, and all calls are enqueued on two
@@ -733,6 +736,7 @@ def test_graph_repoint_in_flight_bit_exact():
     CUDA/HIP contract: launches already enqueued are not affected). Every call
     must equal the oracle bit for bit, and the MSE within 1e-12."""
     torch = pytest.importorskip("torch")
+    monkeypatch.setenv("MDG_GRAPHS", "1")
     names = ["blood_02", "blood_05", "blood_07", "blood_11", "blood_13", "blood_16"]
     cases = [load_case(nm) for nm in names]
     refs = [oracle.deconvolute(c[0], c[1], c[2], c[3]) for c in cases]
@@ -773,9 +777,11 @@ def test_graph_repoint_in_flight_bit_exact():
             c.close()
 
 
-def test_concurrent_contexts_stream_bit_exact():
+@pytest.mark.parametrize("graphs", ["0", "1"])
+def test_concurrent_contexts_stream_bit_exact(graphs, monkeypatch):
     """The bench's stream mode: 6 contexts, each on its own stream,
-    replay their captured pipelines on a stream of distinct spectra (input row
+    run their pipelines (launched directly, or replayed as captured graphs with
+    MDG_GRAPHS=1) on a stream of distinct spectra (input row
     refilled on the context stream before each replay, results copied out after
     it), all enqueued before any synchronisation so the pipelines overlap on the
     GPU. Every spectrum's Lorentzians must equal the oracle's bit for bit: no
@@ -783,6 +789,7 @@ def test_concurrent_contexts_stream_bit_exact():
     whole-CU chain smoother and the term-fold fit stay exact when other
     pipelines run beside them."""
     torch = pytest.importorskip("torch")
+    monkeypatch.setenv("MDG_GRAPHS", graphs)
     names = ["blood_02", "blood_05", "blood_07", "blood_11", "blood_13", "blood_16",
              "sim_02", "sim_05", "sim_08", "sim_11", "sim_14", "sim_16"]
     cases = [load_case(nm) for nm in names]

@@ -28,7 +28,10 @@ for v in "$@"; do
     pad5) one pad5 MDG_DIAG_PAD=5 -- ;;
     pad10) one pad10 MDG_DIAG_PAD=10 -- ;;
     pad10s) one pad10s MDG_DIAG_PAD=10 MDG_DIAG_PAD_SMALL=1 -- ;;
+    pad10w*) one "$v" MDG_DIAG_PAD=10 MDG_DIAG_PAD_WGS="${v#pad10w}" -- ;;
     nograph) one nograph MDG_GRAPHS=0 -- ;;
+    nograph16) one nograph16 MDG_GRAPHS=0 -- --streams 16 ;;
+    nograph24) one nograph24 MDG_GRAPHS=0 -- --streams 24 ;;
     tf) one tf MDG_FITSUP=tf -- ;;
     s[0-9]*) one "$v" -- --streams "${v#s}" ;;
     dup_*) one "$v" MDG_DIAG_DUP="${v#dup_}" -- ;;
