@@ -23,7 +23,7 @@ struct BatchArgs {
     int64_t y_stride;
     const double* sb;     // 2B signal boundaries (ppm, ordered as Spectrum stores them)
     int n_ignore;         // merged ignore regions (ppm), shared by the batch
-    double ignore[2 * kMaxIgnore];
+    const double* ignore; // 2 * n_ignore doubles in device memory (null when none)
     double* out;          // B x cap x {sfhw, hw2, maxp}
     int cap;
     int32_t* out_count;

@@ -30,6 +30,9 @@ for v in "$@"; do
     pad10s) one pad10s MDG_DIAG_PAD=10 MDG_DIAG_PAD_SMALL=1 -- ;;
     pad10w*) one "$v" MDG_DIAG_PAD=10 MDG_DIAG_PAD_WGS="${v#pad10w}" -- ;;
     nograph) one nograph MDG_GRAPHS=0 -- ;;
+    kdev) one kdev HIP_FORCE_DEV_KERNARG=1 -- ;;
+    kdev0) one kdev0 HIP_FORCE_DEV_KERNARG=0 -- ;;
+    kdevg) one kdevg HIP_FORCE_DEV_KERNARG=1 MDG_GRAPHS=1 -- ;;
     nograph16) one nograph16 MDG_GRAPHS=0 -- --streams 16 ;;
     nograph24) one nograph24 MDG_GRAPHS=0 -- --streams 24 ;;
     tf) one tf MDG_FITSUP=tf -- ;;
