@@ -2134,10 +2134,12 @@ __device__ __forceinline__ void fit_init_pair(const BatchArgs& a, const Workspac
                                               int p1, int l1, int c1, int r1, int p2, int l2, int c2,
                                               int r2);
 
+constexpr int kSelLds = 4096;  // selected peaks staged in k_select's LDS (48 KB)
 template <int BS>
 __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double threshold) {
     const int s = blockIdx.x;
     __shared__ int lds_i[BS / 64 + 1];
+    __shared__ int sel_lds[3 * kSelLds];
     __shared__ long long lds_l[BS / 64 + 1];
     __shared__ double thr_sh;
     __shared__ WinLds wl;
@@ -2258,9 +2260,15 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
     for (int q = q0; q < q1; ++q) {
         if (scores[q] >= thr) {
             const size_t o = base + out;
-            w.sel_l[o] = pl[q];
-            w.sel_c[o] = pc[q];
-            w.sel_r[o] = pr[q];
+            const int l = pl[q], c = pc[q], r = pr[q];
+            w.sel_l[o] = l;
+            w.sel_c[o] = c;
+            w.sel_r[o] = r;
+            if (out < kSelLds) {  // the fit initialisation below reads them from LDS
+                sel_lds[3 * out] = l;
+                sel_lds[3 * out + 1] = c;
+                sel_lds[3 * out + 2] = r;
+            }
             ++out;
         }
     }
@@ -2270,14 +2278,25 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
     }
     KSTAMP(14);
     // the fit's initial state (k_fit_init's work), spread evenly over the block:
-    // selected peaks p and p + BS per thread, their loads in flight together
-    __syncthreads();  // the selection above, written by other threads of the block
+    // selected peaks p and p + BS per thread, their loads in flight together. The
+    // selection comes from LDS (a barrier that does not wait for the global
+    // stores above), or from memory after a full barrier when it does not fit
+    const bool in_lds = total <= kSelLds;
+    if (in_lds) lds_barrier();
+    else __syncthreads();
     for (int p = threadIdx.x; p < total; p += 2 * BS) {
         const int p2 = p + BS < total ? p + BS : p;
-        const int l1 = w.sel_l[base + p], c1 = w.sel_c[base + p], r1 = w.sel_r[base + p];
-        const int l2 = w.sel_l[base + p2], c2 = w.sel_c[base + p2], r2 = w.sel_r[base + p2];
+        int l1, c1, r1, l2, c2, r2;
+        if (in_lds) {
+            l1 = sel_lds[3 * p]; c1 = sel_lds[3 * p + 1]; r1 = sel_lds[3 * p + 2];
+            l2 = sel_lds[3 * p2]; c2 = sel_lds[3 * p2 + 1]; r2 = sel_lds[3 * p2 + 2];
+        } else {
+            l1 = w.sel_l[base + p]; c1 = w.sel_c[base + p]; r1 = w.sel_r[base + p];
+            l2 = w.sel_l[base + p2]; c2 = w.sel_c[base + p2]; r2 = w.sel_r[base + p2];
+        }
         fit_init_pair(a, w, s, base, p, l1, c1, r1, p2, l2, c2, r2);
     }
+    KSTAMP(18);
 }
 
 // DetectorOnly: the detector output is the selection (detector_only.rs:17-39)
