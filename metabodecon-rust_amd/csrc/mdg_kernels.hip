@@ -3741,8 +3741,8 @@ __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int
             for (int k = 0; k < PK; ++k) L[k] = 0.0;
             int nnear = 0;
             // the next round's Lorentzian is loaded while this one is expanded
-            double fn = prmv[3 * min(tid, P - 1)], hn = prmv[3 * min(tid, P - 1) + 1],
-                   mn = prmv[3 * min(tid, P - 1) + 2];
+            const int j1 = max(0, min(tid, P - 1));  // P = 0: a harmless in-bounds read
+            double fn = prmv[3 * j1], hn = prmv[3 * j1 + 1], mn = prmv[3 * j1 + 2];
             for (int j0 = 0; j0 < P; j0 += BS) {
                 const int j = j0 + tid;
                 const double f = fn, h = hn, m = mn;
@@ -4052,8 +4052,8 @@ bool smooth_uses_chain(const BatchArgs& a, const Workspace& w, int iters, int ws
 }
 const char* launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int ws, hipStream_t st,
                           int fused_prep) {
-    // the chain kernel; then wave-per-pass (B > 21) or lane-pipelined (window
-    // fits the register FIFO); the one-lane-per-spectrum kernel otherwise.
+    // the chain kernel; then lane-pipelined (window fits the register FIFO); the
+    // one-lane-per-spectrum kernel otherwise (wave-per-pass only when forced).
     // MDG_SMOOTH = chain | waves | pipe | generic forces one (tests); an
     // unsupported shape falls through. fused_prep (chain only): the chain kernel
     // runs k_prep's work itself.
@@ -4070,7 +4070,11 @@ const char* launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int
             default: break;
         }
     }
-    const bool waves = force ? std::string(force) == "waves" : a.B > 21;
+    // beyond the chain's batch limit the lane-pipelined kernel beats one wave per
+    // pass (tools/smooth_sweep.sh: 131072 points, B = 1024: 4.8 against 9.9 ms;
+    // configs[3], 4096 x 65536: 2.7 against 17.0 ms), so the wave kernel is only
+    // taken when forced
+    const bool waves = force && std::string(force) == "waves";
     if (waves && iters >= 1 && iters <= 8 && a.N > ws + 1) {
         switch (ws) {
             case 2: return launch_waves<2>(a, w, iters, st);

@@ -5,8 +5,8 @@ Lorentzians, SURVEY 8d recipe) in ONE batched device call
 (mdg_deconvolute_batch_device: the B > 8 grid layouts -- spectrum-interleaved
 fit grid, CU-interleaved MSE grid, k_smooth_chain at B*passes = 768 -- that no
 smaller test reaches). configs[3]: 4096 synthetic 65536-point spectra (1024
-Lorentzians, half widths x2) in one call on one GPU: the k_smooth_waves path
-(B*passes > 2048) at its largest size.
+Lorentzians, half widths x2) in one call on one GPU: the lane-pipelined
+k_smooth_pipe path (B*passes > 2048, beyond the chain) at its largest size.
 
 Every spectrum is compared with the oracle (the C restatement, run on the box's
 cores as the checker; the spectra come from the device generator, which is
@@ -95,7 +95,7 @@ def test_configs2_256x131072_bit_exact():
 def test_configs3_4096x65536_bit_exact():
     cap = 2048
     res = _device_batch(4096, 65536, 1024, 2.0, cap)
-    assert res["kernels"]["smooth"].startswith("k_smooth_waves<3>")
+    assert res["kernels"]["smooth"].startswith("k_smooth_pipe<3>")
     counts = _compare(res, cap)
     assert counts.min() > 900
     res["ctx"].close()
