@@ -35,7 +35,7 @@ for v in "$@"; do
     kdevg) one kdevg HIP_FORCE_DEV_KERNARG=1 MDG_GRAPHS=1 -- ;;
     nograph16) one nograph16 MDG_GRAPHS=0 -- --streams 16 ;;
     nograph24) one nograph24 MDG_GRAPHS=0 -- --streams 24 ;;
-    tf) one tf MDG_FITSUP=tf -- ;;
+    fit_*) one "$v" MDG_FITSUP="${v#fit_}" -- ;;
     s[0-9]*) one "$v" -- --streams "${v#s}" ;;
     dup_*) one "$v" MDG_DIAG_DUP="${v#dup_}" -- ;;
     noexcl_dup_smooth) one "$v" MDG_CHAIN_EXCL=0 MDG_DIAG_DUP=smooth -- ;;
