@@ -9,8 +9,8 @@ spectrum (--batch 1); inputs are resident in HBM before timing.
 
 Steps are submitted round-robin to --streams engine contexts (one HIP stream and
 one HBM workspace each; default 20, with GPU_MAX_HW_QUEUES=32 so every stream has
-its own hardware queue; from 24 streams on the queues are oversubscribed and the
-throughput drops by a quarter), the way concurrent callers of the reference's
+its own hardware queue; from 23 streams on the queues are oversubscribed and the
+throughput drops by a third), the way concurrent callers of the reference's
 `par_deconvolute_spectrum` (Deconvoluter is Send + Sync, deconvoluter.rs:913-917)
 would use one GPU: the sequential smoothers of some spectra overlap the fits and
 MSEs of others. `value` is that stream's throughput; `latency_ms` is one
