@@ -625,6 +625,7 @@ def main():
         "stages_ms_per_spectrum": h["stages_ms_per_spectrum"],
         "stages_source": "separate profiled pass on one context (hipEvents around every stage)",
         "cpu_baseline": None,
+        "build": {k: v for k, v in nat.build_info().items() if k != "compiler"},
     }
     if rank == 0 and world == 1:
         torch.cuda.synchronize()

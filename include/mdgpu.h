@@ -88,6 +88,9 @@ typedef struct mdg_ctx mdg_ctx;
 
 /* ---- host-only helpers (no GPU needed) ---------------------------------- */
 int mdg_abi_version(void);
+/* Build provenance, "src=<sha256/16 of the engine sources> compiler=<hipcc clang>"
+ * (no reference counterpart: lets a caller check the library matches its sources). */
+const char* mdg_build_info(void);
 const char* mdg_strerror(int status);
 void mdg_settings_default(mdg_settings* s);
 int mdg_settings_validate(const mdg_settings* s);

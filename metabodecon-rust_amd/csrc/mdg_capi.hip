@@ -447,6 +447,16 @@ extern "C" {
 
 int mdg_abi_version(void) { return MDG_ABI_VERSION; }
 
+#ifndef MDG_SOURCE_HASH
+#define MDG_SOURCE_HASH "unknown"
+#endif
+// build provenance: the Makefile's sha256 (16 hex digits) of the engine sources this
+// library was compiled from; metabodecon/_native.py refuses a library whose hash
+// does not match the tree next to it
+const char* mdg_build_info(void) {
+    return "src=" MDG_SOURCE_HASH " compiler=" __clang_version__;
+}
+
 const char* mdg_strerror(int st) {
     // messages of deconvolution/error.rs:105-168 where the kind exists there
     switch (st) {

@@ -37,7 +37,7 @@ STAGE_NAMES = ["prep", "smooth", "detect", "select", "fit_init", "fit_superposit
 
 # every symbol include/mdgpu.h declares (checked by tests/test_capi_exports.py)
 EXPORTS = [
-    "mdg_abi_version", "mdg_strerror", "mdg_settings_default", "mdg_settings_validate",
+    "mdg_abi_version", "mdg_build_info", "mdg_strerror", "mdg_settings_default", "mdg_settings_validate",
     "mdg_ignore_region_add", "mdg_synth_lorentzians", "mdg_synth_noise", "mdg_device_count",
     "mdg_ctx_create", "mdg_ctx_destroy", "mdg_ctx_set_stream", "mdg_ctx_synchronize",
     "mdg_ctx_set_profiling", "mdg_ctx_stage_times", "mdg_ctx_reset_stage_times",
@@ -87,6 +87,35 @@ _sz = ctypes.c_size_t
 _lib = None
 _lib_lock = threading.Lock()
 
+# the engine sources in the Makefile's order (SRC then HDR): their sha256 is compiled
+# into the library (mdg_build_info) so a stale build is refused at load time
+_PKG_ROOT = os.path.dirname(_HERE)
+SOURCE_FILES = ["csrc/mdg_kernels.hip", "csrc/mdg_capi.hip", "csrc/mdg_common.hpp",
+                "csrc/mdg_kernels.hpp", "csrc/mdg_chain_asm.inc", "../include/mdgpu.h"]
+
+
+def source_hash() -> str | None:
+    """sha256 (first 16 hex digits) of the engine sources next to this package, as
+    the Makefile computes it; None when the sources are not present."""
+    import hashlib
+    h = hashlib.sha256()
+    for rel in SOURCE_FILES:
+        path = os.path.join(_PKG_ROOT, rel)
+        if not os.path.exists(path):
+            return None
+        with open(path, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def build_info() -> dict:
+    """{"src": hash the library was built from, "tree": hash of the sources here,
+    "compiler": ..., "path": loaded library}."""
+    raw = lib().mdg_build_info().decode()
+    src, _, comp = raw.partition(" compiler=")
+    return {"src": src.removeprefix("src="), "tree": source_hash(), "compiler": comp,
+            "path": os.path.realpath(LIB_PATH)}
+
 
 def _share_torch_hip_runtime():
     """torch (ROCm wheel) bundles its own libamdhip64.so.7 with the same SONAME as
@@ -113,13 +142,28 @@ def lib() -> ctypes.CDLL:
                 _share_torch_hip_runtime()
                 L = ctypes.CDLL(LIB_PATH)
                 _declare(L)
+                _check_provenance(L)
                 _lib = L
     return _lib
+
+
+def _check_provenance(L):
+    """Refuse a library built from other sources than the tree next to it (a stale
+    build would silently run old kernels); MDGPU_ALLOW_STALE=1 skips the check."""
+    if os.environ.get("MDGPU_ALLOW_STALE"):
+        return
+    built = L.mdg_build_info().decode().split(" ")[0].removeprefix("src=")
+    tree = source_hash()
+    if tree is not None and built != tree:
+        raise NativeLibraryError(
+            f"{LIB_PATH} was built from sources {built}, the tree has {tree}: rebuild it "
+            "with `make -C metabodecon-rust_amd`")
 
 
 def _declare(L):
     sp = ctypes.POINTER(Settings)
     L.mdg_abi_version.restype = ctypes.c_int
+    L.mdg_build_info.restype = ctypes.c_char_p
     L.mdg_strerror.argtypes = [ctypes.c_int]
     L.mdg_strerror.restype = ctypes.c_char_p
     L.mdg_settings_default.argtypes = [sp]

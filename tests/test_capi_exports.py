@@ -50,6 +50,32 @@ def test_abi_version_and_strerror():
     assert _native.strerror(3) == "no peaks found in the signal-free region of the spectrum"
 
 
+def test_library_built_from_the_tree_sources():
+    """Build provenance: the hash compiled into libmdgpu.so (Makefile SRC_HASH) equals
+    the sha256 of the engine sources in this tree, so the library the GPU tests load
+    is the one these sources make."""
+    from metabodecon import _native
+    info = _native.build_info()
+    assert info["tree"] is not None and len(info["src"]) == 16
+    assert info["src"] == info["tree"], info
+    mk = open(os.path.join(ROOT, "metabodecon-rust_amd", "Makefile")).read()
+    m = re.search(r"^SRC = (.*)\nHDR = (.*)$", mk, re.M)
+    assert (m.group(1).split() + m.group(2).split()) == _native.SOURCE_FILES
+
+
+def test_stale_library_is_refused(monkeypatch):
+    from metabodecon import _native
+    L = _native.lib()
+    monkeypatch.delenv("MDGPU_ALLOW_STALE", raising=False)
+    monkeypatch.setattr(_native, "source_hash", lambda: "0" * 16)
+    try:
+        _native._check_provenance(L)
+    except _native.NativeLibraryError as e:
+        assert "rebuild" in str(e)
+    else:
+        raise AssertionError("stale library accepted")
+
+
 def _hipflags():
     mk = open(os.path.join(ROOT, "metabodecon-rust_amd", "Makefile")).read()
     m = re.search(r"^HIPFLAGS \?= (.*?)(?<!\\)\n", mk.replace("\\\n", " "), re.M | re.S)
