@@ -4,10 +4,13 @@ Metric (BASELINE.json): spectra/s for 131072-point spectra with ~2k peaks.
 Headline workload (configs[1]): synthetic 131072-point f64 spectra with 2048
 injected Lorentzians (jittered grid, SURVEY 8d recipe, generated on the device),
 full default Deconvoluter (MA 3x3 smoothing, noise-score selection thr 5,
-analytical fit 10 iterations, MSE). One step = one deconvolution of one distinct
-spectrum (--batch 1); inputs are resident in HBM before timing.
+analytical fit 10 iterations, MSE). One step = one round of the stream: --streams
+distinct spectra (--batch 1 each), one per engine context, all in flight together;
+inputs are resident in HBM before timing. (A step used to be one spectrum: with
+the driver's --steps 20 that timed a single cold burst of 20 spectra, mostly the
+pipeline's fill and drain.)
 
-Steps are submitted round-robin to --streams engine contexts (one HIP stream and
+Spectra are submitted round-robin to --streams engine contexts (one HIP stream and
 one HBM workspace each; default 20, with GPU_MAX_HW_QUEUES=32 so every stream has
 its own hardware queue; from 23 streams on the queues are oversubscribed and the
 throughput drops by a third), the way concurrent callers of the reference's
@@ -64,7 +67,8 @@ CPU_REPS = 5
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=240)
+    ap.add_argument("--steps", type=int, default=24,
+                    help="rounds of the stream (--streams spectra each)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1, help="spectra per step (headline)")
     ap.add_argument("--streams", type=int, default=20,
@@ -302,18 +306,20 @@ def synth_device(nat, ctx, torch, B, n, peaks, seed0, dev, hw_scale=1.0):
 
 
 def headline(args, nat, torch, dist, dev, rank, world):
-    """configs[1] stream: args.steps distinct spectra over args.streams contexts."""
+    """configs[1] stream: args.steps rounds of args.streams distinct spectra (one per
+    context); KS = steps * streams engine calls in the timed region."""
     B, n, cap, K, W, S = args.batch, args.n, args.cap, args.steps, args.warmup, args.streams
+    KS, WS = K * S, W * S  # engine calls timed / warm-up
     settings = nat.default_settings()
     if args.fit_iterations:
         settings.fit_iterations = args.fit_iterations
     slots = [Slot(nat, torch, dev, B, n, cap) for _ in range(S)]
-    R = max(K, W, 1)  # distinct spectra (B each), seeds rank*R*B ...
+    R = max(KS, WS, 1)  # distinct spectra (B each), seeds rank*R*B ...
     x, Y = synth_device(nat, slots[0].ctx, torch, R * B, n, args.peaks, rank * R * B, dev,
                         args.hw_scale)
     Y = Y.view(R, B, n)
     sb = torch.tensor([SB] * B, dtype=torch.float64, device=dev)
-    res = torch.zeros((K, slots[0].rec.numel()), dtype=torch.float64, device=dev)
+    res = torch.zeros((KS, slots[0].rec.numel()), dtype=torch.float64, device=dev)
 
     def submit(k, j, nslots):
         # the engine reads spectrum j where it lies and writes step k's results
@@ -324,24 +330,24 @@ def headline(args, nat, torch, dist, dev, rank, world):
             with torch.cuda.stream(s.stream):
                 s.y.copy_(Y[j])
                 run_batch(nat, s, B, n, x, s.y, sb, settings, cap)
-                if k < K:
+                if k < KS:
                     res[k].copy_(s.rec)
             return
-        run_batch(nat, s, B, n, x, Y[j], sb, settings, cap, rec=res[k] if k < K else None)
+        run_batch(nat, s, B, n, x, Y[j], sb, settings, cap, rec=res[k] if k < KS else None)
 
-    for k in range(max(W, S)):  # every context sizes its workspace (and captures its graph)
-        submit(K + k, k % R, S)
+    for k in range(max(WS, S)):  # every context sizes its workspace (and captures its graph)
+        submit(KS + k, k % R, S)
     torch.cuda.synchronize()
     if world > 1:  # RCCL connections are set up by the first collectives, not in the timing
-        g_res = torch.empty((world * K, res.shape[1]), dtype=torch.float64, device=dev)
+        g_res = torch.empty((world * KS, res.shape[1]), dtype=torch.float64, device=dev)
         dist.all_gather_into_tensor(g_res, res)
         torch.cuda.synchronize()
     # latency: one context, one spectrum at a time on an otherwise idle GPU
     lat = []
-    for k in range(min(K, 10)):
+    for k in range(min(KS, 10)):
         torch.cuda.synchronize()
         t = time.perf_counter()
-        submit(K, k % R, 1)
+        submit(KS, k % R, 1)
         torch.cuda.synchronize()
         lat.append(time.perf_counter() - t)
     # timed region
@@ -349,9 +355,9 @@ def headline(args, nat, torch, dist, dev, rank, world):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(K):
+    for k in range(KS):
         submit(k, k % R, S)
-    submit_s = time.perf_counter() - t0  # host time to enqueue the K steps
+    submit_s = time.perf_counter() - t0  # host time to enqueue the KS calls
     torch.cuda.synchronize()
     if world > 1:  # RCCL gather of every rank's result records (the weak-scaling exchange)
         dist.all_gather_into_tensor(g_res, res)
@@ -368,7 +374,7 @@ def headline(args, nat, torch, dist, dev, rank, world):
     # profiled pass (stage times, roofline) on slot 0, outside the timed region
     s0 = slots[0]
     prof = {}
-    prof_steps = min(K, 5)
+    prof_steps = min(KS, 5)
     if not args.no_profile:
         with torch.cuda.stream(s0.stream):
             s0.y.copy_(Y[0])
@@ -381,8 +387,8 @@ def headline(args, nat, torch, dist, dev, rank, world):
     roof = (roofline_from_stages(s0.ctx, prof, work, f"b{B}", n) if prof else None)
     kept = res_cnt.cpu().numpy()
     out = {
-        "elapsed": elapsed, "spectra": world * K * B, "latency_ms": 1e3 * statistics.median(lat),
-        "host_submit_ms_per_step": 1e3 * submit_s / K,
+        "elapsed": elapsed, "spectra": world * KS * B, "latency_ms": 1e3 * statistics.median(lat),
+        "host_submit_ms_per_call": 1e3 * submit_s / KS,
         "roofline": roof,
         "stages_ms_per_spectrum": {k: v[0] / prof_steps / B for k, v in prof.items() if v[1]},
         "selected_peaks": P_sel[:4], "kept_peaks": [int(c) for c in kept[:4, 0]],
@@ -605,19 +611,22 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": h["elapsed"] / args.steps * 1e3,
         "latency_ms": h["latency_ms"],
-        "latency_in_stream_ms": args.streams * h["elapsed"] / args.steps * 1e3,
-        "host_submit_ms_per_step": h["host_submit_ms_per_step"],
+        # Little's law: streams in flight / throughput = elapsed per round
+        "latency_in_stream_ms": h["elapsed"] / args.steps * 1e3,
+        "host_submit_ms_per_call": h["host_submit_ms_per_call"],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (device-generated, distinct seeds per step and rank)",
         "config": {"workload": ("configs[1]: synthetic 131072-pt f64 spectra, 2048 injected "
-                                "Lorentzians, default Deconvoluter, one distinct spectrum per "
-                                "step" if B == 1 else
-                                f"batch of {B} synthetic spectra per GPU per step"),
+                                "Lorentzians, default Deconvoluter; a step is one round of "
+                                f"{args.streams} distinct spectra, one per engine context "
+                                "(own HIP stream), in flight together" if B == 1 else
+                                f"{args.streams} contexts x batch of {B} synthetic spectra per "
+                                "GPU per step"),
                    "n_points": args.n, "injected_peaks": args.peaks,
-                   "spectra_per_gpu_per_step": B, "streams": args.streams,
+                   "spectra_per_gpu_per_step": B * args.streams, "streams": args.streams,
                    "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]),
                    "selected_peaks": h["selected_peaks"], "kept_peaks": h["kept_peaks"],
                    "parallelism": f"dp{world}" if world > 1 else "single"},

@@ -19,8 +19,8 @@ for step in "$@"; do
     tests) run pytest_gpu 1200 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
     tests_all) run pytest_gpu 1200 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ;;
     bench) run bench1 600 python bench.py ;;
-    bench64) run bench64 600 python bench.py --batch 64 --steps 5 --warmup 1 --no-cpu-baseline ;;
-    bench256) run bench256 600 python bench.py --batch 256 --steps 3 --warmup 1 --no-cpu-baseline ;;
+    bench64) run bench64 600 python bench.py --batch 64 --streams 1 --steps 5 --warmup 1 --no-cpu-baseline ;;
+    bench256) run bench256 600 python bench.py --batch 256 --streams 1 --steps 3 --warmup 1 --no-cpu-baseline ;;
     *) echo "unknown step $step" ;;
   esac
 done

@@ -4,7 +4,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 timeout -k 10 120 python bench.py --no-configs --no-cpu-baseline --streams 1 --steps 40 > gpurun_out/q_b1.json &&
 timeout -k 10 120 python bench.py --no-configs --no-cpu-baseline --streams 1 --batch 256 --steps 2 --warmup 1 > gpurun_out/q_b256.json &&
-timeout -k 10 120 python bench.py --no-configs --no-cpu-baseline --no-profile --steps 480 > gpurun_out/q_s20.json &&
+timeout -k 10 120 python bench.py --no-configs --no-cpu-baseline --no-profile --steps 24 > gpurun_out/q_s20.json &&
 python - <<'PY'
 import json
 for t in ("b1", "b256", "s20"):

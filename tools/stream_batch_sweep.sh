@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/sweep_batch
 for cfg in "1 20" "2 10" "2 16" "2 20" "4 8" "4 12" "4 16" "8 8"; do
   set -- $cfg
-  B=$1; S=$2; K=$(( 480 / B ))
+  B=$1; S=$2; K=$(( 480 / (B * S) ))  # rounds of S calls
   out=gpurun_out/sweep_batch/b${B}_s${S}.json
   timeout -k 10 180 python bench.py --batch "$B" --streams "$S" --steps "$K" --warmup 3 \
       --no-configs --no-cpu-baseline --no-profile > "$out" 2> "${out%.json}.err"
