@@ -360,3 +360,15 @@ def lane_contexts(device: int | None, n: int) -> list[Context]:
         while len(lanes) < n:
             lanes.append(Context(device))
         return lanes[:n]
+
+
+def release_lanes(device: int | None = None) -> None:
+    """Destroy the lane contexts of `device` (all devices when None): their idle
+    streams still hold hardware queues, and with 16 of them alive a single-stream
+    pipeline on the same GPU ran ~15% slower. They are re-created on
+    the next concurrent call."""
+    with _ctx_lock:
+        for d in ([device] if device is not None else list(_lanes)):
+            for c in _lanes.pop(d, []):
+                with c.lock:
+                    c.close()

@@ -103,6 +103,26 @@ def test_detected_peaks_match_oracle(ctx, path, monkeypatch):
     assert np.array_equal(ctx.last_peaks(0, "selected").astype(np.int64), g["selected"])
 
 
+def test_concurrent_lanes_and_release(monkeypatch):
+    """The 16 blood spectra one per lane context (16 concurrent engine contexts, as
+    bench.py's configs[4] runs them), bit-equal to the goldens; then the lanes are
+    released and re-created by the next call."""
+    import metabodecon as md
+    from metabodecon import _native as nat
+    monkeypatch.setattr(md.Deconvoluter, "LANES", 16)
+    spectra = md.Spectrum.read_bruker_set(os.path.join(GOLDEN, "bruker", "blood"), 10, 10,
+                                          (-2.2, 11.8))
+    for rnd in range(2):
+        decs = md.Deconvoluter().par_deconvolute_spectra(spectra)
+        for k, d in enumerate(decs):
+            g = np.load(os.path.join(GOLDEN, "expected", f"blood_{k + 1:02d}.npz"))
+            assert np.array_equal(d.params, g["params"]), (rnd, k)
+            assert abs(d.mse - float(g["mse"])) <= MSE_RTOL * abs(float(g["mse"]))
+        assert len(nat._lanes.get(nat.default_device(), [])) == 16
+        nat.release_lanes()
+        assert not nat._lanes
+
+
 def test_python_api_end_to_end():
     import metabodecon as md
     spectra = md.Spectrum.read_bruker_set(os.path.join(GOLDEN, "bruker", "blood"), 10, 10,
