@@ -11,9 +11,10 @@ the driver's --steps 20 that timed a single cold burst of 20 spectra, mostly the
 pipeline's fill and drain.)
 
 Spectra are submitted round-robin to --streams engine contexts (one HIP stream and
-one HBM workspace each; default 20, with GPU_MAX_HW_QUEUES=32 so every stream has
-its own hardware queue; from 23 streams on the queues are oversubscribed and the
-throughput drops by a third), the way concurrent callers of the reference's
+one HBM workspace each; default 18, with GPU_MAX_HW_QUEUES=32 so every stream has
+its own hardware queue; from about 23 queues in the process, idle ones included,
+the throughput drops by a third, and 18 leaves room for RCCL's own streams in a
+multi-rank run), the way concurrent callers of the reference's
 `par_deconvolute_spectrum` (Deconvoluter is Send + Sync, deconvoluter.rs:913-917)
 would use one GPU: the sequential smoothers of some spectra overlap the fits and
 MSEs of others. `value` is that stream's throughput; `latency_ms` is one
@@ -71,7 +72,7 @@ def parse():
                     help="rounds of the stream (--streams spectra each)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1, help="spectra per step (headline)")
-    ap.add_argument("--streams", type=int, default=20,
+    ap.add_argument("--streams", type=int, default=18,
                     help="engine contexts the steps are spread over (1 = back to back)")
     ap.add_argument("--hw-queues", type=int, default=32,
                     help="GPU_MAX_HW_QUEUES for this process (HIP maps streams onto that "
@@ -89,6 +90,9 @@ def parse():
                     help="stage each step's spectrum and results through the context's own rows")
     ap.add_argument("--fit-iterations", type=int, default=0,
                     help="diagnostics only: override the analytical fit's iterations (0 = 10)")
+    ap.add_argument("--idle-streams", type=int, default=0,
+                    help="diagnostics: keep this many extra idle HIP streams alive (each "
+                         "used once) during the headline, as RCCL's own streams would be")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: exercise the launcher, rendezvous and gather (gloo)")
     return ap.parse_args()
@@ -599,6 +603,11 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
+    idle = [torch.cuda.Stream(device=dev) for _ in range(args.idle_streams)]
+    for st in idle:
+        with torch.cuda.stream(st):
+            torch.ones(1, device=dev).add_(1)  # the stream's hardware queue now exists
+    torch.cuda.synchronize()
     h = headline(args, nat, torch, dist, dev, rank, world)
     value = h["spectra"] / h["elapsed"]
     B = args.batch
