@@ -93,6 +93,9 @@ def parse():
     ap.add_argument("--idle-streams", type=int, default=0,
                     help="diagnostics: keep this many extra idle HIP streams alive (each "
                          "used once) during the headline, as RCCL's own streams would be")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="diagnostics: run the multi-rank path (RCCL process group, gathers) "
+                         "even at world size 1, under torchrun")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: exercise the launcher, rendezvous and gather (gloo)")
     return ap.parse_args()
@@ -314,6 +317,7 @@ def headline(args, nat, torch, dist, dev, rank, world):
     context); KS = steps * streams engine calls in the timed region."""
     B, n, cap, K, W, S = args.batch, args.n, args.cap, args.steps, args.warmup, args.streams
     KS, WS = K * S, W * S  # engine calls timed / warm-up
+    dist_on = world > 1 or args.force_dist
     settings = nat.default_settings()
     if args.fit_iterations:
         settings.fit_iterations = args.fit_iterations
@@ -342,7 +346,7 @@ def headline(args, nat, torch, dist, dev, rank, world):
     for k in range(max(WS, S)):  # every context sizes its workspace (and captures its graph)
         submit(KS + k, k % R, S)
     torch.cuda.synchronize()
-    if world > 1:  # RCCL connections are set up by the first collectives, not in the timing
+    if dist_on:  # RCCL connections are set up by the first collectives, not in the timing
         g_res = torch.empty((world * KS, res.shape[1]), dtype=torch.float64, device=dev)
         dist.all_gather_into_tensor(g_res, res)
         torch.cuda.synchronize()
@@ -355,7 +359,7 @@ def headline(args, nat, torch, dist, dev, rank, world):
         torch.cuda.synchronize()
         lat.append(time.perf_counter() - t)
     # timed region
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -363,12 +367,12 @@ def headline(args, nat, torch, dist, dev, rank, world):
         submit(k, k % R, S)
     submit_s = time.perf_counter() - t0  # host time to enqueue the KS calls
     torch.cuda.synchronize()
-    if world > 1:  # RCCL gather of every rank's result records (the weak-scaling exchange)
+    if dist_on:  # RCCL gather of every rank's result records (the weak-scaling exchange)
         dist.all_gather_into_tensor(g_res, res)
         torch.cuda.synchronize()
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if dist_on:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
@@ -598,7 +602,7 @@ def main():
     import torch.distributed as dist
     from metabodecon import _native as nat
 
-    if world > 1:
+    if world > 1 or args.force_dist:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -695,7 +699,7 @@ def main():
                     configs[key]["speedup_vs_cpu"] = configs[key]["value"] / cb[ref[0]][ref[1]]
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if world > 1 or args.force_dist:
         dist.destroy_process_group()
 
 
