@@ -794,12 +794,12 @@ __global__ __launch_bounds__(512) void k_smooth_waves(BatchArgs a, Workspace w, 
 // on its own CU, in four waves (one per SIMD):
 //  * chain wave: issues little besides the reference's two dependent adds per
 //    tick (moving_average.rs:69-80, in j = i + R form below) on SGPR operands,
-//    and stores one checkpoint per kChainG = 32 ticks (the group's last raw sum);
+//    and stores one checkpoint per kChainG = 48 ticks (the group's last raw sum);
 //  * feeder wave: waits for the previous pass's published blocks (sc1 polls),
 //    publishes them to the chain (in_ready in LDS), pulls them into L2 and
 //    touches them into the scalar cache ahead of the chain;
 //  * two scaler waves, batches of kChainScBatch output blocks round-robin: replay
-//    each group of 32 ticks from its checkpoint with the same two operations
+//    each group of kChainG ticks from its checkpoint with the same two operations
 //    (bit-identical sums), multiply by the reference's 1/len (moving_average.rs:
 //    66-81: 1/len while the buffer grows, 1/ws, then 1/len in the tail) and
 //    publish finished batches to the next pass in batch order (sc1 stores,

@@ -12,7 +12,7 @@ SGPR operands, BPT blocks of CB = 96 ticks per loop trip:
     operand times +1.0 / -1.0 (v[4:5] / v[6:7]) -- fma(a, +-1, s) rounds exactly
     as s +- a, and the dependent VOP2 fmac chain issues in 8.3 cycles per tick
     against 10.3 for VOP3 adds (tools/ubench/eval_cost.hip). Only the last sum
-    of each G = 32 ticks is stored (see block_body);
+    of each G = 48 ticks is stored (see block_body);
   * per block: wait (LDS, cached) until the helper wave has published the input
     block the prefetch reaches; after the trip, s_waitcnt vmcnt(TT/G) proves
     the previous trip's stores complete, then raw_done is published in LDS.
@@ -26,7 +26,7 @@ CB = int(os.environ.get("CHAIN_CB", "96"))  # ticks per block (the feeder / scal
 BPT = int(os.environ.get("CHAIN_BPT", "2"))  # blocks per loop trip (chain_diag, p0 cycles/tick: 1: 10.85, 2: 10.06, 3: 10.28, 4: 12.35)
 TT = CB * BPT        # ticks per trip
 GROUPS = TT // 8     # multiple of 3: buffer rotation period
-G = int(os.environ.get("CHAIN_G", "32"))  # ticks per stored checkpoint (scaler replay group)
+G = int(os.environ.get("CHAIN_G", "48"))  # ticks per stored checkpoint (scaler replay group; 32: smoother 581 us, 48: 573-577, 96: scalers fall behind)
 assert G % 8 == 0 and TT % G == 0 and TT // G <= 63
 RING4 = not os.environ.get("CHAIN_RING3")  # four operand buffers, one lgkmcnt wait per two groups
 # SGPR base of the 8-double buffers (s32 is the stack pointer: not clobbered)
