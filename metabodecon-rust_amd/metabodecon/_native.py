@@ -94,9 +94,24 @@ SOURCE_FILES = ["csrc/mdg_kernels.hip", "csrc/mdg_capi.hip", "csrc/mdg_common.hp
                 "csrc/mdg_kernels.hpp", "csrc/mdg_chain_asm.inc", "../include/mdgpu.h"]
 
 
+def _default_hipflags(makefile: str) -> str | None:
+    """The Makefile's default HIPFLAGS as make expands them (ARCH = gfx950), joined
+    by single spaces as `echo` prints them."""
+    import re
+    try:
+        text = open(makefile).read().replace("\\\n", " ")
+    except OSError:
+        return None
+    m = re.search(r"^HIPFLAGS \?= (.*)$", text, re.M)
+    if not m:
+        return None
+    return " ".join(m.group(1).replace("$(ARCH)", "gfx950").split())
+
+
 def source_hash() -> str | None:
-    """sha256 (first 16 hex digits) of the engine sources next to this package, as
-    the Makefile computes it; None when the sources are not present."""
+    """sha256 (first 16 hex digits) of the engine sources next to this package and
+    the default compile flags, as the Makefile computes it; None when the sources
+    are not present."""
     import hashlib
     h = hashlib.sha256()
     for rel in SOURCE_FILES:
@@ -105,6 +120,10 @@ def source_hash() -> str | None:
             return None
         with open(path, "rb") as f:
             h.update(f.read())
+    flags = _default_hipflags(os.path.join(_PKG_ROOT, "Makefile"))
+    if flags is None:
+        return None
+    h.update((flags + "\n").encode())
     return h.hexdigest()[:16]
 
 
@@ -156,7 +175,7 @@ def _check_provenance(L):
     tree = source_hash()
     if tree is not None and built != tree:
         raise NativeLibraryError(
-            f"{LIB_PATH} was built from sources {built}, the tree has {tree}: rebuild it "
+            f"{LIB_PATH} was built from sources+flags {built}, the tree has {tree}: rebuild it "
             "with `make -C metabodecon-rust_amd`")
 
 
