@@ -450,11 +450,14 @@ int mdg_abi_version(void) { return MDG_ABI_VERSION; }
 #ifndef MDG_SOURCE_HASH
 #define MDG_SOURCE_HASH "unknown"
 #endif
+#ifndef MDG_FLAGS_HASH
+#define MDG_FLAGS_HASH "unknown"
+#endif
 // build provenance: the Makefile's sha256 (16 hex digits) of the engine sources this
-// library was compiled from; metabodecon/_native.py refuses a library whose hash
-// does not match the tree next to it
+// library was compiled from, and of its compile flags; metabodecon/_native.py refuses
+// a library whose source hash does not match the tree next to it
 const char* mdg_build_info(void) {
-    return "src=" MDG_SOURCE_HASH " compiler=" __clang_version__;
+    return "src=" MDG_SOURCE_HASH " flags=" MDG_FLAGS_HASH " compiler=" __clang_version__;
 }
 
 const char* mdg_strerror(int st) {

@@ -109,9 +109,8 @@ def _default_hipflags(makefile: str) -> str | None:
 
 
 def source_hash() -> str | None:
-    """sha256 (first 16 hex digits) of the engine sources next to this package and
-    the default compile flags, as the Makefile computes it; None when the sources
-    are not present."""
+    """sha256 (first 16 hex digits) of the engine sources next to this package, as
+    the Makefile computes it (SRC_HASH); None when the sources are not present."""
     import hashlib
     h = hashlib.sha256()
     for rel in SOURCE_FILES:
@@ -120,19 +119,35 @@ def source_hash() -> str | None:
             return None
         with open(path, "rb") as f:
             h.update(f.read())
-    flags = _default_hipflags(os.path.join(_PKG_ROOT, "Makefile"))
-    if flags is None:
-        return None
-    h.update((flags + "\n").encode())
     return h.hexdigest()[:16]
 
 
+def flags_hash() -> str | None:
+    """sha256 (16 hex digits) of the Makefile's default HIPFLAGS (FLAGS_HASH)."""
+    import hashlib
+    flags = _default_hipflags(os.path.join(_PKG_ROOT, "Makefile"))
+    if flags is None:
+        return None
+    return hashlib.sha256((flags + "\n").encode()).hexdigest()[:16]
+
+
+def _parse_build_info(raw: str) -> dict:
+    out = {}
+    head, _, comp = raw.partition(" compiler=")
+    for tok in head.split():
+        k, _, v = tok.partition("=")
+        out[k] = v
+    out["compiler"] = comp
+    return out
+
+
 def build_info() -> dict:
-    """{"src": hash the library was built from, "tree": hash of the sources here,
-    "compiler": ..., "path": loaded library}."""
-    raw = lib().mdg_build_info().decode()
-    src, _, comp = raw.partition(" compiler=")
-    return {"src": src.removeprefix("src="), "tree": source_hash(), "compiler": comp,
+    """{"src": source hash the library was built from, "tree": hash of the sources
+    here, "flags": hash of its compile flags, "default_flags": hash of the
+    Makefile's defaults, "compiler": ..., "path": loaded library}."""
+    b = _parse_build_info(lib().mdg_build_info().decode())
+    return {"src": b.get("src"), "tree": source_hash(), "flags": b.get("flags"),
+            "default_flags": flags_hash(), "compiler": b["compiler"],
             "path": os.path.realpath(LIB_PATH)}
 
 
@@ -168,15 +183,22 @@ def lib() -> ctypes.CDLL:
 
 def _check_provenance(L):
     """Refuse a library built from other sources than the tree next to it (a stale
-    build would silently run old kernels); MDGPU_ALLOW_STALE=1 skips the check."""
+    build would silently run old kernels); MDGPU_ALLOW_STALE=1 skips the check. A
+    build with other compile flags than the Makefile's defaults (make ARCH=..., an
+    A/B -D override) is only reported: same sources, deliberate flags."""
     if os.environ.get("MDGPU_ALLOW_STALE"):
         return
-    built = L.mdg_build_info().decode().split(" ")[0].removeprefix("src=")
+    b = _parse_build_info(L.mdg_build_info().decode())
     tree = source_hash()
-    if tree is not None and built != tree:
+    if tree is not None and b.get("src") != tree:
         raise NativeLibraryError(
-            f"{LIB_PATH} was built from sources+flags {built}, the tree has {tree}: rebuild it "
+            f"{LIB_PATH} was built from sources {b.get('src')}, the tree has {tree}: rebuild it "
             "with `make -C metabodecon-rust_amd`")
+    dflt = flags_hash()
+    if dflt is not None and b.get("flags") != dflt:
+        import warnings
+        warnings.warn(f"{LIB_PATH} was built with non-default compile flags "
+                      f"({b.get('flags')} != {dflt})", RuntimeWarning, stacklevel=3)
 
 
 def _declare(L):
@@ -345,13 +367,24 @@ _ctx: dict[int, Context] = {}
 _ctx_lock = threading.Lock()
 
 
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    lib().mdg_device_count(ctypes.byref(n))
+    return n.value
+
+
 def default_device() -> int:
-    """MDGPU_DEVICE if set; else LOCAL_RANK (one process per GPU under torchrun,
-    so every rank runs on its own device); else 0."""
-    for var in ("MDGPU_DEVICE", "LOCAL_RANK"):
-        env = os.environ.get(var)
-        if env is not None:
-            return int(env)
+    """MDGPU_DEVICE if set; else LOCAL_RANK modulo the visible devices (one process
+    per GPU under torchrun sees all GPUs and takes its own; a launcher that exposes
+    one GPU per rank, HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES, leaves device 0);
+    else 0."""
+    env = os.environ.get("MDGPU_DEVICE")
+    if env is not None:
+        return int(env)
+    env = os.environ.get("LOCAL_RANK")
+    if env is not None:
+        n = device_count()
+        return int(env) % n if n > 0 else 0
     return 0
 
 

@@ -58,6 +58,7 @@ def test_library_built_from_the_tree_sources():
     info = _native.build_info()
     assert info["tree"] is not None and len(info["src"]) == 16
     assert info["src"] == info["tree"], info
+    assert info["flags"] == info["default_flags"] and len(info["flags"]) == 16, info
     mk = open(os.path.join(ROOT, "metabodecon-rust_amd", "Makefile")).read()
     m = re.search(r"^SRC = (.*)\nHDR = (.*)$", mk, re.M)
     assert (m.group(1).split() + m.group(2).split()) == _native.SOURCE_FILES
@@ -74,6 +75,20 @@ def test_stale_library_is_refused(monkeypatch):
         assert "rebuild" in str(e)
     else:
         raise AssertionError("stale library accepted")
+
+
+def test_other_compile_flags_only_warn(monkeypatch):
+    """Same sources built with other flags (make ARCH=..., an A/B -D override) load
+    with a warning; only a source mismatch is refused."""
+    import warnings
+    from metabodecon import _native
+    L = _native.lib()
+    monkeypatch.delenv("MDGPU_ALLOW_STALE", raising=False)
+    monkeypatch.setattr(_native, "flags_hash", lambda: "f" * 16)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        _native._check_provenance(L)
+    assert any("non-default compile flags" in str(x.message) for x in w)
 
 
 def _hipflags():

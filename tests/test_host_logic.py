@@ -213,3 +213,20 @@ def test_ignore_region_engine_limit_is_reported_at_add_time():
     assert d.ignore_regions == before
     d.add_ignore_region((0.0, 0.12))  # merges with existing ones: still accepted
     assert len(d.ignore_regions) == Deconvoluter.MAX_IGNORE - 1
+
+
+@pytest.mark.parametrize("visible,local_rank,want", [(1, "1", 0), (1, "3", 0), (8, "3", 3),
+                                                      (2, "5", 1), (0, "2", 0)])
+def test_default_device_wraps_local_rank_to_visible_devices(monkeypatch, visible, local_rank,
+                                                            want):
+    """A launcher that exposes one GPU per rank (HIP_VISIBLE_DEVICES) with LOCAL_RANK>0
+    must still land on a device that exists (LOCAL_RANK used unchecked)."""
+    monkeypatch.delenv("MDGPU_DEVICE", raising=False)
+    monkeypatch.setenv("LOCAL_RANK", local_rank)
+    monkeypatch.setattr(nat, "device_count", lambda: visible)
+    assert nat.default_device() == want
+    monkeypatch.setenv("MDGPU_DEVICE", "1")
+    assert nat.default_device() == 1
+    monkeypatch.delenv("MDGPU_DEVICE")
+    monkeypatch.delenv("LOCAL_RANK")
+    assert nat.default_device() == 0
