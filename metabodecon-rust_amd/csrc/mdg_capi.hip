@@ -55,7 +55,9 @@ struct mdg_ctx {
     // a fixed place for every (B, P) the chain supports (B * P <= 2048), zeroed
     // once and left at zero by every run (k_flags), so no run has to clear them
     Buffer chain_flags;
-    Buffer ign;  // the call's merged ignore regions (2 * kMaxIgnore doubles)
+    Buffer ign;  // the call's merged ignore regions (ppm pairs, device row)
+    std::vector<double> ign_last;  // the regions the device row holds now
+    int ws_igcap = 0;  // ignore-region pairs per spectrum row of the arena
     // optimize_settings: per-spectrum overrides for the next run_pipeline, buffers
     const double* ovr_thr = nullptr;
     const int32_t* ovr_fit = nullptr;
@@ -162,9 +164,11 @@ void drain_timers(mdg_ctx* c) {
 
 size_t align256(size_t v) { return (v + 255) & ~size_t(255); }
 
-int ensure_workspace(mdg_ctx* c, int B, int N) {
-    if (!(B <= c->ws_B && N <= c->ws_N && c->arena.p)) {
+int ensure_workspace(mdg_ctx* c, int B, int N, int n_ignore) {
+    const int igcap = std::max(kIgnoreRow, (n_ignore + kIgnoreRow - 1) / kIgnoreRow * kIgnoreRow);
+    if (!(B <= c->ws_B && N <= c->ws_N && igcap <= c->ws_igcap && c->arena.p)) {
         const int nB = std::max(B, c->ws_B), nN = std::max(N, c->ws_N);
+        const int nIg = std::max(igcap, c->ws_igcap);
         const size_t W = (size_t)(nN + 63) / 64;
         const size_t capD = (size_t)nN / 2 + 2;
         const size_t Bs = (size_t)nB;
@@ -181,7 +185,7 @@ int ensure_workspace(mdg_ctx* c, int B, int N) {
         const size_t o_msep = take(Bs * kMseMaxParts * 8);
         const size_t o_sfr = take(Bs * 16);
         const size_t o_sbi = take(Bs * 16);
-        const size_t o_ig = take(Bs * 2 * kMaxIgnore * 8);
+        const size_t o_ig = take(Bs * 2 * (size_t)nIg * 8), o_igc = take(Bs * ((size_t)nIg + 2) * 8);
         const size_t o_nig = take(Bs * 4), o_panic = take(Bs * 4), o_status = take(Bs * 4);
         const size_t o_dcnt = take(Bs * 4), o_scnt = take(Bs * 4), o_kcnt = take(Bs * 4);
         const size_t o_xok = take(Bs * 4), o_unsafe = take(Bs * 16), o_uk = take(Bs * 4);
@@ -216,6 +220,8 @@ int ensure_workspace(mdg_ctx* c, int B, int N) {
         w.sfr_stats = (double*)(base + o_sfr);
         w.sbi = (int64_t*)(base + o_sbi);
         w.ig = (int64_t*)(base + o_ig);
+        w.ig_cum = (int64_t*)(base + o_igc);
+        w.ig_cap = nIg;
         w.n_ig = (int32_t*)(base + o_nig);
         w.mse_panic = (int32_t*)(base + o_panic);
         w.status = (int32_t*)(base + o_status);
@@ -232,6 +238,7 @@ int ensure_workspace(mdg_ctx* c, int B, int N) {
 
         c->ws_B = nB;
         c->ws_N = nN;
+        c->ws_igcap = nIg;
         ++c->ws_gen;
     }
     return MDG_OK;
@@ -265,14 +272,14 @@ int validate_common(const mdg_settings* s, size_t n_ignore, const double* ignore
     if (!s) return MDG_INVALID_ARGUMENT;
     int v = mdg_settings_validate(s);
     if (v) return v;
-    if (n_ignore > (size_t)kMaxIgnore) return MDG_INVALID_ARGUMENT;
+    if (n_ignore > (size_t)(INT32_MAX / 4)) return MDG_INVALID_ARGUMENT;
     if (n_ignore > 0 && !ignore) return MDG_INVALID_ARGUMENT;
     return MDG_OK;
 }
 
 // Runs the whole pipeline for a device-resident batch. Caller holds c->mu.
 int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
-    int rc = ensure_workspace(c, a.B, a.N);
+    int rc = ensure_workspace(c, a.B, a.N, a.n_ignore);
     if (rc) return rc;
     // Row strides follow the current shape; the arena is sized for the largest
     // (B, N) seen so far, so every current-shape row fits.
@@ -406,10 +413,12 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     return MDG_OK;
 }
 
-// The per-call arguments. The ignore regions (host memory) go to the context's
-// device row on its stream, ahead of the pipeline, so the kernels' argument block
-// stays small (every launch copies it: ≈0.5 KB instead of 1.5 KB with the
-// regions inline).
+// The per-call arguments. The ignore regions (host memory, any number of merged
+// pairs) go to the context's device row on its stream, ahead of the pipeline, so
+// the kernels' argument block stays small (every launch copies it). The row is
+// uploaded only when the regions differ from the ones it holds (the usual caller
+// passes the same Deconvoluter's regions every call): no host-to-device copy, and
+// no pageable-copy stall, in a stream of calls.
 int fill_args(mdg_ctx* c, BatchArgs& a, size_t b, size_t n, const double* x, size_t xs, const double* y,
               size_t ys, const double* sb, const double* ignore, size_t n_ignore, double* out,
               size_t cap, int32_t* cnt, double* mse, int32_t* status) {
@@ -424,10 +433,17 @@ int fill_args(mdg_ctx* c, BatchArgs& a, size_t b, size_t n, const double* x, siz
     a.n_ignore = (int)n_ignore;
     a.ignore = nullptr;
     if (n_ignore > 0) {
-        int rc = ensure(c->ign, 2 * kMaxIgnore * sizeof(double));
-        if (rc) return rc;
-        HIPCHK(hipMemcpyAsync(c->ign.p, ignore, 2 * n_ignore * sizeof(double), hipMemcpyHostToDevice,
-                              c->stream));
+        const size_t cnt = 2 * n_ignore;
+        const bool same = c->ign.p && c->ign_last.size() == cnt &&
+                          std::memcmp(c->ign_last.data(), ignore, cnt * sizeof(double)) == 0;
+        if (!same) {
+            const void* old = c->ign.p;
+            int rc = ensure(c->ign, std::max<size_t>(cnt, 2 * kIgnoreRow) * sizeof(double));
+            if (rc) return rc;
+            if (c->ign.p != old) ++c->ws_gen;  // graphs bake the row's address
+            HIPCHK(hipMemcpyAsync(c->ign.p, ignore, cnt * sizeof(double), hipMemcpyHostToDevice, c->stream));
+            c->ign_last.assign(ignore, ignore + cnt);
+        }
         a.ignore = (const double*)c->ign.p;
     }
     a.out = out;
@@ -797,7 +813,7 @@ int run_pipeline_graphed(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
         return run_pipeline(c, a, s);
     // size every buffer first: the capture must not allocate, and the key needs the
     // final addresses
-    int rc = ensure_workspace(c, a.B, a.N);
+    int rc = ensure_workspace(c, a.B, a.N, a.n_ignore);
     if (rc) return rc;
     if (ma && chain_supported(a.B, a.N, (int)s->smooth_iterations, (int)s->smooth_window) &&
         !(std::getenv("MDG_SMOOTH") && std::string(std::getenv("MDG_SMOOTH")) != "chain"))
@@ -1130,7 +1146,7 @@ extern "C" int mdg_optimize_settings(mdg_ctx* c, const double* x, const double* 
                                      size_t n_ignore, mdg_settings* best, double* best_mse) {
     if (!c || !x || !y || !best || !best_mse) return MDG_INVALID_ARGUMENT;
     if (n < 2 || n > (size_t)INT32_MAX / 2) return MDG_INVALID_ARGUMENT;
-    if (n_ignore > (size_t)kMaxIgnore || (n_ignore && !ignore)) return MDG_INVALID_ARGUMENT;
+    if (n_ignore > (size_t)(INT32_MAX / 4) || (n_ignore && !ignore)) return MDG_INVALID_ARGUMENT;
     std::lock_guard<std::mutex> g(c->mu);
     HIPCHK(hipSetDevice(c->device));
     hipStream_t st = c->stream;
@@ -1209,24 +1225,15 @@ extern "C" int mdg_optimize_settings(mdg_ctx* c, const double* x, const double* 
                             (double*)c->opt[BMSE].p, (int32_t*)c->opt[BST].p)))
             return rc;
         if ((rc = run_pipeline(c, a, &s))) return rc;
-        int32_t cnt = 0, sst = 0, nig = 0;
-        int64_t sbi[2], ig[2 * kMaxIgnore];
+        int32_t cnt = 0, sst = 0;
         HIPCHK(hipMemcpyAsync(&cnt, c->opt[BCNT].p, 4, hipMemcpyDeviceToHost, st));
         HIPCHK(hipMemcpyAsync(&sst, c->opt[BST].p, 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipMemcpyAsync(&nig, c->w.n_ig, 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipMemcpyAsync(sbi, c->w.sbi, 16, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipMemcpyAsync(ig, c->w.ig, sizeof(ig), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         if (sst) return sst;
-        ExactRegions r;
-        r.n = nig + 1;
-        for (int q = 0; q <= nig; ++q) {
-            r.lo[q] = q == 0 ? sbi[0] : ig[2 * (q - 1) + 1];
-            r.hi[q] = q == nig ? sbi[1] : ig[2 * q];
-        }
+        // the MSE regions come from the run's own workspace rows (on the device)
         launch_superposition_vec(dx, (int64_t)n, (const double*)c->opt[BOUT].p, cnt,
                                  (double*)c->opt[BSUP].p, (int*)c->opt[BRES].p + 8, st);
-        launch_mse_exact((const double*)c->opt[BSUP].p, dy, (int64_t)n, r, (double*)c->opt[BSCR].p,
+        launch_mse_exact((const double*)c->opt[BSUP].p, dy, (int64_t)n, c->w, (double*)c->opt[BSCR].p,
                          (double*)c->opt[BRES].p, st);
         HIPCHK(hipGetLastError());
         double exact = 0.0;

@@ -21,7 +21,7 @@ namespace mdg {
 // lib.rs:277  CHECK_PRECISION = 1.0e+3 * f64::EPSILON
 constexpr double kCheckPrecision = 1.0e+3 * 2.220446049250313080847e-16;
 constexpr double kEpsilon = 2.220446049250313080847e-16;  // f64::EPSILON
-constexpr int kMaxIgnore = 64;  // merged ignore regions per call (engine limit)
+constexpr int kIgnoreRow = 64;  // ignore-region pairs per spectrum row, grown in steps of this
 constexpr int kMseMaxParts = 2048;  // MSE partial sums per spectrum (workspace rows)
 
 // ---- counter-based splitmix64 (synthetic workload only) ----------------------

@@ -361,7 +361,7 @@ __device__ __forceinline__ void prep_spectrum(const BatchArgs& a, const Workspac
     w.sbi[2 * s] = bi0;
     w.sbi[2 * s + 1] = bi1;
     int nig = 0;
-    int64_t* pairs = w.ig + (size_t)s * 2 * kMaxIgnore;
+    int64_t* pairs = w.ig + (size_t)s * 2 * w.ig_cap;
     if (a.n_ignore > 0) {
         const double lower_b = fmin(sb0, sb1), upper_b = fmax(sb0, sb1);
         const int64_t lower = bi0 < bi1 ? bi0 : bi1, upper = bi0 < bi1 ? bi1 : bi0;
@@ -384,11 +384,17 @@ __device__ __forceinline__ void prep_spectrum(const BatchArgs& a, const Workspac
     w.n_ig[s] = nig;
     // MSE regions (sbi.0, ig0.s), (ig0.e, ig1.s), ... (igk.e, sbi.1); Rust slicing
     // panics when start > end or end > len.
+    // Their cumulative lengths (mse_index: virtual index -> point) as well.
     int panic = 0;
+    int64_t* cum = w.ig_cum + (size_t)s * (w.ig_cap + 2);
+    int64_t run = 0;
+    cum[0] = 0;
     for (int r = 0; r <= nig; ++r) {
         const int64_t lo = r == 0 ? bi0 : pairs[2 * (r - 1) + 1];
         const int64_t hi = r == nig ? bi1 : pairs[2 * r];
         if (lo > hi || hi > (int64_t)a.N) panic = 1;
+        run += hi - lo;
+        cum[r + 1] = run;
     }
     w.mse_panic[s] = panic;
     // the axis is monotone (Spectrum invariant): its end points bound every x
@@ -1389,9 +1395,30 @@ __global__ void k_flags(BatchArgs a, Workspace w) {
 // the block scan preserves center order.
 // ----------------------------------------------------------------------------------
 __device__ __forceinline__ bool in_ignore(int v, const int64_t* pairs, int n) {
-    for (int k = 0; k < n; ++k)
-        if (v >= pairs[2 * k] && v < pairs[2 * k + 1]) return true;
-    return false;
+    if (n <= 8) {
+        for (int k = 0; k < n; ++k)
+            if (v >= pairs[2 * k] && v < pairs[2 * k + 1]) return true;
+        return false;
+    }
+    // Many regions: the merged regions are sorted and disjoint in ppm, so both ends
+    // of their index pairs are monotone in the same direction (ascending, or
+    // descending for a descending axis; floor/ceil, the clamps and the filter keep
+    // that). In ascending order the last pair starting at or before v has the
+    // largest end of all such pairs, so v is ignored iff it lies before that end.
+    const bool desc = pairs[0] > pairs[2 * (n - 1)] ||
+                      (pairs[0] == pairs[2 * (n - 1)] && pairs[1] > pairs[2 * (n - 1) + 1]);
+    int lo = 0, hi = n - 1, k = -1;
+    while (lo <= hi) {
+        const int mid = (lo + hi) >> 1;
+        const int q = desc ? n - 1 - mid : mid;
+        if (pairs[2 * q] <= v) {
+            k = q;
+            lo = mid + 1;
+        } else {
+            hi = mid - 1;
+        }
+    }
+    return k >= 0 && v < pairs[2 * k + 1];
 }
 
 // The peaks of one mask word (64 points), in centre order: borders by bit scans,
@@ -1404,7 +1431,7 @@ __device__ __forceinline__ int word_peaks(const BatchArgs& a, const Workspace& w
     const uint64_t* mc = w.masks + (size_t)s * 3 * W;
     const uint64_t* mr = mc + W;
     const uint64_t* ml = mc + 2 * W;
-    const int64_t* pairs = w.ig + (size_t)s * 2 * kMaxIgnore;
+    const int64_t* pairs = w.ig + (size_t)s * 2 * w.ig_cap;
     const int nig = w.n_ig[s];
     const int64_t sbi0 = w.sbi[2 * s], sbi1 = w.sbi[2 * s + 1];
     // the word and its neighbours' border masks in one round trip; a border farther
@@ -3236,9 +3263,40 @@ __device__ __forceinline__ void retain_body(const BatchArgs& a, const Workspace&
 // ----------------------------------------------------------------------------------
 __device__ __forceinline__ void mse_region(const Workspace& w, int s, int r, int nig, int64_t* lo,
                                            int64_t* hi) {
-    const int64_t* pairs = w.ig + (size_t)s * 2 * kMaxIgnore;
+    const int64_t* pairs = w.ig + (size_t)s * 2 * w.ig_cap;
     *lo = r == 0 ? w.sbi[2 * s] : pairs[2 * (r - 1) + 1];
     *hi = r == nig ? w.sbi[2 * s + 1] : pairs[2 * r];
+}
+
+// Point of virtual index v (0 <= v < mse_len) of the concatenated MSE regions:
+// the first region whose cumulative end exceeds v (empty regions are skipped).
+// A walk for a few regions, a binary search over prep's cumulative lengths for many.
+__device__ __forceinline__ int64_t mse_index(const Workspace& w, int s, int nig, int64_t v) {
+    if (nig <= 8) {
+        int64_t rem = v;
+        for (int r = 0; r <= nig; ++r) {
+            int64_t lo, hi;
+            mse_region(w, s, r, nig, &lo, &hi);
+            if (rem < hi - lo) return lo + rem;
+            rem -= hi - lo;
+        }
+        return 0;
+    }
+    const int64_t* cum = w.ig_cum + (size_t)s * (w.ig_cap + 2);
+    int lo = 0, hi = nig;  // the largest r with cum[r] <= v
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (cum[mid] <= v) lo = mid;
+        else hi = mid - 1;
+    }
+    int64_t rlo, rhi;
+    mse_region(w, s, lo, nig, &rlo, &rhi);
+    return rlo + (v - cum[lo]);
+}
+
+// points in the MSE regions of spectrum s (their total length)
+__device__ __forceinline__ int64_t mse_len(const Workspace& w, int s) {
+    return w.ig_cum[(size_t)s * (w.ig_cap + 2) + w.n_ig[s] + 1];  // prep_spectrum
 }
 
 template <int BS>
@@ -3254,25 +3312,11 @@ __global__ __launch_bounds__(BS) void k_mse_partial(BatchArgs a, Workspace w, in
     const double* x = a.x + (size_t)s * a.x_stride;
     const double* y = a.y + (size_t)s * a.y_stride;
     const int nig = w.n_ig[s];
-    int64_t total = 0;
-    for (int r = 0; r <= nig; ++r) {
-        int64_t lo, hi;
-        mse_region(w, s, r, nig, &lo, &hi);
-        total += hi - lo;
-    }
+    const int64_t total = mse_len(w, s);
     const bool fast = w.x_ok[s] && w.unsafe_kept[s] == 0;
     double acc = 0.0;
     for (int64_t v = (int64_t)part * BS + threadIdx.x; v < total; v += (int64_t)nparts * BS) {
-        int64_t rem = v, idx = 0;
-        for (int r = 0; r <= nig; ++r) {
-            int64_t lo, hi;
-            mse_region(w, s, r, nig, &lo, &hi);
-            if (rem < hi - lo) {
-                idx = lo + rem;
-                break;
-            }
-            rem -= hi - lo;
-        }
+        const int64_t idx = mse_index(w, s, nig, v);
         const double sup = superpose(x[idx], kept, P, fast);
         const double d = sup - y[idx];
         acc += d * d;
@@ -3293,7 +3337,6 @@ __global__ __launch_bounds__(BS) void k_mse_partial(BatchArgs a, Workspace w, in
 // two points per lane fit every thread block on its own SIMDs (718 waves) with two
 // independent evaluations per term. Same per-point folds, same residual order
 // within a thread (point i before i + 1), then the same shuffle / LDS tree.
-__device__ __forceinline__ int64_t mse_len(const Workspace& w, int s);
 template <int BS>
 __device__ __forceinline__ void mse_publish_fold(const BatchArgs& a, const Workspace& w, int s, int part,
                                                  int nparts, double acc, int kept_n, double* parts);
@@ -3317,12 +3360,7 @@ __global__ __launch_bounds__(BS) void k_mse_partial_n(BatchArgs a, Workspace w, 
     const double* x = a.x + (size_t)s * a.x_stride;
     const double* y = a.y + (size_t)s * a.y_stride;
     const int nig = w.n_ig[s];
-    int64_t total = 0;
-    for (int r = 0; r <= nig; ++r) {
-        int64_t lo, hi;
-        mse_region(w, s, r, nig, &lo, &hi);
-        total += hi - lo;
-    }
+    const int64_t total = mse_len(w, s);
     const bool fast = w.x_ok[s] && w.unsafe_kept[s] == 0;
     double acc = 0.0;
     for (int64_t v0 = (int64_t)part * BS * NPT + threadIdx.x; v0 < total;
@@ -3333,16 +3371,7 @@ __global__ __launch_bounds__(BS) void k_mse_partial_n(BatchArgs a, Workspace w, 
         for (int i = 0; i < NPT; ++i) {
             const int64_t v = v0 + (int64_t)i * BS;
             ok[i] = v < total;
-            int64_t rem = ok[i] ? v : 0, idx = 0;
-            for (int r = 0; r <= nig; ++r) {
-                int64_t lo, hi;
-                mse_region(w, s, r, nig, &lo, &hi);
-                if (rem < hi - lo) {
-                    idx = lo + rem;
-                    break;
-                }
-                rem -= hi - lo;
-            }
+            const int64_t idx = mse_index(w, s, nig, ok[i] ? v : 0);
             xv[i] = x[idx];
             yv[i] = y[idx];
         }
@@ -3490,12 +3519,7 @@ __global__ __launch_bounds__(256) void k_mse_quad(BatchArgs a, Workspace w, int 
     const double* x = a.x + (size_t)s * a.x_stride;
     const double* y = a.y + (size_t)s * a.y_stride;
     const int nig = w.n_ig[s];
-    int64_t total = 0;
-    for (int r = 0; r <= nig; ++r) {
-        int64_t lo, hi;
-        mse_region(w, s, r, nig, &lo, &hi);
-        total += hi - lo;
-    }
+    const int64_t total = mse_len(w, s);
     const bool fast = w.x_ok[s] && w.unsafe_kept[s] == 0;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     // wave wv's Lorentzians: [j0, j1), quad-aligned split
@@ -3509,16 +3533,7 @@ __global__ __launch_bounds__(256) void k_mse_quad(BatchArgs a, Workspace w, int 
         for (int i = 0; i < NPT; ++i) {
             const int64_t v = v0 + lane + 64 * i;
             ok[i] = v < total;
-            int64_t rem = ok[i] ? v : 0, idx = 0;
-            for (int r = 0; r <= nig; ++r) {
-                int64_t lo, hi;
-                mse_region(w, s, r, nig, &lo, &hi);
-                if (rem < hi - lo) {
-                    idx = lo + rem;
-                    break;
-                }
-                rem -= hi - lo;
-            }
+            const int64_t idx = mse_index(w, s, nig, ok[i] ? v : 0);
             xv[i] = x[idx];
             yv[i] = wv == 0 ? y[idx] : 0.0;
         }
@@ -3675,12 +3690,7 @@ __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int
     const double* x = a.x + (size_t)s * a.x_stride;
     const double* y = a.y + (size_t)s * a.y_stride;
     const int nig = w.n_ig[s];
-    int64_t total = 0;
-    for (int r = 0; r <= nig; ++r) {
-        int64_t lo, hi;
-        mse_region(w, s, r, nig, &lo, &hi);
-        total += hi - lo;
-    }
+    const int64_t total = mse_len(w, s);
     // every workgroup counts the retained Lorentzians (the last one reports the
     // capacity status) and checks their fast ranges (k_retain's unsafe_kept)
     int cnt = 0, uns = 0;
@@ -3698,16 +3708,7 @@ __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int
     for (int64_t v0 = (int64_t)part * TP; v0 < total; v0 += (int64_t)nparts * TP) {
         const int64_t v = v0 + tid;
         const bool ok = v < total;
-        int64_t rem = ok ? v : 0, idx = 0;
-        for (int r = 0; r <= nig; ++r) {
-            int64_t lo, hi;
-            mse_region(w, s, r, nig, &lo, &hi);
-            if (rem < hi - lo) {
-                idx = lo + rem;
-                break;
-            }
-            rem -= hi - lo;
-        }
+        const int64_t idx = mse_index(w, s, nig, ok ? v : 0);
         const double xv = x[idx], yv = y[idx];
         double sup;
         if (!fast) {
@@ -3850,16 +3851,6 @@ __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int
 }
 
 // total length of the MSE regions of spectrum s (the divisor of compute_mse)
-__device__ __forceinline__ int64_t mse_len(const Workspace& w, int s) {
-    const int nig = w.n_ig[s];
-    int64_t total = 0;
-    for (int r = 0; r <= nig; ++r) {
-        int64_t lo, hi;
-        mse_region(w, s, r, nig, &lo, &hi);
-        total += hi - lo;
-    }
-    return total;
-}
 
 // One wave per spectrum: the nparts partial sums are folded left to right from +0.0
 // (the order k_mse_partial's tree fixes) with the ordered DPP fold, instead of a
@@ -3908,12 +3899,14 @@ __global__ void k_sq_residuals(const double* __restrict__ sup, const double* __r
     }
 }
 
-__global__ __launch_bounds__(64) void k_exact_fold(const double* __restrict__ t, ExactRegions r,
+__global__ __launch_bounds__(64) void k_exact_fold(const double* __restrict__ t, Workspace w,
                                                    double* __restrict__ out) {
+    const int nig = w.n_ig[0];
     double total = -0.0;
     int64_t len = 0;
-    for (int k = 0; k < r.n; ++k) {
-        const int64_t lo = r.lo[k], hi = r.hi[k];
+    for (int k = 0; k <= nig; ++k) {
+        int64_t lo, hi;
+        mse_region(w, 0, k, nig, &lo, &hi);
         total += dpp_fold(-0.0, t + lo, (int)(hi - lo));
         len += hi - lo;
     }
@@ -4279,10 +4272,10 @@ void launch_mse_final(const BatchArgs& a, const Workspace& w, int nparts, hipStr
     if (mse_kind() != "plain") return;  // k_mse_quad / k_mse_partial_n fold the partials
     launch_k(k_mse_final, dim3(a.B), dim3(64), 0, st, a, w, nparts);
 }
-void launch_mse_exact(const double* sup, const double* y, int64_t n, const ExactRegions& r,
+void launch_mse_exact(const double* sup, const double* y, int64_t n, const Workspace& w,
                       double* scratch, double* out, hipStream_t st) {
     hipLaunchKernelGGL(k_sq_residuals, dim3(cdiv(n, 256)), dim3(256), 0, st, sup, y, n, scratch);
-    hipLaunchKernelGGL(k_exact_fold, dim3(1), dim3(64), 0, st, scratch, r, out);
+    hipLaunchKernelGGL(k_exact_fold, dim3(1), dim3(64), 0, st, scratch, w, out);
 }
 void launch_superposition_vec(const double* x, int64_t n, const double* params, int P,
                               double* out, int* flag, hipStream_t st) {

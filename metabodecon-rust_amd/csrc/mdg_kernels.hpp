@@ -67,7 +67,9 @@ struct Workspace {
     double* mse_part;         // B x nparts
     double* sfr_stats;        // B x {mean, sd}
     int64_t* sbi;             // B x 2
-    int64_t* ig;              // B x 2*kMaxIgnore
+    int64_t* ig;              // B x 2*ig_cap: ignore-region index pairs
+    int64_t* ig_cum;          // B x (ig_cap + 2): cumulative lengths of the MSE regions
+    int ig_cap;               // pairs per spectrum the rows hold (>= the call's n_ignore)
     int32_t* n_ig;
     int32_t* mse_panic;
     int32_t* status;
@@ -96,13 +98,9 @@ int64_t chain_stride_for(int N, int ws);
 size_t chain_bytes(int B, int N, int ws, int passes);
 bool chain_supported(int B, int N, int iters, int ws);
 
-// MSE regions (start, end) of one spectrum for the exact MSE
-struct ExactRegions {
-    int n;
-    int64_t lo[kMaxIgnore + 1];
-    int64_t hi[kMaxIgnore + 1];
-};
-void launch_mse_exact(const double* sup, const double* y, int64_t n, const ExactRegions& r,
+// exact-order MSE of spectrum 0 of the last pipeline run over its MSE regions
+// (read on the device from the workspace: signal boundaries and ignore pairs)
+void launch_mse_exact(const double* sup, const double* y, int64_t n, const Workspace& w,
                       double* scratch, double* out, hipStream_t st);
 
 // Every pipeline kernel takes (BatchArgs, Workspace, ...) by value and is launched

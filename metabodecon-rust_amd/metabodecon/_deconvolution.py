@@ -311,11 +311,6 @@ def _lane_pool(n: int):
 
 
 class Deconvoluter:
-    # merged ignore regions the engine takes per call (kMaxIgnore, mdg_common.hpp);
-    # the reference has no limit -- add_ignore_region refuses the 65th disjoint
-    # region with InvalidIgnoreRegion instead of failing later at deconvolute time
-    MAX_IGNORE = 64
-
     def __init__(self):
         self._s = nat.default_settings()
         self._ignore: list[tuple[float, float]] | None = None
@@ -374,10 +369,6 @@ class Deconvoluter:
         if st:
             raise exc.InvalidIgnoreRegion(
                 f"ignore region boundaries [{a}, {b}] are invalid")
-        if n.value > self.MAX_IGNORE:
-            raise exc.InvalidIgnoreRegion(
-                f"ignore region [{a}, {b}] would make {n.value} disjoint regions; the GPU "
-                f"engine takes at most {self.MAX_IGNORE}")
         self._ignore = [(float(buf[2 * i]), float(buf[2 * i + 1])) for i in range(n.value)]
 
     def clear_ignore_regions(self) -> None:
@@ -400,8 +391,6 @@ class Deconvoluter:
     def _ignore_array(self) -> np.ndarray:
         if not self._ignore:
             return np.zeros(0)
-        if len(self._ignore) > self.MAX_IGNORE:
-            raise exc.UnexpectedError(f"more than {self.MAX_IGNORE} ignore regions")
         return np.array(self._ignore, dtype=np.float64).reshape(-1)
 
     # Spectra of one call deconvoluted concurrently, one per engine context (own

@@ -199,20 +199,17 @@ def test_division_hard_cases_lie_next_to_rounding_midpoints():
     assert valid > 1000
 
 
-def test_ignore_region_engine_limit_is_reported_at_add_time():
-    """The engine takes up to Deconvoluter.MAX_IGNORE (64) merged regions per call;
-    the next disjoint region is refused by add_ignore_region itself with the
-    reference's InvalidIgnoreRegion kind, leaving the list unchanged."""
+def test_ignore_regions_have_no_engine_limit():
+    """The reference's add_ignore_region accepts any number of disjoint regions
+    (deconvoluter.rs:438-472); so does this one (the engine sizes its per-spectrum
+    region rows per call), merging exactly like the oracle."""
     d = Deconvoluter()
-    for k in range(Deconvoluter.MAX_IGNORE):
-        d.add_ignore_region((0.1 * k, 0.1 * k + 0.05))
-    assert len(d.ignore_regions) == Deconvoluter.MAX_IGNORE
-    before = d.ignore_regions
-    with pytest.raises(exceptions.InvalidIgnoreRegion):
-        d.add_ignore_region((100.0, 100.5))
-    assert d.ignore_regions == before
-    d.add_ignore_region((0.0, 0.12))  # merges with existing ones: still accepted
-    assert len(d.ignore_regions) == Deconvoluter.MAX_IGNORE - 1
+    for k in range(300):
+        d.add_ignore_region((0.01 * k, 0.01 * k + 0.005))
+    assert len(d.ignore_regions) == 300
+    d.add_ignore_region((0.0, 0.012))  # merges the first two
+    assert len(d.ignore_regions) == 299
+    assert d.ignore_regions[0] == (0.0, 0.015)
 
 
 @pytest.mark.parametrize("visible,local_rank,want", [(1, "1", 0), (1, "3", 0), (8, "3", 3),
