@@ -59,6 +59,7 @@ HBM_PEAK_GBS = 8000.0     # MI355X HBM3E, MI355X_MICROARCH.md (spec)
 FLOPS_PER_EVAL = 5        # sub, mul, add, div, accumulate (div counted once)
 CLOCK_GHZ = 2.35          # shader clock measured by tools/ubench/eval_cost.hip (cycles / wall ns)
 CHAIN_FLOOR_CYC = 8.34    # two dependent v_fmac_f64 per smoother tick, one wave (eval_cost.hip)
+FIT_ISSUE_CEILING = 1024 * CLOCK_GHZ * 1e9 * 64 / 60  # exact evaluations/s
 WORK_STAGES = ["fit_superposition", "mse_superposition", "smooth", "detect"]
 SB = (11.8, -2.2)         # signal boundaries of the synthetic configs (ppm, Spectrum order)
 BLOOD = os.path.join(ROOT, "tests", "golden", "bruker", "blood")
@@ -71,12 +72,25 @@ def parse():
     ap.add_argument("--steps", type=int, default=24,
                     help="rounds of the stream (--streams spectra each)")
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=1, help="spectra per step (headline)")
+    ap.add_argument("--mode", choices=["queue", "stream"], default="queue",
+                    help="queue: single-spectrum submissions to an mdg_queue (batched into "
+                         "pipelines of --max-batch on --lanes contexts); stream: the round-2 form, "
+                         "one B=--batch pipeline per call on --streams contexts")
+    ap.add_argument("--max-batch", type=int, default=128, help="queue: spectra per pipeline")
+    ap.add_argument("--lanes", type=int, default=2, help="queue: engine contexts (own streams)")
+    ap.add_argument("--step-spectra", type=int, default=0,
+                    help="queue: spectra per step (0 = max_batch * lanes)")
+    ap.add_argument("--verify", type=int, default=2,
+                    help="queue: spectra per launched batch checked against the oracle after "
+                         "timing (0 = none)")
+    ap.add_argument("--batch", type=int, default=1, help="stream mode: spectra per call")
     ap.add_argument("--streams", type=int, default=18,
-                    help="engine contexts the steps are spread over (1 = back to back)")
-    ap.add_argument("--hw-queues", type=int, default=32,
+                    help="stream mode: engine contexts the calls are spread over")
+    ap.add_argument("--hw-queues", type=int, default=0,
                     help="GPU_MAX_HW_QUEUES for this process (HIP maps streams onto that "
-                         "many hardware queues round-robin; <= 32)")
+                         "many hardware queues round-robin; <= 32). 0: queue mode leaves the "
+                         "environment as it is (HIP's default is 4; the queue needs one per "
+                         "lane), stream mode sets 32")
     ap.add_argument("--n", type=int, default=131072)
     ap.add_argument("--peaks", type=int, default=2048)
     ap.add_argument("--hw-scale", type=float, default=1.0, help="half-width scale (configs[3]: 2)")
@@ -289,13 +303,14 @@ def run_batch(nat, slot, B, n, x, y, sb, settings, cap, x_stride=0, rec=None):
 def profiled_pass(nat, torch, slot, fn, steps):
     """`steps` calls of fn() with hipEvents around every stage launch (the engine
     runs un-graphed while timing) -> stage -> (ms, launches)."""
-    slot.ctx.reset_stage_times()
-    slot.ctx.set_profiling(True)
+    ctx = getattr(slot, "ctx", slot)  # a Slot or an engine Context
+    ctx.reset_stage_times()
+    ctx.set_profiling(True)
     for _ in range(steps):
         fn()
     torch.cuda.synchronize()
-    st = slot.ctx.stage_times()
-    slot.ctx.set_profiling(False)
+    st = ctx.stage_times()
+    ctx.set_profiling(False)
     return st
 
 
@@ -404,6 +419,194 @@ def headline(args, nat, torch, dist, dev, rank, world):
     for s in slots:
         s.ctx.close()
     return out
+
+
+def oracle_check(x_host, Yh, sb, res_status, res_cnt, res_out, res_mse, threads, cap):
+    """The checker (test infrastructure, after the timed region): the oracle on the
+    host for the sampled spectra; parameters and counts bit-identical, statuses equal,
+    MSE within 1e-12 relative (tests/test_gpu_parity.py's bar). Returns (ok, total,
+    first mismatch or None)."""
+    import oracle
+    st, cnt, out, mse = oracle.deconvolute_batch(x_host, Yh, np.array([sb] * Yh.shape[0]),
+                                                 threads=threads, cap=cap)
+    ok, bad = 0, None
+    for i in range(Yh.shape[0]):
+        k = int(cnt[i])
+        good = (int(res_status[i]) == int(st[i]) and int(res_cnt[i]) == k and
+                np.array_equal(res_out[i][:min(k, cap)], out[i][:min(k, cap)]) and
+                abs(float(res_mse[i]) - float(mse[i])) <= 1e-12 * abs(float(mse[i])))
+        ok += good
+        if not good and bad is None:
+            bad = {"sample": i, "status": (int(res_status[i]), int(st[i])),
+                   "count": (int(res_cnt[i]), k)}
+    return ok, Yh.shape[0], bad
+
+
+def pipeline_work(P_sel, kept, L, iters):
+    """Algorithmic FP64 flops of one spectrum's pipeline: the fit's
+    3*P_sel^2 Lorentzian evaluations per iteration and the MSE's L*P_kept, 5 flops
+    each, plus 3L for the residuals (the smoother's and detection's adds are
+    negligible beside them: 6N and ~10N)."""
+    return FLOPS_PER_EVAL * (3 * P_sel * P_sel * iters + L * kept) + 3 * L
+
+
+def headline_queue(args, nat, torch, dist, dev, rank, world):
+    """configs[1] through the spectrum queue (mdg_queue, include/mdgpu.h): each step
+    submits S distinct device-resident spectra ONE AT A TIME (S = --step-spectra,
+    default max_batch * lanes), each with its own result row; the queue gathers them
+    into pipelines of --max-batch spectra on --lanes engine contexts. The timed region
+    ends when every submitted spectrum's results are written (mdg_queue_synchronize)."""
+    n, cap, K, W = args.n, args.cap, args.steps, args.warmup
+    S = args.step_spectra or args.max_batch * args.lanes
+    KS, WS = K * S, W * S
+    dist_on = world > 1 or args.force_dist
+    settings = nat.default_settings()
+    if args.fit_iterations:
+        settings.fit_iterations = args.fit_iterations
+    q = nat.SpectrumQueue(dev.index, n, args.max_batch, args.lanes, settings)
+    gen = nat.Context(dev.index)
+    R = max(KS, WS, 1)  # distinct spectra, seeds rank*R ...
+    x, Y = synth_device(nat, gen, torch, R, n, args.peaks, rank * R, dev, args.hw_scale)
+    out = torch.zeros((KS, cap, 3), dtype=torch.float64, device=dev)
+    cnt = torch.zeros(KS, dtype=torch.int32, device=dev)
+    mse = torch.zeros(KS, dtype=torch.float64, device=dev)
+    status = torch.full((KS,), -1, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    xp, yp, op = x.data_ptr(), Y.data_ptr(), out.data_ptr()
+    cp, mp, sp = cnt.data_ptr(), mse.data_ptr(), status.data_ptr()
+    row_y, row_o = n * 8, cap * 24
+    submit = nat.lib().mdg_queue_submit
+    qh = q.handle
+
+    def submit_all(count, seed_off):
+        for k in range(count):
+            j = (k + seed_off) % R
+            r = k % KS
+            rc = submit(qh, xp, yp + j * row_y, SB[0], SB[1], op + r * row_o, cap,
+                        cp + 4 * r, mp + 8 * r, sp + 4 * r)
+            if rc:
+                raise RuntimeError(nat.strerror(rc))
+
+    submit_all(max(WS, args.max_batch * args.lanes), 0)  # warm-up: every lane sizes its rows
+    q.synchronize()
+    torch.cuda.synchronize()
+    if dist_on:  # RCCL connections are set up by the first collectives, not in the timing
+        g_rec = torch.empty((world * KS,), dtype=torch.float64, device=dev)
+        dist.all_gather_into_tensor(g_rec, mse)
+        g_out = torch.empty((world * KS, cap, 3), dtype=torch.float64, device=dev)
+        dist.all_gather_into_tensor(g_out, out)
+        torch.cuda.synchronize()
+    status.fill_(-1)
+    torch.cuda.synchronize()
+    # latency of one spectrum alone (B = 1 pipeline, idle GPU) and of one batch alone
+    lat, blat = [], []
+    ctx1 = nat.Context(dev.index)
+    sb1 = torch.tensor([SB], dtype=torch.float64, device=dev)
+    o1 = torch.zeros((1, cap, 3), dtype=torch.float64, device=dev)
+    i1 = torch.zeros(2, dtype=torch.int32, device=dev)
+    m1 = torch.zeros(1, dtype=torch.float64, device=dev)
+    for k in range(6):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        rc = nat.lib().mdg_deconvolute_batch_device(
+            ctx1.handle, 1, n, xp, 0, yp + (k % R) * row_y, n, sb1.data_ptr(),
+            ctypes.byref(settings), None, 0, o1.data_ptr(), cap, i1.data_ptr(), m1.data_ptr(),
+            i1.data_ptr() + 4)
+        ctx1.synchronize()
+        lat.append(time.perf_counter() - t)
+        assert rc == 0
+    ctx1.close()
+    for k in range(3):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        submit_all(args.max_batch, k * args.max_batch)
+        q.synchronize()
+        blat.append(time.perf_counter() - t)
+    status.fill_(-1)
+    torch.cuda.synchronize()
+    st0 = q.stats()
+    # timed region
+    if dist_on:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    submit_all(KS, 0)
+    submit_s = time.perf_counter() - t0  # host time to submit the KS spectra
+    q.synchronize()
+    torch.cuda.synchronize()
+    if dist_on:  # RCCL gather of every rank's results (the weak-scaling exchange)
+        dist.all_gather_into_tensor(g_rec, mse)
+        dist.all_gather_into_tensor(g_out, out)
+        torch.cuda.synchronize()
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist_on:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    st1 = q.stats()
+    batches = st1["batches"] - st0["batches"]
+    assert st1["spectra"] - st0["spectra"] == KS, (st0, st1)
+    status_h = status.cpu().numpy()
+    assert int(np.abs(status_h).max()) == 0, np.unique(status_h)
+    cnt_h = cnt.cpu().numpy()
+    # parity of the timed results: args.verify spectra of every batch the timed region
+    # launched (its first and last submission, ...) against the oracle, on the host
+    verified = None
+    if args.verify and rank == 0:
+        picks = sorted({min(KS - 1, b * args.max_batch + o) for b in range(batches)
+                        for o in np.linspace(0, args.max_batch - 1, args.verify).astype(int)})
+        Yh = Y[[p % R for p in picks]].cpu().numpy()
+        threads, _, _ = host_threads(args)
+        t = time.perf_counter()
+        ok, tot, bad = oracle_check(x.cpu().numpy(), Yh, SB, status_h[picks], cnt_h[picks],
+                                    out[picks].cpu().numpy(), mse[picks].cpu().numpy(), threads,
+                                    cap)
+        verified = {"ok": ok, "checked": tot, "verified": f"{ok}/{tot}",
+                    "sample": (f"{args.verify} submissions of each of the {batches} batches the "
+                               "timed region launched (first ... last), whole result rows against "
+                               "the oracle: status, count and parameters bit-identical, MSE "
+                               "within 1e-12 relative"),
+                    "first_mismatch": bad, "check_s": time.perf_counter() - t}
+    # profiled pass (stage times, roofline): one batch of max_batch spectra on lane 0,
+    # un-graphed, hipEvents around every stage on that lane's stream
+    lane = q.lane(0)
+    B = args.max_batch
+    sbB = torch.tensor([SB] * B, dtype=torch.float64, device=dev)
+    oB = torch.zeros((B, cap, 3), dtype=torch.float64, device=dev)
+    iB = torch.zeros(2 * B, dtype=torch.int32, device=dev)
+    mB = torch.zeros(B, dtype=torch.float64, device=dev)
+    torch.cuda.synchronize()
+
+    def prof_step():
+        rc = nat.lib().mdg_deconvolute_batch_device(
+            lane.handle, B, n, xp, 0, yp, n, sbB.data_ptr(), ctypes.byref(settings), None, 0,
+            oB.data_ptr(), cap, iB.data_ptr(), mB.data_ptr(), iB.data_ptr() + 4 * B)
+        assert rc == 0, nat.strerror(rc)
+
+    prof = {}
+    if not args.no_profile:
+        prof = profiled_pass(nat, torch, lane, prof_step, 2)
+    lane.synchronize()
+    counts = iB[:B].cpu().numpy()
+    work, P_sel = work_per_launch(nat, lane, B, n, counts, settings, 14.8,
+                                  14.8 - 20.0 / (n - 1.0), SB)
+    roof = roofline_from_stages(lane, prof, work, f"b{B}", n) if prof else None
+    L = sbi_len(14.8, -20.0 / (n - 1.0), SB[0], SB[1])
+    iters = settings.fit_iterations
+    flops = float(np.mean([pipeline_work(p, int(k), L, iters) for p, k in zip(P_sel, counts)]))
+    res = {
+        "elapsed": elapsed, "spectra": world * KS, "latency_ms": 1e3 * statistics.median(lat),
+        "batch_latency_ms": 1e3 * statistics.median(blat),
+        "host_submit_us_per_spectrum": 1e6 * submit_s / KS, "batches": batches,
+        "roofline": roof, "pipeline_flops_per_spectrum": flops,
+        "stages_ms_per_spectrum": {k: v[0] / 2 / B for k, v in prof.items() if v[1]},
+        "selected_peaks": P_sel[:4], "kept_peaks": [int(c) for c in cnt_h[:4]],
+        "verified": verified, "step_spectra": S,
+    }
+    q.close()
+    gen.close()
+    return res
 
 
 def batch_config(args, nat, torch, dev, B, n, peaks, steps, warmup, tag, hw_scale=1.0):
@@ -586,7 +789,8 @@ def main():
     # before anything initialises HIP (torch is imported below, and ranks inherit
     # the environment): one hardware queue per busy stream, or two streams that
     # share a queue serialise
-    os.environ["GPU_MAX_HW_QUEUES"] = str(max(1, min(32, args.hw_queues)))
+    if args.hw_queues or args.mode == "stream":
+        os.environ["GPU_MAX_HW_QUEUES"] = str(max(1, min(32, args.hw_queues or 32)))
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -612,7 +816,76 @@ def main():
         with torch.cuda.stream(st):
             torch.ones(1, device=dev).add_(1)  # the stream's hardware queue now exists
     torch.cuda.synchronize()
-    h = headline(args, nat, torch, dist, dev, rank, world)
+    if args.mode == "queue":
+        h = headline_queue(args, nat, torch, dist, dev, rank, world)
+        line = queue_line(args, h, world, nat)
+    else:
+        h = headline(args, nat, torch, dist, dev, rank, world)
+        line = stream_line(args, h, world, nat)
+    value = line["value"]
+    finish(args, line, value, nat, torch, dist, dev, rank, world, local)
+
+
+def queue_line(args, h, world, nat):
+    value = h["spectra"] / h["elapsed"]
+    S = h["step_spectra"]
+    roof = h["roofline"]
+    pipe = {"bound": "fp64 VALU issue", "achieved": h["pipeline_flops_per_spectrum"] * value / 1e12,
+            "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "flops_per_spectrum": h["pipeline_flops_per_spectrum"],
+            "source": ("algorithmic FP64 of the whole pipeline per spectrum (5 flops per "
+                       "Lorentzian evaluation: fit 3 P_sel^2 x iterations, MSE L x P_kept; + 3L) "
+                       "x value")}
+    pipe["frac"] = pipe["achieved"] / pipe["peak"]
+    if roof and roof.get("stage") == "fit_superposition":
+        evals = roof["algorithmic_per_launch"] / FLOPS_PER_EVAL / (roof["avg_launch_ms"] / 1e3)
+        roof["issue_roofline"] = {
+            "unit": "Lorentzian evaluations/s", "achieved": evals, "ceiling": FIT_ISSUE_CEILING,
+            "frac": evals / FIT_ISSUE_CEILING,
+            "source": ("12 FP64 VALU instructions per exact evaluation (one quarter-rate "
+                       "v_rcp_f64): ~60 issue cycles per wave-evaluation, 1024 SIMDs x 2.35 GHz "
+                       "x 64 / 60 (tools/ubench/eval_cost.hip, DESIGN.md §5)")}
+    return {
+        "metric": "spectra/s (128k pts, ~2k peaks)",
+        "value": value,
+        "unit": "spectra/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": h["elapsed"] / args.steps * 1e3,
+        "latency_ms": h["latency_ms"],
+        "batch_latency_ms": h["batch_latency_ms"],
+        # Little's law: spectra in flight (one batch per lane) / throughput
+        "latency_in_queue_ms": args.max_batch * args.lanes / value * 1e3,
+        "host_submit_us_per_spectrum": h["host_submit_us_per_spectrum"],
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (device-generated, distinct seeds per spectrum and rank)",
+        "config": {"workload": ("configs[1]: synthetic 131072-pt f64 spectra, 2048 injected "
+                                "Lorentzians, default Deconvoluter; each spectrum submitted on its "
+                                "own (mdg_queue_submit, device arrays, own result row); the queue "
+                                f"runs them in pipelines of {args.max_batch} on {args.lanes} "
+                                f"engine contexts; a step is {S} submissions"),
+                   "n_points": args.n, "injected_peaks": args.peaks,
+                   "spectra_per_gpu_per_step": S, "max_batch": args.max_batch,
+                   "lanes": args.lanes, "batches_timed": h["batches"],
+                   "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "unset (HIP default 4)"),
+                   "selected_peaks": h["selected_peaks"], "kept_peaks": h["kept_peaks"],
+                   "parallelism": f"dp{world}" if world > 1 else "single"},
+        "verified": h["verified"],
+        "roofline": roof,
+        "roofline_pipeline": pipe,
+        "stages_ms_per_spectrum": h["stages_ms_per_spectrum"],
+        "stages_source": (f"separate profiled pass: one batch of {args.max_batch} on lane 0 "
+                          "(hipEvents around every stage), per spectrum"),
+        "cpu_baseline": None,
+        "build": {k: v for k, v in nat.build_info().items() if k != "compiler"},
+    }
+
+
+def stream_line(args, h, world, nat):
     value = h["spectra"] / h["elapsed"]
     B = args.batch
     line = {
@@ -649,6 +922,10 @@ def main():
         "cpu_baseline": None,
         "build": {k: v for k, v in nat.build_info().items() if k != "compiler"},
     }
+    return line
+
+
+def finish(args, line, value, nat, torch, dist, dev, rank, world, local):
     if rank == 0 and world == 1:
         torch.cuda.synchronize()
         want = set() if args.no_configs else {int(c) for c in args.configs.split(",") if c}

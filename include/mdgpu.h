@@ -88,7 +88,8 @@ typedef struct mdg_ctx mdg_ctx;
 
 /* ---- host-only helpers (no GPU needed) ---------------------------------- */
 int mdg_abi_version(void);
-/* Build provenance, "src=<sha256/16 of the engine sources> compiler=<hipcc clang>"
+/* Build provenance, "src=<sha256/16 of the engine sources> flags=<sha256/16 of the
+ * compile flags> compiler=<hipcc clang>"
  * (no reference counterpart: lets a caller check the library matches its sources). */
 const char* mdg_build_info(void);
 const char* mdg_strerror(int status);
@@ -230,6 +231,37 @@ int mdg_synth_batch_device(mdg_ctx* ctx, size_t b, size_t n, double xmax, double
 int mdg_synth_batch_device_hw(mdg_ctx* ctx, size_t b, size_t n, double xmax, double width,
                               uint64_t seed0, size_t n_peaks, double lo, double hi, double hw_scale,
                               double sigma, double* d_x, double* d_y);
+
+/* ---- spectrum queue (serving form of many concurrent calls) ----------------
+ * Replaces Deconvoluter::par_deconvolute_spectrum called by many concurrent
+ * callers (Deconvoluter is Send + Sync, deconvoluter.rs:913-917) and
+ * par_deconvolute_spectra over an open-ended stream of spectra (:700-710).
+ * A queue owns `lanes` engine contexts on `device` (own HIP stream and workspace
+ * each; lanes <= 16) and deconvolutes spectra of n points with the settings and
+ * ignore regions given at creation. Each submission is ONE spectrum with its own
+ * device arrays; the queue gathers submissions into batches of max_batch spectra
+ * (a batch is launched when it is full, or by flush/synchronize) and runs each
+ * batch as one pipeline on the next lane, so consecutive batches overlap. The
+ * results of a submission (count, mse, status as in mdg_deconvolute_batch_device,
+ * min(count, cap) Lorentzians) are bit-identical to a mdg_deconvolute_batch_device
+ * call on that spectrum. Submissions are asynchronous: the input arrays must stay
+ * unchanged, and the outputs are written, until mdg_queue_synchronize returns.
+ * Thread-safe. A failed batch launch makes every later call return its status. */
+typedef struct mdg_queue mdg_queue;
+int mdg_queue_create(int device, size_t n, size_t max_batch, int lanes, const mdg_settings* s,
+                     const double* ignore, size_t n_ignore, mdg_queue** out);
+int mdg_queue_submit(mdg_queue* q, const double* d_x, const double* d_y, double sb0, double sb1,
+                     mdg_lorentzian* d_out, size_t cap, int32_t* d_count, double* d_mse,
+                     int32_t* d_status);
+/* Launch the open (partial) batch. */
+int mdg_queue_flush(mdg_queue* q);
+/* Flush, then wait until every submitted spectrum's outputs are written. */
+int mdg_queue_synchronize(mdg_queue* q);
+/* The engine context of lane `lane` (stage timing, kernel names; owned by the queue). */
+int mdg_queue_lane(mdg_queue* q, int lane, mdg_ctx** ctx);
+/* Batches launched, spectra launched, submissions waiting in the open batch. */
+int mdg_queue_stats(mdg_queue* q, uint64_t* batches, uint64_t* spectra, size_t* open);
+int mdg_queue_destroy(mdg_queue* q);
 
 #ifdef __cplusplus
 }

@@ -1248,3 +1248,186 @@ extern "C" int mdg_optimize_settings(mdg_ctx* c, const double* x, const double* 
     *best_mse = best_exact;
     return MDG_OK;
 }
+
+// ------------------------------------------------------------------------------
+// Spectrum queue: the serving form of many concurrent deconvolute_spectrum calls
+// (Deconvoluter is Send + Sync, deconvoluter.rs:913-917; par_deconvolute_spectra
+// over an open-ended stream, :700-710). One submission is one spectrum with its
+// own device arrays. Submissions are gathered into batches of up to max_batch
+// spectra; each batch runs as one pipeline on the next of `lanes` engine contexts
+// (own stream and workspace, round-robin), so a batch's sequential smoother
+// overlaps the fits of the batch before it. Single spectra launched one by one use
+// a B = 1 pipeline whose fit and smoother leave most of the chip idle, and
+// concurrent B = 1 streams run out of hardware queues; a batch
+// shares every launch among its spectra and needs one queue per lane.
+// ------------------------------------------------------------------------------
+struct mdg_queue {
+    struct Lane {
+        mdg_ctx* ctx = nullptr;
+        Buffer x, y, sb, out, cnt, mse, st, table;
+        QueueItem* host_table = nullptr;  // pinned: the upload of a batch's submission table
+        hipEvent_t table_done = nullptr;  // that upload finished (the pinned rows are free)
+        bool table_pending = false;
+    };
+    int device = 0;
+    size_t n = 0;
+    int max_batch = 0;
+    mdg_settings s{};
+    std::vector<double> ignore;
+    std::mutex mu;
+    std::vector<Lane> lanes;
+    int next = 0;
+    std::vector<QueueItem> open;  // the open batch
+    uint64_t batches = 0, spectra = 0;
+    int error = MDG_OK;  // first failure of an asynchronous batch launch (sticky)
+};
+
+namespace {
+
+int queue_launch(mdg_queue* q) {
+    if (q->open.empty()) return MDG_OK;
+    mdg_queue::Lane& L = q->lanes[q->next];
+    q->next = (q->next + 1) % (int)q->lanes.size();
+    const int B = (int)q->open.size();
+    const size_t n = q->n, cap = n / 2 + 2;
+    mdg_ctx* c = L.ctx;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    // the pinned table rows are rewritten only after their previous upload ran
+    if (L.table_pending) HIPCHK(hipEventSynchronize(L.table_done));
+    std::memcpy(L.host_table, q->open.data(), sizeof(QueueItem) * B);
+    HIPCHK(hipMemcpyAsync(L.table.p, L.host_table, sizeof(QueueItem) * B, hipMemcpyHostToDevice, st));
+    HIPCHK(hipEventRecord(L.table_done, st));
+    L.table_pending = true;
+    // one shared axis (the usual case: every spectrum of a set on the same grid) is
+    // read where it lies; otherwise the axes are gathered too
+    const double* x0 = q->open[0].x;
+    bool shared = true;
+    for (const QueueItem& it : q->open) shared = shared && it.x == x0;
+    const QueueItem* items = (const QueueItem*)L.table.p;
+    launch_queue_gather(items, B, (int64_t)n, shared ? 0 : 1, (double*)L.x.p, (double*)L.y.p, (double*)L.sb.p, st);
+    BatchArgs a;
+    int rc = fill_args(c, a, B, n, shared ? x0 : (const double*)L.x.p, shared ? 0 : n, (const double*)L.y.p, n,
+                       (const double*)L.sb.p, q->ignore.empty() ? nullptr : q->ignore.data(), q->ignore.size() / 2,
+                       (double*)L.out.p, cap, (int32_t*)L.cnt.p, (double*)L.mse.p, (int32_t*)L.st.p);
+    if (rc) return rc;
+    if ((rc = run_pipeline(c, a, &q->s))) return rc;
+    launch_queue_scatter(items, B, (const double*)L.out.p, (int64_t)cap, (const int32_t*)L.cnt.p,
+                         (const double*)L.mse.p, (const int32_t*)L.st.p, st);
+    HIPCHK(hipGetLastError());
+    q->open.clear();
+    q->batches += 1;
+    q->spectra += (uint64_t)B;
+    return MDG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mdg_queue_create(int device, size_t n, size_t max_batch, int lanes, const mdg_settings* s,
+                     const double* ignore, size_t n_ignore, mdg_queue** out) {
+    if (!out) return MDG_INVALID_ARGUMENT;
+    *out = nullptr;
+    int v = validate_common(s, n_ignore, ignore);
+    if (v) return v;
+    if (n < 2 || n > (size_t)INT32_MAX / 2 || max_batch == 0 || max_batch > 4096 || lanes < 1 || lanes > 16)
+        return MDG_INVALID_ARGUMENT;
+    mdg_queue* q = new (std::nothrow) mdg_queue();
+    if (!q) return MDG_ERR_OUT_OF_MEMORY;
+    q->device = device;
+    q->n = n;
+    q->max_batch = (int)max_batch;
+    q->s = *s;
+    if (n_ignore) q->ignore.assign(ignore, ignore + 2 * n_ignore);
+    q->open.reserve(max_batch);
+    q->lanes.resize(lanes);
+    const size_t cap = n / 2 + 2;
+    int rc = MDG_OK;
+    for (auto& L : q->lanes) {
+        if ((rc = mdg_ctx_create(device, &L.ctx))) break;
+        if ((rc = ensure(L.y, max_batch * n * 8)) || (rc = ensure(L.x, max_batch * n * 8)) ||
+            (rc = ensure(L.sb, max_batch * 16)) || (rc = ensure(L.out, max_batch * cap * 24)) ||
+            (rc = ensure(L.cnt, max_batch * 4)) || (rc = ensure(L.mse, max_batch * 8)) ||
+            (rc = ensure(L.st, max_batch * 4)) || (rc = ensure(L.table, max_batch * sizeof(QueueItem))))
+            break;
+        if (hipHostMalloc((void**)&L.host_table, max_batch * sizeof(QueueItem), hipHostMallocDefault) != hipSuccess ||
+            hipEventCreateWithFlags(&L.table_done, hipEventDisableTiming) != hipSuccess) {
+            rc = MDG_ERR_HIP;
+            break;
+        }
+    }
+    if (rc) {
+        mdg_queue_destroy(q);
+        return rc;
+    }
+    *out = q;
+    return MDG_OK;
+}
+
+int mdg_queue_submit(mdg_queue* q, const double* d_x, const double* d_y, double sb0, double sb1,
+                     mdg_lorentzian* d_out, size_t cap, int32_t* d_count, double* d_mse, int32_t* d_status) {
+    if (!q || !d_x || !d_y || !d_count || !d_mse || !d_status || (!d_out && cap) || cap > (size_t)INT64_MAX / 24)
+        return MDG_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> g(q->mu);
+    if (q->error) return q->error;
+    q->open.push_back({d_x, d_y, sb0, sb1, (double*)d_out, (int64_t)cap, d_count, d_mse, d_status});
+    if ((int)q->open.size() >= q->max_batch) {
+        const int rc = queue_launch(q);
+        if (rc) q->error = rc;
+        return rc;
+    }
+    return MDG_OK;
+}
+
+int mdg_queue_flush(mdg_queue* q) {
+    if (!q) return MDG_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> g(q->mu);
+    if (q->error) return q->error;
+    const int rc = queue_launch(q);
+    if (rc) q->error = rc;
+    return rc;
+}
+
+int mdg_queue_synchronize(mdg_queue* q) {
+    if (!q) return MDG_INVALID_ARGUMENT;
+    int rc = mdg_queue_flush(q);
+    std::lock_guard<std::mutex> g(q->mu);
+    for (auto& L : q->lanes) {
+        const int r = mdg_ctx_synchronize(L.ctx);
+        if (!rc) rc = r;
+    }
+    return rc;
+}
+
+int mdg_queue_lane(mdg_queue* q, int lane, mdg_ctx** ctx) {
+    if (!q || !ctx || lane < 0 || lane >= (int)q->lanes.size()) return MDG_INVALID_ARGUMENT;
+    *ctx = q->lanes[lane].ctx;
+    return MDG_OK;
+}
+
+int mdg_queue_stats(mdg_queue* q, uint64_t* batches, uint64_t* spectra, size_t* open) {
+    if (!q) return MDG_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> g(q->mu);
+    if (batches) *batches = q->batches;
+    if (spectra) *spectra = q->spectra;
+    if (open) *open = q->open.size();
+    return MDG_OK;
+}
+
+int mdg_queue_destroy(mdg_queue* q) {
+    if (!q) return MDG_OK;
+    for (auto& L : q->lanes) {
+        if (L.ctx) (void)mdg_ctx_synchronize(L.ctx);
+        for (Buffer* b : {&L.x, &L.y, &L.sb, &L.out, &L.cnt, &L.mse, &L.st, &L.table})
+            if (b->p) (void)hipFree(b->p);
+        if (L.host_table) (void)hipHostFree(L.host_table);
+        if (L.table_done) (void)hipEventDestroy(L.table_done);
+        if (L.ctx) (void)mdg_ctx_destroy(L.ctx);
+    }
+    delete q;
+    return MDG_OK;
+}
+
+}  // extern "C"

@@ -4293,6 +4293,64 @@ void launch_synth(double* x, double* y, int64_t n, int B, double xmax, double wi
     hipLaunchKernelGGL(k_synth_y, dim3(g, B), dim3(256), 0, st, x, n, params, P, seed0, sigma, y);
 }
 
+
+// ----------------------------------------------------------------------------------
+// Spectrum queue: gather the submissions' rows, scatter the results (HBM copies)
+// ----------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_queue_gather(const QueueItem* __restrict__ items,
+                                                      int64_t n, int gather_x,
+                                                      double* __restrict__ x_rows,
+                                                      double* __restrict__ y_rows,
+                                                      double* __restrict__ sb) {
+    const int s = blockIdx.y;
+    const QueueItem it = items[s];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        sb[2 * s] = it.sb0;
+        sb[2 * s + 1] = it.sb1;
+    }
+    double* yr = y_rows + (size_t)s * n;
+    double* xr = x_rows + (size_t)s * n;
+    // consecutive threads copy consecutive points: every load and store coalesces
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        yr[i] = it.y[i];
+        if (gather_x) xr[i] = it.x[i];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_queue_scatter(const QueueItem* __restrict__ items,
+                                                       const double* __restrict__ out,
+                                                       int64_t stage_cap,
+                                                       const int32_t* __restrict__ counts,
+                                                       const double* __restrict__ mse,
+                                                       const int32_t* __restrict__ status) {
+    const int s = blockIdx.x;
+    const QueueItem it = items[s];
+    const int32_t cnt = counts[s];
+    const int64_t rows = cnt < 0 ? 0 : (cnt < it.cap ? cnt : it.cap);
+    if (threadIdx.x == 0) {
+        *it.count = cnt;
+        *it.mse = mse[s];
+        const int32_t st = status[s];
+        *it.status = (st == MDG_OK && cnt > it.cap) ? MDG_CAPACITY : st;
+    }
+    const double* src = out + 3 * (size_t)s * stage_cap;
+    for (int64_t i = threadIdx.x; i < 3 * rows; i += blockDim.x) it.out[i] = src[i];
+}
+
+void launch_queue_gather(const QueueItem* items, int B, int64_t n, int gather_x, double* x_rows,
+                         double* y_rows, double* sb, hipStream_t st) {
+    const unsigned gx = std::max(1u, std::min(cdiv(n, 1024), 64u));
+    hipLaunchKernelGGL(k_queue_gather, dim3(gx, B), dim3(256), 0, st, items, n, gather_x, x_rows,
+                       y_rows, sb);
+}
+void launch_queue_scatter(const QueueItem* items, int B, const double* out, int64_t stage_cap,
+                          const int32_t* counts, const double* mse, const int32_t* status,
+                          hipStream_t st) {
+    hipLaunchKernelGGL(k_queue_scatter, dim3(B), dim3(256), 0, st, items, out, stage_cap, counts,
+                       mse, status);
+}
+
 }  // namespace mdg
 
 #ifdef MDG_DIAG

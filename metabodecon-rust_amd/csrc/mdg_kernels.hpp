@@ -160,4 +160,27 @@ void launch_superposition_vec(const double* x, int64_t n, const double* params, 
 void launch_synth(double* x, double* y, int64_t n, int B, double xmax, double width,
                   const double* params, int P, uint64_t seed0, double sigma, hipStream_t st);
 
+// Spectrum queue (mdg_queue_*): one submission = one spectrum with its own device
+// arrays. A batch of submissions is gathered into the lane's contiguous rows, runs
+// as one pipeline, and its results are scattered back to each submission's arrays.
+struct QueueItem {
+    const double* x;      // n chemical shifts
+    const double* y;      // n intensities
+    double sb0, sb1;      // signal boundaries (ppm, as the Spectrum stores them)
+    double* out;          // cap Lorentzians {sfhw, hw2, maxp}
+    int64_t cap;
+    int32_t* count;
+    double* mse;
+    int32_t* status;
+};
+// rows y (and x when gather_x) of the B items into y_rows / x_rows (B x n), sb pairs
+void launch_queue_gather(const QueueItem* items, int B, int64_t n, int gather_x, double* x_rows,
+                         double* y_rows, double* sb, hipStream_t st);
+// the pipeline's B results (table rows of stage_cap) to each item's arrays: count,
+// mse, status (MDG_CAPACITY when the item's cap is below the count) and min(count,
+// cap) Lorentzians
+void launch_queue_scatter(const QueueItem* items, int B, const double* out, int64_t stage_cap,
+                          const int32_t* counts, const double* mse, const int32_t* status,
+                          hipStream_t st);
+
 }  // namespace mdg

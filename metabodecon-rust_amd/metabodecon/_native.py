@@ -47,6 +47,8 @@ EXPORTS = [
     "mdg_optimize_settings", "mdg_ordered_sum", "mdg_check_fast_division",
     "mdg_check_division", "mdg_division_hard_case", "mdg_ctx_stage_kernel", "mdg_ctx_get_stream",
     "mdg_synth_lorentzians_hw", "mdg_synth_batch_device_hw",
+    "mdg_queue_create", "mdg_queue_submit", "mdg_queue_flush", "mdg_queue_synchronize",
+    "mdg_queue_lane", "mdg_queue_stats", "mdg_queue_destroy",
 ]
 
 
@@ -246,6 +248,15 @@ def _declare(L):
     L.mdg_synth_batch_device.argtypes = [_vp, _sz, _sz, ctypes.c_double, ctypes.c_double,
                                          ctypes.c_uint64, _sz, ctypes.c_double, ctypes.c_double,
                                          ctypes.c_double, _vp, _vp]
+    L.mdg_queue_create.argtypes = [ctypes.c_int, _sz, _sz, ctypes.c_int, sp, _dp, _sz,
+                                   ctypes.POINTER(_vp)]
+    L.mdg_queue_submit.argtypes = [_vp, _vp, _vp, ctypes.c_double, ctypes.c_double, _vp, _sz, _vp,
+                                   _vp, _vp]
+    L.mdg_queue_flush.argtypes = [_vp]
+    L.mdg_queue_synchronize.argtypes = [_vp]
+    L.mdg_queue_lane.argtypes = [_vp, ctypes.c_int, ctypes.POINTER(_vp)]
+    L.mdg_queue_stats.argtypes = [_vp, _u64p, _u64p, _szp]
+    L.mdg_queue_destroy.argtypes = [_vp]
     L.mdg_synth_batch_device_hw.argtypes = [_vp, _sz, _sz, ctypes.c_double, ctypes.c_double,
                                             ctypes.c_uint64, _sz, ctypes.c_double, ctypes.c_double,
                                             ctypes.c_double, ctypes.c_double, _vp, _vp]
@@ -361,6 +372,82 @@ class Context:
 
     def reset_stage_times(self):
         lib().mdg_ctx_reset_stage_times(self.handle)
+
+
+class _LaneView(Context):
+    """A queue lane's engine context (owned by the queue: never destroyed here)."""
+
+    def __init__(self, handle, device):  # noqa: D107 (no Context.__init__: no new context)
+        self.handle = handle
+        self.device = device
+        self.lock = threading.Lock()
+
+    def close(self):
+        self.handle = None
+
+
+class SpectrumQueue:
+    """mdg_queue: single-spectrum submissions on device arrays, gathered into
+    batches of up to `max_batch` spectra that run one pipeline each on `lanes`
+    engine contexts (include/mdgpu.h). The serving form of many concurrent
+    ``Deconvoluter.par_deconvolute_spectrum`` calls."""
+
+    def __init__(self, device: int, n: int, max_batch: int, lanes: int, settings: Settings,
+                 ignore: np.ndarray | None = None):
+        c = ctypes.c_int(0)
+        lib().mdg_device_count(ctypes.byref(c))
+        if c.value <= 0:
+            raise DeviceUnavailableError("no HIP device visible: the metabodecon GPU engine "
+                                         "needs an MI355X (there is deliberately no CPU fallback)")
+        ign = np.zeros(0) if ignore is None else np.ascontiguousarray(ignore, dtype=np.float64)
+        h = _vp()
+        st = lib().mdg_queue_create(device, n, max_batch, lanes, ctypes.byref(settings),
+                                    ptr(ign) if ign.size else None, ign.size // 2, ctypes.byref(h))
+        if st:
+            raise RuntimeError(f"mdg_queue_create failed: {strerror(st)}")
+        self.handle, self.device, self.n = h, device, n
+        self.max_batch, self.lanes = max_batch, lanes
+
+    def submit(self, x_ptr: int, y_ptr: int, sb, out_ptr: int, cap: int, count_ptr: int,
+               mse_ptr: int, status_ptr: int) -> None:
+        st = lib().mdg_queue_submit(self.handle, x_ptr, y_ptr, float(sb[0]), float(sb[1]), out_ptr,
+                                    cap, count_ptr, mse_ptr, status_ptr)
+        if st:
+            raise RuntimeError(f"mdg_queue_submit: {strerror(st)}")
+
+    def flush(self) -> None:
+        st = lib().mdg_queue_flush(self.handle)
+        if st:
+            raise RuntimeError(f"mdg_queue_flush: {strerror(st)}")
+
+    def synchronize(self) -> None:
+        st = lib().mdg_queue_synchronize(self.handle)
+        if st:
+            raise RuntimeError(f"mdg_queue_synchronize: {strerror(st)}")
+
+    def lane(self, k: int) -> Context:
+        h = _vp()
+        st = lib().mdg_queue_lane(self.handle, k, ctypes.byref(h))
+        if st:
+            raise RuntimeError(strerror(st))
+        return _LaneView(h, self.device)
+
+    def stats(self) -> dict:
+        b, s = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        o = ctypes.c_size_t(0)
+        lib().mdg_queue_stats(self.handle, ctypes.byref(b), ctypes.byref(s), ctypes.byref(o))
+        return {"batches": b.value, "spectra": s.value, "open": o.value}
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib().mdg_queue_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 _ctx: dict[int, Context] = {}

@@ -30,7 +30,16 @@ def many_regions(count, lo=0.6, hi=8.9, width=0.004):
     return regs
 
 
+def engine_settings(st):
+    """The oracle's settings as the engine's ctypes struct (same fields)."""
+    s = nat.Settings()
+    for f, _ in nat.Settings._fields_:
+        setattr(s, f, getattr(st, f))
+    return s
+
+
 def host_run(ctx, x, y, sb, st, regs):
+    st = engine_settings(st)
     ign = np.asarray(regs, dtype=np.float64).reshape(-1)
     n = y.size
     cap = n // 2 + 2

@@ -1,0 +1,149 @@
+"""GPU parity of the spectrum queue (mdg_queue_*, include/mdgpu.h) and of the exact
+configuration bench.py times.
+
+Each submission is one spectrum with its own device arrays; the queue batches them
+into pipelines. Every result must equal the oracle (and the goldens): parameters and
+counts bit-identical, statuses equal, MSE within 1e-12 relative.
+"""
+import argparse
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from tests.conftest import GOLDEN
+from tests.golden.cases import load_case
+
+pytestmark = pytest.mark.gpu
+
+MSE_RTOL = 1e-12
+
+nat = pytest.importorskip("metabodecon._native")
+
+
+def _outputs(torch, k, cap, dev="cuda"):
+    return (torch.zeros((k, cap, 3), dtype=torch.float64, device=dev),
+            torch.zeros(k, dtype=torch.int32, device=dev),
+            torch.zeros(k, dtype=torch.float64, device=dev),
+            torch.full((k,), -1, dtype=torch.int32, device=dev))
+
+
+def test_queue_blood_submissions_match_goldens():
+    """The 16 blood spectra submitted one at a time, twice over (32 submissions),
+    into batches of 5 on 2 lanes: full batches, a partial batch launched by
+    synchronize, each spectrum's own axis row (gathered, not shared)."""
+    torch = pytest.importorskip("torch")
+    names = [f"blood_{i:02d}" for i in range(1, 17)]
+    cases = [load_case(nm) for nm in names]
+    n = cases[0][1].size
+    X = torch.from_numpy(np.stack([c[0] for c in cases])).cuda()
+    Y = torch.from_numpy(np.stack([c[1] for c in cases])).cuda()
+    cap = n // 2 + 2
+    out, cnt, mse, st = _outputs(torch, 32, cap)
+    torch.cuda.synchronize()
+    q = nat.SpectrumQueue(0, n, 5, 2, nat.default_settings())
+    try:
+        for k in range(32):
+            i = k % 16
+            q.submit(X[i].data_ptr(), Y[i].data_ptr(), cases[i][2], out[k].data_ptr(), cap,
+                     cnt[k:].data_ptr(), mse[k:].data_ptr(), st[k:].data_ptr())
+        assert q.stats() == {"batches": 6, "spectra": 30, "open": 2}
+        q.synchronize()
+        assert q.stats() == {"batches": 7, "spectra": 32, "open": 0}
+    finally:
+        q.close()
+    for k in range(32):
+        g = np.load(os.path.join(GOLDEN, "expected", f"{names[k % 16]}.npz"))
+        assert int(st[k]) == 0 and int(cnt[k]) == g["params"].shape[0]
+        assert np.array_equal(out[k, : int(cnt[k])].cpu().numpy(), g["params"]), k
+        assert abs(float(mse[k]) - float(g["mse"])) <= MSE_RTOL * abs(float(g["mse"]))
+
+
+def test_queue_shared_axis_statuses_and_capacity():
+    """A shared axis pointer (read in place), a spectrum that fails (no signal-free
+    peaks: its status, count 0), and a submission whose own capacity is below its
+    count (MDG_CAPACITY, count reported, the first cap rows written) in one batch;
+    the other spectra of that batch are unaffected."""
+    torch = pytest.importorskip("torch")
+    x, y, sb, st_, _ = load_case("blood_03")
+    n = y.size
+    ys = [y, np.zeros(n), y * 0.5, y]
+    sbs = [sb, sb, sb, sb]
+    xd = torch.from_numpy(x).cuda()
+    Yd = torch.from_numpy(np.stack(ys)).cuda()
+    cap = n // 2 + 2
+    out, cnt, mse, st = _outputs(torch, 4, cap)
+    torch.cuda.synchronize()
+    caps = [cap, cap, cap, 7]
+    q = nat.SpectrumQueue(0, n, 8, 1, nat.default_settings())
+    try:
+        for k in range(4):
+            q.submit(xd.data_ptr(), Yd[k].data_ptr(), sbs[k], out[k].data_ptr(), caps[k],
+                     cnt[k:].data_ptr(), mse[k:].data_ptr(), st[k:].data_ptr())
+        q.synchronize()
+    finally:
+        q.close()
+    for k in range(4):
+        o = oracle.deconvolute(x, ys[k], sbs[k], st_)
+        want = o.status if k < 3 else nat.CAPACITY
+        assert int(st[k]) == want, (k, int(st[k]), o.status)
+        if o.status:
+            assert int(cnt[k]) == 0
+            continue
+        assert int(cnt[k]) == o.params.shape[0]
+        rows = min(caps[k], o.params.shape[0])
+        assert np.array_equal(out[k, :rows].cpu().numpy(), o.params[:rows])
+        assert abs(float(mse[k]) - o.mse) <= MSE_RTOL * abs(o.mse)
+
+
+def test_queue_ignore_regions_and_settings():
+    """Settings and ignore regions fixed at queue creation (the Deconvoluter's),
+    on an increasing axis with two regions, and detector-only selection."""
+    torch = pytest.importorskip("torch")
+    names = ["blood_02_two_regions_increasing", "sim_01_detector_only"]
+    for name in names:
+        x, y, sb, st_, ign = load_case(name)
+        n = y.size
+        s = nat.Settings()
+        for f, _ in nat.Settings._fields_:
+            setattr(s, f, getattr(st_, f))
+        xd = torch.from_numpy(x).cuda()
+        yd = torch.from_numpy(np.stack([y, y])).cuda()
+        cap = n // 2 + 2
+        out, cnt, mse, st = _outputs(torch, 2, cap)
+        torch.cuda.synchronize()
+        ig = np.asarray(ign, dtype=np.float64).reshape(-1)
+        q = nat.SpectrumQueue(0, n, 2, 1, s, ig if ig.size else None)
+        try:
+            for k in range(2):
+                q.submit(xd.data_ptr(), yd[k].data_ptr(), sb, out[k].data_ptr(), cap,
+                         cnt[k:].data_ptr(), mse[k:].data_ptr(), st[k:].data_ptr())
+            q.synchronize()
+        finally:
+            q.close()
+        g = np.load(os.path.join(GOLDEN, "expected", f"{name}.npz"))
+        for k in range(2):
+            assert int(st[k]) == int(g["status"])
+            if int(g["status"]) == 0:
+                assert np.array_equal(out[k, : int(cnt[k])].cpu().numpy(), g["params"])
+
+
+def test_bench_headline_configuration_bit_exact():
+    """the exact mode bench.py times -- headline_queue with its
+    default queue (128-spectrum batches on 2 lanes), device-generated distinct
+    configs[1] spectra submitted one at a time -- with EVERY timed result row checked
+    against the oracle (bench's own checker, verify = every submission)."""
+    torch = pytest.importorskip("torch")
+    import bench
+    args = argparse.Namespace(
+        n=131072, peaks=2048, cap=4096, steps=2, warmup=1, max_batch=128, lanes=2,
+        step_spectra=0, verify=128, fit_iterations=0, hw_scale=1.0, force_dist=False,
+        no_profile=True, cpu_threads=0)
+    import torch.distributed as dist
+    dev = torch.device("cuda", 0)
+    h = bench.headline_queue(args, nat, torch, dist, dev, 0, 1)
+    v = h["verified"]
+    assert v["checked"] == 2 * 256 and v["ok"] == v["checked"], v
+    assert h["batches"] == 4
