@@ -491,10 +491,14 @@ def headline_queue(args, nat, torch, dist, dev, rank, world):
     q.synchronize()
     torch.cuda.synchronize()
     if dist_on:  # RCCL connections are set up by the first collectives, not in the timing
-        g_rec = torch.empty((world * KS,), dtype=torch.float64, device=dev)
-        dist.all_gather_into_tensor(g_rec, mse)
-        g_out = torch.empty((world * KS, cap, 3), dtype=torch.float64, device=dev)
-        dist.all_gather_into_tensor(g_out, out)
+        from metabodecon.distributed import gather_tables
+
+        def gather():
+            # the Lorentzian tables trimmed to the largest count of any rank, with the
+            # (status, count, mse) records: distributed.gather_tables, RCCL over xGMI
+            w = max(1, int(cnt.max().item()))
+            return gather_tables(status, cnt, mse, out[:, :w], world * KS)
+        gather()
         torch.cuda.synchronize()
     status.fill_(-1)
     torch.cuda.synchronize()
@@ -534,12 +538,14 @@ def headline_queue(args, nat, torch, dist, dev, rank, world):
     submit_s = time.perf_counter() - t0  # host time to submit the KS spectra
     q.synchronize()
     torch.cuda.synchronize()
+    t_compute = time.perf_counter() - t0
     if dist_on:  # RCCL gather of every rank's results (the weak-scaling exchange)
-        dist.all_gather_into_tensor(g_rec, mse)
-        dist.all_gather_into_tensor(g_out, out)
+        g = gather()
         torch.cuda.synchronize()
         dist.barrier()
+        assert int(g[0].abs().max()) == 0 and g[0].shape[0] == world * KS
     elapsed = time.perf_counter() - t0
+    gather_s = elapsed - t_compute
     if dist_on:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -603,6 +609,7 @@ def headline_queue(args, nat, torch, dist, dev, rank, world):
         "stages_ms_per_spectrum": {k: v[0] / 2 / B for k, v in prof.items() if v[1]},
         "selected_peaks": P_sel[:4], "kept_peaks": [int(c) for c in cnt_h[:4]],
         "verified": verified, "step_spectra": S,
+        "gather_ms": 1e3 * gather_s if dist_on else None,
     }
     q.close()
     gen.close()
@@ -710,6 +717,150 @@ def bruker_set(args, nat, torch, dev):
                              "(PCIe inside the timed region)"}
 
 
+# ------------------------------------------------------------------ multi-rank configs
+C3_N, C3_POINTS, C3_PEAKS, C3_CAP = 4096, 65536, 1024, 2048
+GOLDEN = os.path.join(ROOT, "tests", "golden", "expected")
+
+
+def max_over_ranks(dist, torch, dev, vals):
+    t = torch.tensor(vals, dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(v) for v in t.cpu()]
+
+
+def dist_configs(args, nat, torch, dist, dev, rank, world, threads):
+    """The configs that shard, timed across all ranks (world > 1, or --force-dist):
+    - configs[3]: 4096 synthetic 65536-pt/1024-peak spectra (hw x2) split by
+      distributed.shard_range, each rank's block generated on its own GPU (seeds =
+      global indices, so the spectra are the 1-GPU run's) and run as one
+      device-resident batch; the timed region ends after the RCCL gather of every
+      rank's tables and records (distributed.gather_tables), reported separately;
+    - configs[4]: the 16 blood spectra through distributed.par_deconvolute_spectra
+      (host buffers: the H2D copies and the gather are inside).
+    Results checked after timing: configs[3] the first spectrum of every rank's block
+    against the oracle (rank 0), configs[4] all 16 against the goldens."""
+    import metabodecon as md
+    from metabodecon.distributed import gather_tables, par_deconvolute_spectra, shard_range
+    out = {}
+    settings = nat.default_settings()
+    lo, hi = shard_range(C3_N, rank, world)
+    b = hi - lo
+    ctx = nat.Context(dev.index)
+    x3, y3 = synth_device(nat, ctx, torch, b, C3_POINTS, C3_PEAKS, lo, dev, 2.0)
+    o3 = torch.zeros((b, C3_CAP, 3), dtype=torch.float64, device=dev)
+    c3 = torch.zeros(b, dtype=torch.int32, device=dev)
+    m3 = torch.zeros(b, dtype=torch.float64, device=dev)
+    s3 = torch.full((b,), -1, dtype=torch.int32, device=dev)
+    sb3 = torch.tensor([SB] * b, dtype=torch.float64, device=dev)
+    torch.cuda.synchronize()
+
+    def run():
+        rc = nat.lib().mdg_deconvolute_batch_device(
+            ctx.handle, b, C3_POINTS, x3.data_ptr(), 0, y3.data_ptr(), C3_POINTS, sb3.data_ptr(),
+            ctypes.byref(settings), None, 0, o3.data_ptr(), C3_CAP, c3.data_ptr(), m3.data_ptr(),
+            s3.data_ptr())
+        assert rc == 0, nat.strerror(rc)
+        ctx.synchronize()
+
+    def gather():
+        w = max(1, int(c3.max().item()))
+        g = gather_tables(s3, c3, m3, o3[:, :w], C3_N)
+        torch.cuda.synchronize()
+        return g
+
+    run()
+    gather()
+    comp, tot = [], []
+    for _ in range(3):
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run()
+        t1 = time.perf_counter()
+        g = gather()
+        dist.barrier()
+        t2 = time.perf_counter()
+        a, bt = max_over_ranks(dist, torch, dev, [t1 - t0, t2 - t0])
+        comp.append(a)
+        tot.append(bt)
+    st_all = g[0].cpu().numpy()
+    assert st_all.shape[0] == C3_N and int(np.abs(st_all).max()) == 0
+    r3 = {"value": C3_N / statistics.median(tot), "unit": "spectra/s", "n_ranks": world,
+          "spectra": C3_N, "spectra_per_rank": b, "ms_per_step": 1e3 * statistics.median(tot),
+          "compute_ms": 1e3 * statistics.median(comp),
+          "rccl_gather_ms": 1e3 * (statistics.median(tot) - statistics.median(comp)),
+          "steps": 3, "scaling": "strong",
+          "workload": ("4096 synthetic 65536-pt/1024-peak spectra (hw x2) sharded over the ranks "
+                       "(distributed.shard_range), one device-resident batch per rank, RCCL "
+                       "gather of the Lorentzian tables + records inside the timed region")}
+    if rank == 0 and args.verify:
+        import oracle
+        firsts = [shard_range(C3_N, r, world)[0] for r in range(world)]
+        ys = []
+        for sidx in firsts:
+            xs, ys1 = synth_device(nat, ctx, torch, 1, C3_POINTS, C3_PEAKS, sidx, dev, 2.0)
+            ys.append(ys1[0].cpu().numpy())
+        st, cnt, tab, mse = oracle.deconvolute_batch(xs.cpu().numpy(), np.stack(ys),
+                                                     np.array([SB] * len(ys)), threads=threads,
+                                                     cap=C3_CAP)
+        gs, gc, gm, gt = (t.cpu().numpy() for t in g)
+        ok = 0
+        for i, sidx in enumerate(firsts):
+            k = int(cnt[i])
+            ok += (int(gs[sidx]) == int(st[i]) and int(gc[sidx]) == k and
+                   np.array_equal(gt[sidx, :k], tab[i, :k]) and
+                   abs(gm[sidx] - mse[i]) <= 1e-12 * abs(mse[i]))
+        r3["verified"] = f"{ok}/{len(firsts)} (first spectrum of every rank's block vs the oracle)"
+    out["configs[3]"] = r3
+    ctx.close()
+    del x3, y3, o3
+    torch.cuda.empty_cache()
+    # configs[4]
+    spectra = md.Spectrum.read_bruker_set(BLOOD, 10, 10, (-2.2, 11.8))
+    dec = md.Deconvoluter()
+    dec.device = dev.index
+    res = par_deconvolute_spectra(dec, spectra)
+    ts = []
+    for _ in range(10):
+        dist.barrier()
+        t0 = time.perf_counter()
+        res = par_deconvolute_spectra(dec, spectra)
+        dist.barrier()
+        ts.append(max_over_ranks(dist, torch, dev, [time.perf_counter() - t0])[0])
+    ok = 0
+    for k, d in enumerate(res):
+        gd = np.load(os.path.join(GOLDEN, f"blood_{k + 1:02d}.npz"))
+        ok += (np.array_equal(d.params, gd["params"]) and
+               abs(d.mse - float(gd["mse"])) <= 1e-12 * abs(float(gd["mse"])))
+    out["configs[4]"] = {
+        "value": len(spectra) / statistics.median(ts), "unit": "spectra/s", "n_ranks": world,
+        "ms_per_step": 1e3 * statistics.median(ts), "steps": 10, "scaling": "strong",
+        "verified": f"{ok}/{len(res)} (goldens)",
+        "workload": ("the 16 blood spectra, Spectrum.read_bruker_set + "
+                     "distributed.par_deconvolute_spectra (sharded, host buffers, RCCL gather)")}
+    return out
+
+
+def dist_configs_dry(args, rank, world):
+    """--dry-run: the same sharding and gathers on CPU tensors (gloo), no engine: zero
+    tables for configs[3], an empty compute for configs[4]."""
+    import torch
+    import metabodecon as md
+    from metabodecon.distributed import deconvolute_distributed, gather_tables, shard_range
+    lo, hi = shard_range(C3_N, rank, world)
+    b = hi - lo
+    g = gather_tables(torch.zeros(b, dtype=torch.int32), torch.zeros(b, dtype=torch.int32),
+                      torch.zeros(b, dtype=torch.float64), torch.zeros((b, 4, 3), dtype=torch.float64),
+                      C3_N)
+    assert g[0].shape[0] == C3_N
+    spectra = md.Spectrum.read_bruker_set(BLOOD, 10, 10, (-2.2, 11.8))
+    res = deconvolute_distributed(spectra, lambda blk: [(0, np.zeros((0, 3)), 0.0)] * len(blk))
+    assert len(res) == len(spectra)
+    return {"configs[3]": {"n_ranks": world, "spectra": C3_N, "spectra_per_rank": b,
+                           "dry_run": True},
+            "configs[4]": {"n_ranks": world, "spectra": len(res), "dry_run": True}}
+
+
 # ------------------------------------------------------------------ CPU baselines
 def cpu_baselines(args, threads, Yh, x, blood_sp, blood_set, c3):
     """The oracle (C restatement, -O3, no FMA) timed on this host: median of 5."""
@@ -775,10 +926,12 @@ def dry_run(args, world, rank):
     el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    configs = dist_configs_dry(args, rank, world) if world > 1 else {}
     if rank == 0:
         print(json.dumps({"metric": "spectra/s (128k pts, ~2k peaks)", "value": None,
                           "unit": "spectra/s", "n_gpus": world, "steps": args.steps,
-                          "warmup": args.warmup, "dry_run": True, "max_elapsed_s": float(el)}),
+                          "warmup": args.warmup, "dry_run": True, "max_elapsed_s": float(el),
+                          "configs": configs}),
               flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -875,6 +1028,7 @@ def queue_line(args, h, world, nat):
                    "selected_peaks": h["selected_peaks"], "kept_peaks": h["kept_peaks"],
                    "parallelism": f"dp{world}" if world > 1 else "single"},
         "verified": h["verified"],
+        "rccl_gather_ms": h["gather_ms"],
         "roofline": roof,
         "roofline_pipeline": pipe,
         "stages_ms_per_spectrum": h["stages_ms_per_spectrum"],
@@ -926,6 +1080,10 @@ def stream_line(args, h, world, nat):
 
 
 def finish(args, line, value, nat, torch, dist, dev, rank, world, local):
+    if (world > 1 or args.force_dist) and not args.no_configs:
+        threads, _, _ = host_threads(args)
+        dc = dist_configs(args, nat, torch, dist, dev, rank, world, threads)
+        line["configs" if world > 1 else "configs_dist"] = dc
     if rank == 0 and world == 1:
         torch.cuda.synchronize()
         want = set() if args.no_configs else {int(c) for c in args.configs.split(",") if c}

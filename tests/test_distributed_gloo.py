@@ -101,7 +101,9 @@ def test_bench_gpus_2_spawns_two_ranks():
     """`bench.py --gpus 2` (no torchrun environment) starts 2 rank processes itself
     as a child torch.distributed.run; --dry-run keeps them off the GPU (gloo), while
     the launcher, rendezvous, table gather and max-over-ranks timing run as on the
-    GPU path. The rank-0 line reports n_gpus 2."""
+    GPU path, and so do the sharding and gathers of the multi-rank configs[3]
+    (4096 spectra by shard_range, gather_tables) and configs[4] (the blood set
+    through deconvolute_distributed). The rank-0 line reports n_gpus 2."""
     import json
     import subprocess
     import sys
@@ -115,6 +117,10 @@ def test_bench_gpus_2_spawns_two_ranks():
     assert len(lines) == 1, p.stdout
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["dry_run"] is True
+    # the sharded configs' launch, sharding and gather code ran on both ranks
+    c3, c4 = rec["configs"]["configs[3]"], rec["configs"]["configs[4]"]
+    assert c3["n_ranks"] == 2 and c3["spectra"] == 4096 and c3["spectra_per_rank"] == 2048
+    assert c4["n_ranks"] == 2 and c4["spectra"] == 16
 
 
 def test_bench_rejects_gpus_world_mismatch():
