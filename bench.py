@@ -672,6 +672,26 @@ def blood_gpu(args, nat, torch, dev):
                 "path": "Deconvoluter.deconvolute_spectrum, host buffers (H2D/D2H inside)"}
 
 
+def optimize_gpu(args, nat, torch, dev, sp):
+    """Deconvoluter.optimize_settings on blood_01 (deconvoluter.rs:762-825): 810
+    deconvolutions of one 131072-point spectrum (27 batched pipelines of 30
+    settings, near-ties re-run in the exact order), host buffers."""
+    import metabodecon as md
+    ts, mse = [], None
+    for k in range(3):
+        dec = md.Deconvoluter()
+        dec.device = dev.index
+        t = time.perf_counter()
+        mse = dec.optimize_settings(sp)
+        ts.append(time.perf_counter() - t)
+    s = dec.settings
+    return {"value": 810 / statistics.median(ts[1:]), "unit": "deconvolutions/s",
+            "seconds": statistics.median(ts[1:]), "steps": 2, "warmup": 1, "mse": mse,
+            "best": [int(s.smooth_iterations), int(s.smooth_window), float(s.threshold),
+                     int(s.fit_iterations)],
+            "workload": "Deconvoluter.optimize_settings(blood_01): the 810-setting grid"}
+
+
 def bruker_set(args, nat, torch, dev):
     """configs[4]: the 16 blood spectra, Spectrum.read_bruker_set ->
     Deconvoluter.par_deconvolute_spectra (one batched call, host buffers)."""
@@ -888,6 +908,13 @@ def cpu_baselines(args, threads, Yh, x, blood_sp, blood_set, c3):
         par, _ = median_rate(lambda: oracle.deconvolute(bx, by, bsb, threads=threads), 1)
         out["blood_01"] = {"deconvolute_spectrum": seq, "par_deconvolute_spectrum": par,
                            "unit": "spectra/s", "par_threads": threads}
+    if blood_sp is not None:  # optimize_settings: the exhaustive grid, one setting per thread
+        t = time.perf_counter()
+        st, best, mse = oracle.optimize_settings(bx, by, bsb, threads=threads)
+        el = time.perf_counter() - t
+        out["optimize_settings"] = {"value": 810 / el, "unit": "deconvolutions/s", "seconds": el,
+                                    "threads": threads, "best": list(best) if best else None,
+                                    "mse": mse, "reps": 1}
     if blood_set is not None:  # configs[4]: par_deconvolute_spectra over the 16 spectra
         X = np.stack([s.chemical_shifts for s in blood_set])
         Yb = np.stack([s.intensities for s in blood_set])
@@ -1097,6 +1124,7 @@ def finish(args, line, value, nat, torch, dist, dev, rank, world, local):
             nat.release_lanes(dev.index)  # 16 idle lane streams slow configs[0] by ~15%
         if 0 in want:
             blood_sp, configs["configs[0]"] = blood_gpu(args, nat, torch, dev)
+            configs["optimize_settings"] = optimize_gpu(args, nat, torch, dev, blood_sp)
         if 2 in want:
             configs["configs[2]"] = batch_config(args, nat, torch, dev, 256, 131072, 2048, 3, 1,
                                                  "b256")
@@ -1126,6 +1154,10 @@ def finish(args, line, value, nat, torch, dist, dev, rank, world, local):
             line["cpu_baseline"] = cb["synthetic"]
             line["cpu_baselines"] = {k: v for k, v in cb.items() if k != "synthetic"}
             line["speedup_vs_cpu"] = value / cb["synthetic"]["value"]
+            if "optimize_settings" in configs and "optimize_settings" in cb:
+                g, c = configs["optimize_settings"], cb["optimize_settings"]
+                g["speedup_vs_cpu"] = g["value"] / c["value"]
+                g["same_result_as_cpu"] = (g["best"] == c["best"] and g["mse"] == c["mse"])
             for key, ref in (("configs[0]", ("blood_01", "par_deconvolute_spectrum")),
                              ("configs[2]", ("synthetic", "value")),
                              ("configs[3]", ("synthetic_65536", "value")),

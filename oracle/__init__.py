@@ -331,3 +331,47 @@ def deconvolute_batch(x, y, sb, settings: Settings | None = None, ignore=(), thr
                                        status.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
                                        threads, inner_threads)
     return status, counts.astype(np.int64), out, mse
+
+
+def optimize_settings_grid():
+    """The reference's grid in its order (deconvoluter.rs:762-788): smoothing
+    (iterations 2..=10 x window 3, 5, 7) outermost, then the 10 noise-score
+    thresholds 5 + c * 3 / 9, then the analytical fit iterations 5, 10, 15."""
+    grid = []
+    for it in range(2, 11):
+        for ws in (3, 5, 7):
+            for c in range(10):
+                thr = 5.0 + (c * (8.0 - 5.0)) / 9.0
+                for fit in (5, 10, 15):
+                    grid.append((it, ws, thr, fit))
+    return grid
+
+
+def optimize_settings(x, y, sb, ignore=(), threads: int = 1):
+    """Deconvoluter::optimize_settings (deconvoluter.rs:762-825): every grid setting
+    deconvolutes the reference spectrum; a failing one returns its status (the
+    reference's `?`; the first in grid order here); otherwise the FIRST minimum MSE
+    in grid order wins (Iterator::min_by). Returns (status, (iterations, window,
+    threshold, fit_iterations) or None, mse). The 810 deconvolutions run on
+    ``threads`` worker threads (ctypes releases the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+    grid = optimize_settings_grid()
+    x, y = _f64(x), _f64(y)
+
+    def one(g):
+        it, ws, thr, fit = g
+        st = make_settings(smooth_iterations=it, smooth_window=ws, threshold=thr,
+                           fit_iterations=fit)
+        r = deconvolute(x, y, sb, st, ignore=ignore)
+        return r.status, r.mse
+
+    with ThreadPoolExecutor(max_workers=max(1, threads)) as pool:
+        res = list(pool.map(one, grid))
+    for st, _ in res:
+        if st:
+            return st, None, None
+    best = 0
+    for k in range(1, len(res)):
+        if res[k][1] < res[best][1]:
+            best = k
+    return 0, grid[best], res[best][1]

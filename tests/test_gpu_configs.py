@@ -99,3 +99,23 @@ def test_configs3_4096x65536_bit_exact():
     counts = _compare(res, cap)
     assert counts.min() > 900
     res["ctx"].close()
+
+
+def test_optimize_settings_blood_01_full_size():
+    """Deconvoluter.optimize_settings on a real 131072-point
+    spectrum (blood_01, Bruker 10/10, sb (-2.2, 11.8)) against the exhaustive
+    810-setting oracle sweep (deconvoluter.rs:762-825; first minimum in the grid's
+    order) on the box's cores: the argmin and its MSE bit for bit."""
+    import os
+    import metabodecon as md
+    from tests.conftest import GOLDEN
+    sp = md.Spectrum.read_bruker(os.path.join(GOLDEN, "bruker", "blood", "blood_01"), 10, 10,
+                                 (-2.2, 11.8))
+    dec = md.Deconvoluter()
+    got = dec.optimize_settings(sp)
+    st, best, mse = oracle.optimize_settings(sp.chemical_shifts, sp.intensities,
+                                             sp.signal_boundaries, threads=host_threads())
+    assert st == 0
+    s = dec.settings
+    assert (s.smooth_iterations, s.smooth_window, s.threshold, s.fit_iterations) == best
+    assert got == mse
