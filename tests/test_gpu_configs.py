@@ -31,13 +31,13 @@ torch = pytest.importorskip("torch")
 SB = (11.8, -2.2)
 
 
-def _device_batch(B, n, peaks, hw_scale, cap, seed0=0):
+def _device_batch(B, n, peaks, hw_scale, cap, seed0=0, sigma=1.0e3):
     ctx = nat.Context(0)
     dev = torch.device("cuda", 0)
     x = torch.empty(n, dtype=torch.float64, device=dev)
     y = torch.empty((B, n), dtype=torch.float64, device=dev)
     rc = nat.lib().mdg_synth_batch_device_hw(ctx.handle, B, n, 14.8, 20.0, seed0, peaks, -1.8,
-                                             11.4, hw_scale, 1.0e3, x.data_ptr(), y.data_ptr())
+                                             11.4, hw_scale, sigma, x.data_ptr(), y.data_ptr())
     assert rc == 0, nat.strerror(rc)
     sb = torch.tensor([SB] * B, dtype=torch.float64, device=dev)
     out = torch.zeros((B, cap, 3), dtype=torch.float64, device=dev)
@@ -119,3 +119,19 @@ def test_optimize_settings_blood_01_full_size():
     s = dec.settings
     assert (s.smooth_iterations, s.smooth_window, s.threshold, s.fit_iterations) == best
     assert got == mse
+
+
+@pytest.mark.parametrize("hw_scale,sigma", [(0.5, 1.0), (0.3, 1.0e-3), (0.5, 0.0)])
+def test_mse_narrow_peaks_close_fit(hw_scale, sigma):
+    """k_mse_local sums the far Lorentzians of a tile as a 20-term series of
+    Im[a/(x - z)], whose terms exceed the Lorentzian by ~distance/half-width, so its
+    roundoff is amplified most by narrow peaks; and a close fit (near-zero noise)
+    makes the residual, hence the MSE, small against the superposition. Narrow
+    half-widths (x0.3, x0.5) with sigma 1, 1e-3 and 0: every MSE within MSE_RTOL of
+    the oracle's left fold (and the parameters bit-identical, as everywhere)."""
+    cap = 4096
+    res = _device_batch(4, 131072, 2048, hw_scale, cap, seed0=40, sigma=sigma)
+    assert res["kernels"].get("mse_superposition", "").startswith("k_mse_local")
+    counts = _compare(res, cap)
+    assert counts.min() > 100
+    res["ctx"].close()
