@@ -76,7 +76,7 @@ def parse():
                     help="queue: single-spectrum submissions to an mdg_queue (batched into "
                          "pipelines of --max-batch on --lanes contexts); stream: the round-2 form, "
                          "one B=--batch pipeline per call on --streams contexts")
-    ap.add_argument("--max-batch", type=int, default=128, help="queue: spectra per pipeline")
+    ap.add_argument("--max-batch", type=int, default=192, help="queue: spectra per pipeline")
     ap.add_argument("--lanes", type=int, default=2, help="queue: engine contexts (own streams)")
     ap.add_argument("--step-spectra", type=int, default=0,
                     help="queue: spectra per step (0 = max_batch * lanes)")
@@ -110,6 +110,9 @@ def parse():
     ap.add_argument("--force-dist", action="store_true",
                     help="diagnostics: run the multi-rank path (RCCL process group, gathers) "
                          "even at world size 1, under torchrun")
+    ap.add_argument("--c4-only", action="store_true",
+                    help="measure configs[4] only and print its JSON block (bench.py runs itself "
+                         "this way under GPU_MAX_HW_QUEUES=32 for the second environment)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: exercise the launcher, rendezvous and gather (gloo)")
     return ap.parse_args()
@@ -733,8 +736,9 @@ def bruker_set(args, nat, torch, dev):
                      "ms_per_step": el / steps * 1e3, "steps": steps, "spectra_per_step":
                      len(spectra), "read_s": read_s, "kept_peaks": counts, "roofline": roof,
                      "path": "Spectrum.read_bruker_set + Deconvoluter.par_deconvolute_spectra "
-                             "(one spectrum per engine context, concurrently), host buffers "
-                             "(PCIe inside the timed region)"}
+                             "(the set cut into Deconvoluter.LANES chunks, one batched pipeline "
+                             "per lane context, concurrently), host buffers (PCIe inside the "
+                             "timed region)"}
 
 
 # ------------------------------------------------------------------ multi-rank configs
@@ -990,6 +994,12 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if args.c4_only:
+        _, c4 = bruker_set(args, nat, torch, dev)
+        c4["hw_queues"] = os.environ.get("GPU_MAX_HW_QUEUES", "unset (HIP default 4)")
+        c4["lanes"] = __import__("metabodecon").Deconvoluter.LANES
+        print(json.dumps(c4), flush=True)
+        return
 
     idle = [torch.cuda.Stream(device=dev) for _ in range(args.idle_streams)]
     for st in idle:
@@ -1120,8 +1130,20 @@ def finish(args, line, value, nat, torch, dist, dev, rank, world, local):
         # streams created before the 16 lanes') its sets took 5.5 instead of 3.9 ms
         # (tools/c4_order.sh), the others are single-stream and order-insensitive
         if 4 in want:
+            import metabodecon as md
             blood_set, configs["configs[4]"] = bruker_set(args, nat, torch, dev)
-            nat.release_lanes(dev.index)  # 16 idle lane streams slow configs[0] by ~15%
+            configs["configs[4]"]["hw_queues"] = os.environ.get("GPU_MAX_HW_QUEUES",
+                                                               "unset (HIP default 4)")
+            configs["configs[4]"]["lanes"] = md.Deconvoluter.LANES
+            nat.release_lanes(dev.index)  # idle lane streams slow configs[0]
+            # the same measurement in a child process with 32 hardware queues (16 lanes)
+            env = dict(os.environ, GPU_MAX_HW_QUEUES="32")
+            p = subprocess.run([sys.executable, os.path.abspath(__file__), "--c4-only"],
+                               env=env, capture_output=True, text=True, timeout=300)
+            try:
+                configs["configs[4]_hw_queues_32"] = json.loads(p.stdout.strip().splitlines()[-1])
+            except (ValueError, IndexError):
+                configs["configs[4]_hw_queues_32"] = {"error": p.stderr[-500:]}
         if 0 in want:
             blood_sp, configs["configs[0]"] = blood_gpu(args, nat, torch, dev)
             configs["optimize_settings"] = optimize_gpu(args, nat, torch, dev, blood_sp)

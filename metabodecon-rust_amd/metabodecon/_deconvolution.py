@@ -393,12 +393,14 @@ class Deconvoluter:
             return np.zeros(0)
         return np.array(self._ignore, dtype=np.float64).reshape(-1)
 
-    # Spectra of one call deconvoluted concurrently, one per engine context (own
-    # HIP stream and workspace), up to this many; larger groups run as one batched
-    # pipeline. Small sets gain: each spectrum's sequential smoother overlaps the
-    # others' fits; a large batch already fills the GPU. HIP maps
-    # streams round-robin onto GPU_MAX_HW_QUEUES hardware queues (4 unless set)
-    # and two busy streams on one queue serialise, so the lanes stay below it.
+    # Engine contexts (own HIP stream and workspace each) a call spreads its spectra
+    # over: a set of one length is cut into that many contiguous chunks (one
+    # spectrum each when the set is that small), each chunk one batched pipeline on
+    # its own lane, all lanes concurrently: each chunk's sequential smoother overlaps
+    # the others' fits. HIP maps streams round-robin onto
+    # GPU_MAX_HW_QUEUES hardware queues (4 unless set) and two busy streams on one
+    # queue serialise, so the lanes stay below it (one queue is left for the
+    # caller's own stream); with the default 4 queues that is 3 lanes.
     LANES = max(1, min(16, int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) - 1))
 
     def _run_batch(self, ctx, spectra: list[Spectrum], idx: list[int], n: int, ign):
@@ -423,9 +425,9 @@ class Deconvoluter:
                 for k in range(b)]
 
     def _run(self, spectra: list[Spectrum]) -> list[tuple[int, np.ndarray, float]]:
-        """GPU results per spectrum, (status, params, mse) in input order: spectra of
-        one length run one per context concurrently (up to LANES of them), or as one
-        batched pipeline."""
+        """GPU results per spectrum, (status, params, mse) in input order: the
+        spectra of one length are cut into min(LANES, count) contiguous chunks that
+        run concurrently, one batched pipeline per lane context."""
         results: list = [None] * len(spectra)
         by_n: dict[int, list[int]] = {}
         for i, sp in enumerate(spectra):
@@ -434,16 +436,20 @@ class Deconvoluter:
             by_n.setdefault(len(sp), []).append(i)
         ign = self._ignore_array()
         for n, idx in by_n.items():
-            if 1 < len(idx) <= self.LANES:
-                lanes = nat.lane_contexts(self.device, len(idx))
-                pool = _lane_pool(self.LANES)
-                futs = [pool.submit(self._run_batch, lanes[k], spectra, [i], n, ign)
-                        for k, i in enumerate(idx)]
-                for i, f in zip(idx, futs):
-                    results[i] = f.result()[0]
-            else:
+            k = min(self.LANES, len(idx))
+            if k <= 1:
                 res = self._run_batch(nat.context(self.device), spectra, idx, n, ign)
                 for i, r in zip(idx, res):
+                    results[i] = r
+                continue
+            from .distributed import shard_range
+            chunks = [idx[lo:hi] for lo, hi in (shard_range(len(idx), r, k) for r in range(k))]
+            lanes = nat.lane_contexts(self.device, k)
+            pool = _lane_pool(self.LANES)
+            futs = [pool.submit(self._run_batch, lanes[j], spectra, c, n, ign)
+                    for j, c in enumerate(chunks)]
+            for c, f in zip(chunks, futs):
+                for i, r in zip(c, f.result()):
                     results[i] = r
         return results
 
