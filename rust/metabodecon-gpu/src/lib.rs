@@ -11,6 +11,7 @@
 //! | `Deconvoluter::deconvolute_spectra` (:651-661), `par_deconvolute_spectra` (:700-710) | [`GpuDeconvoluter::gpu_deconvolute_spectra`] |
 //! | `Deconvoluter::optimize_settings` (:762-825)     | [`GpuDeconvoluter::gpu_optimize_settings`] |
 //! | `Lorentzian::superposition_vec` / `par_superposition_vec` (lorentzian.rs:631-663) | [`gpu_superposition_vec`] |
+//! | many concurrent `par_deconvolute_spectrum` callers (Deconvoluter is `Send + Sync`, deconvoluter.rs:913-917) | [`GpuSpectrumQueue`] (device arrays, batched internally) |
 //!
 //! The reference's stage traits are `pub(crate)`, so the seam is these public
 //! methods; everything here uses only the reference's public API
@@ -67,6 +68,12 @@ pub mod ffi {
     /// Opaque `mdg_ctx`.
     #[repr(C)]
     pub struct MdgCtx {
+        _private: [u8; 0],
+    }
+
+    /// Opaque `mdg_queue` (the spectrum queue).
+    #[repr(C)]
+    pub struct MdgQueue {
         _private: [u8; 0],
     }
 
@@ -187,6 +194,38 @@ pub mod ffi {
             p: usize,
             d_out: *mut f64,
         ) -> c_int;
+        pub fn mdg_queue_create(
+            device: c_int,
+            n: usize,
+            max_batch: usize,
+            lanes: c_int,
+            s: *const MdgSettings,
+            ignore: *const f64,
+            n_ignore: usize,
+            out: *mut *mut MdgQueue,
+        ) -> c_int;
+        pub fn mdg_queue_submit(
+            q: *mut MdgQueue,
+            d_x: *const f64,
+            d_y: *const f64,
+            sb0: f64,
+            sb1: f64,
+            d_out: *mut MdgLorentzian,
+            cap: usize,
+            d_count: *mut i32,
+            d_mse: *mut f64,
+            d_status: *mut i32,
+        ) -> c_int;
+        pub fn mdg_queue_flush(q: *mut MdgQueue) -> c_int;
+        pub fn mdg_queue_synchronize(q: *mut MdgQueue) -> c_int;
+        pub fn mdg_queue_lane(q: *mut MdgQueue, lane: c_int, ctx: *mut *mut MdgCtx) -> c_int;
+        pub fn mdg_queue_stats(
+            q: *mut MdgQueue,
+            batches: *mut u64,
+            spectra: *mut u64,
+            open: *mut usize,
+        ) -> c_int;
+        pub fn mdg_queue_destroy(q: *mut MdgQueue) -> c_int;
     }
 }
 
@@ -238,6 +277,98 @@ impl GpuContext {
 impl Drop for GpuContext {
     fn drop(&mut self) {
         unsafe { ffi::mdg_ctx_destroy(self.ctx.as_ptr()) };
+    }
+}
+
+/// The spectrum queue (`mdg_queue_*`): the serving form of many concurrent
+/// `Deconvoluter::par_deconvolute_spectrum` calls (the reference's Deconvoluter
+/// is `Send + Sync`, deconvoluter.rs:913-917). Each submission is one spectrum in
+/// device memory; the engine runs them in batches of `max_batch` on `lanes`
+/// engine contexts. Settings and ignore regions are the Deconvoluter's at
+/// creation.
+pub struct GpuSpectrumQueue {
+    q: NonNull<ffi::MdgQueue>,
+}
+
+unsafe impl Send for GpuSpectrumQueue {}
+unsafe impl Sync for GpuSpectrumQueue {}
+
+impl GpuSpectrumQueue {
+    /// Queue for spectra of `n` points on HIP device `device`.
+    pub fn new(
+        deconvoluter: &Deconvoluter,
+        device: i32,
+        n: usize,
+        max_batch: usize,
+        lanes: i32,
+    ) -> Result<Self> {
+        let s = Settings::of(deconvoluter).to_ffi()?;
+        let ig = ignore_pairs(deconvoluter);
+        let mut raw: *mut ffi::MdgQueue = ptr::null_mut();
+        let st = unsafe {
+            ffi::mdg_queue_create(
+                device as c_int,
+                n,
+                max_batch,
+                lanes as c_int,
+                &s,
+                opt_ptr(&ig),
+                ig.len() / 2,
+                &mut raw,
+            )
+        };
+        match NonNull::new(raw) {
+            Some(q) if st == ffi::MDG_OK => Ok(Self { q }),
+            _ => Err(engine_error(st)),
+        }
+    }
+
+    /// Submit one spectrum (asynchronous).
+    ///
+    /// # Safety
+    /// Every pointer is device memory of the queue's device: `d_x`, `d_y` hold `n`
+    /// values and stay unchanged, and `d_out` (`cap` entries), `d_count`, `d_mse`,
+    /// `d_status` stay valid, until [`GpuSpectrumQueue::synchronize`] returns.
+    #[allow(clippy::too_many_arguments)]
+    pub unsafe fn submit(
+        &self,
+        d_x: *const f64,
+        d_y: *const f64,
+        signal_boundaries: (f64, f64),
+        d_out: *mut ffi::MdgLorentzian,
+        cap: usize,
+        d_count: *mut i32,
+        d_mse: *mut f64,
+        d_status: *mut i32,
+    ) -> Result<()> {
+        check(ffi::mdg_queue_submit(
+            self.q.as_ptr(),
+            d_x,
+            d_y,
+            signal_boundaries.0,
+            signal_boundaries.1,
+            d_out,
+            cap,
+            d_count,
+            d_mse,
+            d_status,
+        ))
+    }
+
+    /// Launch the open (partial) batch.
+    pub fn flush(&self) -> Result<()> {
+        check(unsafe { ffi::mdg_queue_flush(self.q.as_ptr()) })
+    }
+
+    /// Flush and wait until every submission's outputs are written.
+    pub fn synchronize(&self) -> Result<()> {
+        check(unsafe { ffi::mdg_queue_synchronize(self.q.as_ptr()) })
+    }
+}
+
+impl Drop for GpuSpectrumQueue {
+    fn drop(&mut self) {
+        unsafe { ffi::mdg_queue_destroy(self.q.as_ptr()) };
     }
 }
 

@@ -26,6 +26,7 @@ RUST_TO_C = {
     "c_int": "int", "i32": "int32_t", "u32": "uint32_t", "u64": "uint64_t", "i64": "int64_t",
     "usize": "size_t", "f64": "double", "c_void": "void", "c_char": "char",
     "MdgSettings": "mdg_settings", "MdgLorentzian": "mdg_lorentzian", "MdgCtx": "mdg_ctx",
+    "MdgQueue": "mdg_queue",
 }
 
 
