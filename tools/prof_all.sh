@@ -1,15 +1,17 @@
 #!/bin/bash
-# full profile set for one round: traces and PMC passes of the headline (B=1
-# stream), the B=256 batch (configs[2]) and the 4096 x 65536 batch (configs[3]),
-# plus the FETCH/WRITE width calibration
+# Full profile set for one round (GPU box): kernel traces + stats and the two PMC
+# passes (FETCH_SIZE, WRITE_SIZE; one counter per run) of
+#   q192         the headline: queue mode, 192-spectrum batches on 2 lanes
+#   b256         configs[2]: one 256-spectrum batch per step (stream mode, 1 context)
+#   b4096_n65536 configs[3] on one GPU
+# then tools/pmc_summary.py / tools/trace_summary.py turn them into profiles/.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 set -e
-bash tools/prof_session.sh calib FETCH_SIZE
-bash tools/prof_session.sh calib WRITE_SIZE
-bash tools/prof_session.sh trace b1 --streams 1 --steps 40
-bash tools/prof_session.sh trace b256 --batch 256 --streams 1 --steps 2 --warmup 1
-bash tools/prof_session.sh trace b4096_n65536 --batch 4096 --streams 1 --steps 1 --warmup 1 --n 65536 --peaks 1024 --hw-scale 2 --cap 2048
-bash tools/prof_session.sh pmc b1 FETCH_SIZE --streams 1 --steps 5
-bash tools/prof_session.sh pmc b1 WRITE_SIZE --streams 1 --steps 5
-bash tools/prof_session.sh pmc b256 FETCH_SIZE --batch 256 --streams 1 --steps 1 --warmup 1
-bash tools/prof_session.sh pmc b256 WRITE_SIZE --batch 256 --streams 1 --steps 1 --warmup 1
+S=tools/prof_session.sh
+bash $S trace q192 --steps 6 --warmup 2 --verify 0
+bash $S pmc q192 FETCH_SIZE --steps 2 --warmup 1 --verify 0
+bash $S pmc q192 WRITE_SIZE --steps 2 --warmup 1 --verify 0
+bash $S trace b256 --mode stream --batch 256 --streams 1 --steps 2 --warmup 1
+bash $S pmc b256 FETCH_SIZE --mode stream --batch 256 --streams 1 --steps 1 --warmup 1
+bash $S pmc b256 WRITE_SIZE --mode stream --batch 256 --streams 1 --steps 1 --warmup 1
+bash $S trace b4096_n65536 --mode stream --batch 4096 --streams 1 --steps 1 --warmup 1 --n 65536 --peaks 1024 --hw-scale 2 --cap 2048
