@@ -2974,6 +2974,56 @@ __global__ void k_fit_sup(BatchArgs a, Workspace w, int it) {
     }
 }
 
+// K6f  fit superposition with the stencil update fused (batches, B > 8): one point
+// per lane and each lane's left fold over the P Lorentzians as in k_fit_sup, but a
+// 256-thread workgroup owns 255 consecutive points = 85 whole peaks, so after the
+// superposition the ratios meet in LDS and 85 threads do k_fit_update's work for
+// their peak (scale the stencil by the ratios, mirror_shoulder, solve). Version it+1
+// of the parameters goes into the other buffer (params / params_alt, as the
+// term-fold kernels do), because other workgroups still read version it: one launch
+// per fit iteration instead of two. Range flags rotate over three slots as in
+// k_fit_sup_tf: iteration it reads slot it % 3, its updates count into (it+1) % 3,
+// and it clears (it+2) % 3 (last read by iteration it-1).
+constexpr int kFuPts = 255;  // points per workgroup: 85 peaks
+
+__global__ __launch_bounds__(256) void k_fit_sup_fu(BatchArgs a, Workspace w, int it) {
+    const int s = blockIdx.x % a.B, part = blockIdx.x / a.B, parts = gridDim.x / a.B;
+    __shared__ double rat[256];
+    if (w.status[s] || fit_done(w, s, it)) return;
+    const int P = w.sel_count[s];
+    const int npts = 3 * P;
+    const size_t base = (size_t)s * w.capD;
+    if (part == 0 && threadIdx.x == 0) w.unsafe[4 * s + (it + 2) % 3] = 0;
+    const bool fast = w.x_ok[s] && w.unsafe[4 * s + it % 3] == 0;
+    const double* __restrict__ prm = params_version(w, base, it);
+    double* __restrict__ next = (double*)params_version(w, base, it + 1);
+    const int tid = threadIdx.x;
+    for (int t = part; t * kFuPts < npts; t += parts) {  // uniform over the workgroup
+        const int i = t * kFuPts + tid;
+        double ratio = 0.0;
+        if (tid < kFuPts && i < npts) {
+            const double sup = superpose(w.rx[3 * base + i], prm, P, fast);
+            ratio = w.ry[3 * base + i] / sup;  // fitter_analytical.rs:42-47
+        }
+        rat[tid] = ratio;
+        __syncthreads();
+        const int pk = t * (kFuPts / 3) + tid;
+        if (tid < kFuPts / 3 && pk < P) {  // fitter_analytical.rs:48-65
+            double* st = w.stencil + 6 * base + 6 * (size_t)pk;
+            Stencil q{st[0], st[1], st[2], st[3], st[4], st[5]};
+            q.y1 = q.y1 * rat[3 * tid];
+            q.y2 = q.y2 * rat[3 * tid + 1];
+            q.y3 = q.y3 * rat[3 * tid + 2];
+            mirror_shoulder(q);
+            st[0] = q.x1; st[1] = q.x2; st[2] = q.x3; st[3] = q.y1; st[4] = q.y2; st[5] = q.y3;
+            double* L = next + 3 * (size_t)pk;
+            solve(q, L);
+            if (!peak_fast_ok(L[0], L[1], L[2])) atomicAdd(&w.unsafe[4 * s + (it + 1) % 3], 1);
+        }
+        __syncthreads();
+    }
+}
+
 // EXPERIMENT (configs[2] "superposition recast as MFMA outer product", SURVEY
 // 8d): the fit superposition with every denominator hw2 + (x - maxp)^2 taken
 // from v_mfma_f64_16x16x4_f64 as the product [x'^2, x', 1, 0] . [1, -2m', m'^2 +
@@ -4144,11 +4194,11 @@ void launch_fit_init(const BatchArgs& a, const Workspace& w, int gx, hipStream_t
 static std::string fit_choice(const BatchArgs& a) {
     const char* force = std::getenv("MDG_FITSUP");
     if (force && *force) return force;
-    return a.B == 1 ? "tw7" : a.B <= 2 ? "tf" : a.B <= 8 ? "dpp" : "plain";
+    return a.B == 1 ? "tw7" : a.B <= 2 ? "tf" : a.B <= 8 ? "dpp" : "fu";
 }
 bool fit_sup_fused(const BatchArgs& a) {
     const std::string f = fit_choice(a);
-    return f == "tf" || f.rfind("tw", 0) == 0;
+    return f == "tf" || f == "fu" || f.rfind("tw", 0) == 0;
 }
 const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st) {
     const std::string f = fit_choice(a);
@@ -4206,6 +4256,13 @@ const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int i
         const int g = std::max(64, std::min(1024, 2048 / a.B));
         launch_k((k_fit_sup_split<16, 128, 1024>), dim3(g, a.B), dim3(1024), 0, st, a, w, it);
         return "k_fit_sup_split<16, 128, 1024>";
+    }
+    if (f == "fu") {
+        // 255 points per workgroup: 25 workgroups per spectrum at P = 2048
+        // (6144 points), grid-stride beyond
+        const int parts = std::max(1, (3 * 2048 + kFuPts - 1) / kFuPts);
+        launch_k(k_fit_sup_fu, dim3(parts * a.B), dim3(256), 0, st, a, w, it);
+        return "k_fit_sup_fu";
     }
     // gx 256-thread workgroups per spectrum (24: one point per thread at P = 2048)
     launch_k(k_fit_sup, dim3(gx * a.B), dim3(256), 0, st, a, w, it);
