@@ -191,6 +191,8 @@ int ensure_workspace(mdg_ctx* c, int B, int N, int n_ignore) {
         const size_t o_xok = take(Bs * 4), o_unsafe = take(Bs * 16), o_uk = take(Bs * 4);
         const size_t o_pcnt = take(Bs * 2 * ((W + 255) / 256) * 4);
         const size_t o_mcnt = take(Bs * 4);
+        const size_t o_fdyn = take((kFitDynCtl + Bs * (3 * capD / 64 + 2)) * 4);
+        const size_t o_fpart = take(Bs * (3 * capD + 64) * 8);
 
         if (c->arena.p) (void)hipFree(c->arena.p);
         c->arena.p = nullptr;
@@ -233,6 +235,8 @@ int ensure_workspace(mdg_ctx* c, int B, int N, int n_ignore) {
         w.unsafe_kept = (int32_t*)(base + o_uk);
         w.peak_cnt = (int32_t*)(base + o_pcnt);
         w.mse_done = (int32_t*)(base + o_mcnt);
+        w.fit_dyn = (int32_t*)(base + o_fdyn);
+        w.fit_part = (double*)(base + o_fpart);
         // k_mse_partial_n's arrival counters start (and are always left) at zero
         HIPCHK(hipMemset(w.mse_done, 0, Bs * 4));
 
@@ -384,6 +388,10 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
         StageTimer t(c, ST_FIT_INIT);
         launch_fit_init(a, w, gupd, st);
         kn[ST_FIT_INIT] = "k_fit_init";
+    }
+    if (fit_sup_dyn(a)) {
+        StageTimer t(c, ST_FIT_INIT);
+        launch_fit_plan(a, w, st);
     }
     for (uint32_t it = 0; it < s->fit_iterations; ++it) {
         {

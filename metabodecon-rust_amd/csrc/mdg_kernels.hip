@@ -3024,6 +3024,117 @@ __global__ __launch_bounds__(256) void k_fit_sup_fu(BatchArgs a, Workspace w, in
     }
 }
 
+// K6q  work-queue fit superposition (batches): the same per-point left folds as
+// k_fit_sup, but a point's fold over the P Lorentzians is cut into kDynPieces
+// consecutive ranges, and persistent workgroups pull (64-point chunk, piece) items
+// from eight queue heads (one per XCD group of blocks, blockIdx % 8; a workgroup
+// whose queue is empty takes from the others). Items are ordered piece-major, so a
+// launch's tail is a fraction of a piece instead of a whole 2048-term fold: with one
+// 64-point chunk per wave and every fold as long as the others, the static grid of
+// k_fit_sup leaves SIMDs idle for up to a whole fold at its end (at B = 256 about a
+// tenth of the launch). A piece k > 0 continues the fold from the
+// partial sum piece k-1 left: it waits for the chunk's counter to reach it*K + k
+// (the item was taken earlier, by a running wave, so the wait always ends), then
+// loads the 64 partial sums. Hand-off per MI355X_MICROARCH.md (valid forms): the
+// producer stores its sums write-through (agent-scope relaxed atomic stores, sc1),
+// drains them with s_waitcnt vmcnt(0), and one lane stores the counter (agent
+// scope); the consumer polls it with sc1 loads and loads the sums with sc1 loads.
+// Each point's operations are the reference's, in its order: bit-identical.
+// ctl layout (int32): [0] chunks per spectrum; [64 + 32 * (slot * 8 + q)] queue
+// head q of iteration slot (it & 1), each on its own 128-B line; [kFitDynCtl + chunk]
+// the chunk's progress (it * K + pieces done; monotone, zeroed per pipeline).
+#ifndef MDG_DYN_PIECES
+#define MDG_DYN_PIECES 4
+#endif
+constexpr int kDynPieces = MDG_DYN_PIECES;
+constexpr unsigned kDynSpins = 1u << 22;
+
+__global__ __launch_bounds__(1024) void k_fit_plan(BatchArgs a, Workspace w) {
+    __shared__ int pmax;
+    if (threadIdx.x == 0) pmax = 0;
+    __syncthreads();
+    int m = 0;
+    for (int s = threadIdx.x; s < a.B; s += blockDim.x)
+        if (w.status[s] == 0) m = max(m, w.sel_count[s]);
+    atomicMax(&pmax, m);
+    __syncthreads();
+    const int CH = max(1, (3 * pmax + 63) / 64);
+    int32_t* ctl = w.fit_dyn;
+    if (threadIdx.x == 0) ctl[0] = CH;
+    if (threadIdx.x < 16) ctl[64 + 32 * threadIdx.x] = 0;
+    for (int q = threadIdx.x; q < a.B * CH; q += blockDim.x) ctl[kFitDynCtl + q] = 0;
+}
+
+__global__ __launch_bounds__(256) void k_fit_sup_dyn(BatchArgs a, Workspace w, int it) {
+    int32_t* ctl = w.fit_dyn;
+    const int CH = ctl[0];
+    const int nq = a.B * CH;
+    const int lane = threadIdx.x & 63;
+    const int slot = it & 1;
+    if (blockIdx.x == 0) {
+        // the next iteration's heads, and the range flags its k_fit_update counts into
+        if (threadIdx.x < 8) ctl[64 + 32 * ((slot ^ 1) * 8 + threadIdx.x)] = 0;
+        for (int s = threadIdx.x; s < a.B; s += blockDim.x)
+            if (!fit_done(w, s, it)) w.unsafe[4 * s + ((it + 1) & 1)] = 0;
+    }
+    const int home = blockIdx.x & 7;
+    for (int qi = 0; qi < 8; ++qi) {
+        const int x = (home + qi) & 7;
+        const int nx = (nq - x + 7) / 8;  // chunks x, x + 8, ... of the batch
+        const int items = nx * kDynPieces;
+        int32_t* head = ctl + 64 + 32 * (slot * 8 + x);
+        for (;;) {
+            int j = 0;
+            if (lane == 0) j = __hip_atomic_fetch_add(head, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            j = __builtin_amdgcn_readfirstlane(j);
+            if (j >= items) break;
+            const int k = j / nx;
+            const int ch = x + 8 * (j - k * nx);
+            const int s = ch / CH, c = ch - s * CH;
+            if (w.status[s] || fit_done(w, s, it)) continue;
+            const int P = w.sel_count[s];
+            const int npts = 3 * P;
+            if (c * 64 >= npts) continue;
+            const size_t base = (size_t)s * w.capD;
+            const bool fast = w.x_ok[s] && w.unsafe[4 * s + (it & 1)] == 0;
+            const int T = (P + kDynPieces - 1) / kDynPieces;
+            const int lo = min(P, k * T), hi = min(P, lo + T);
+            const int i = c * 64 + lane;
+            const double xv = w.rx[3 * base + min(i, npts - 1)];
+            double* part = w.fit_part + (size_t)ch * 64 + lane;
+            int32_t* done = ctl + kFitDynCtl + ch;
+            double acc = -0.0;
+            if (k > 0) {
+                const int need = it * kDynPieces + k;
+                unsigned spins = 0;
+                bool ok = true;
+                while (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins > kDynSpins) {
+                        ok = false;
+                        break;
+                    }
+                }
+                if (!ok) {  // never expected: bounds a protocol bug
+                    if (lane == 0) w.status[s] = MDG_ERR_HIP;
+                    continue;
+                }
+                acc = __hip_atomic_load(part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            const double* prm = w.params + 3 * base + 3 * (size_t)lo;
+            acc = fast ? superpose_t<true>(xv, prm, hi - lo, acc) : superpose_t<false>(xv, prm, hi - lo, acc);
+            if (k < kDynPieces - 1) {
+                __hip_atomic_store(part, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (lane == 0)
+                    __hip_atomic_store(done, it * kDynPieces + k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else if (i < npts) {
+                w.ratio[3 * base + i] = w.ry[3 * base + i] / acc;  // fitter_analytical.rs:42-47
+            }
+        }
+    }
+}
+
 // EXPERIMENT (configs[2] "superposition recast as MFMA outer product", SURVEY
 // 8d): the fit superposition with every denominator hw2 + (x - maxp)^2 taken
 // from v_mfma_f64_16x16x4_f64 as the product [x'^2, x', 1, 0] . [1, -2m', m'^2 +
@@ -4198,6 +4309,10 @@ static std::string fit_choice(const BatchArgs& a) {
     // fast alone but slower in the queue (14.8k against 15.1k spectra/s)
     return a.B == 1 ? "tw7" : a.B <= 2 ? "tf" : a.B <= 8 ? "dpp" : "plain";
 }
+bool fit_sup_dyn(const BatchArgs& a) { return fit_choice(a) == "dyn"; }
+void launch_fit_plan(const BatchArgs& a, const Workspace& w, hipStream_t st) {
+    launch_k(k_fit_plan, dim3(1), dim3(1024), 0, st, a, w);
+}
 bool fit_sup_fused(const BatchArgs& a) {
     const std::string f = fit_choice(a);
     return f == "tf" || f == "fu" || f.rfind("tw", 0) == 0;
@@ -4258,6 +4373,11 @@ const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int i
         const int g = std::max(64, std::min(1024, 2048 / a.B));
         launch_k((k_fit_sup_split<16, 128, 1024>), dim3(g, a.B), dim3(1024), 0, st, a, w, it);
         return "k_fit_sup_split<16, 128, 1024>";
+    }
+    if (f == "dyn") {
+        // persistent: 7 workgroups per CU (the SGPR-limited occupancy of the fold)
+        launch_k(k_fit_sup_dyn, dim3(256 * 7), dim3(256), 0, st, a, w, it);
+        return "k_fit_sup_dyn";
     }
     if (f == "fu") {
         // 255 points per workgroup: 25 workgroups per spectrum at P = 2048

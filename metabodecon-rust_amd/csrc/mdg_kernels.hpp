@@ -81,6 +81,11 @@ struct Workspace {
                               // (k_fit_update path: version & 1; fused k_fit_sup_tf: version % 3)
     int32_t* unsafe_kept;     // B: same for the retained Lorentzians
     int32_t* mse_done;        // B: k_mse_partial_n workgroups finished (the last one folds, resets)
+    // k_fit_sup_dyn (work-queue fit): control words (chunks per spectrum, per-XCD
+    // queue heads of two iteration slots, one progress counter per 64-point chunk)
+    // and the chunks' partial sums between the pieces of a fold
+    int32_t* fit_dyn;
+    double* fit_part;
     int32_t* peak_cnt;        // B x ceil(W/256) u64: k_peaks slots {valid, bordered, kept} per mask chunk
     // k_smooth_chain (allocated on first use; null otherwise)
     double* chain_raw;        // P x B x chain_stride: raw running sums of every pass
@@ -142,6 +147,10 @@ void launch_fit_init(const BatchArgs& a, const Workspace& w, int gx, hipStream_t
 // returns true when the launched kernel also did the stencil update (no k_fit_update)
 bool fit_sup_fused(const BatchArgs& a);
 const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st);
+// the work-queue fit (k_fit_sup_dyn) needs its plan (chunks per spectrum, zeroed
+// queue heads and chunk counters) once per pipeline, before iteration 0
+bool fit_sup_dyn(const BatchArgs& a);
+void launch_fit_plan(const BatchArgs& a, const Workspace& w, hipStream_t st);
 void launch_fit_update(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st);
 void launch_retain(const BatchArgs& a, const Workspace& w, hipStream_t st);
 // MSE partial sums per spectrum for launch_mse / launch_mse_final (<= 1024)

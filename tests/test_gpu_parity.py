@@ -376,7 +376,7 @@ def test_chain_smoother_repeated_launches(ctx, monkeypatch):
             assert np.array_equal(row, oracle.moving_average(ys[s], 3, 3)), (rep, s)
 
 
-@pytest.mark.parametrize("path", ["dpp", "split", "plain", "fu", "tf", "tw", "tw3", "tw4", "tw7", "tw9", "tw14"])
+@pytest.mark.parametrize("path", ["dpp", "split", "plain", "fu", "dyn", "tf", "tw", "tw3", "tw4", "tw7", "tw9", "tw14"])
 def test_fit_superposition_kernels(ctx, path, monkeypatch):
     """Every fit-superposition kernel (row-broadcast DPP fold, LDS split fold, one
     thread per point, term fold; chosen by MDG_FITSUP) gives the oracle's Lorentzians bit for
@@ -393,7 +393,7 @@ def test_fit_superposition_kernels(ctx, path, monkeypatch):
 
 
 
-@pytest.mark.parametrize("path", ["dpp", "split", "plain", "fu", "tf", "tw", "tw3", "tw4", "tw7", "tw9", "tw14"])
+@pytest.mark.parametrize("path", ["dpp", "split", "plain", "fu", "dyn", "tf", "tw", "tw3", "tw4", "tw7", "tw9", "tw14"])
 def test_fit_superposition_kernels_batch(ctx, path, monkeypatch):
     """The fit kernels on a batch whose spectra have different peak counts (tail
     tiles, grid-stride loops, per-spectrum range flags) against the oracle."""
