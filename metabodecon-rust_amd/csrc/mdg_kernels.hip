@@ -3047,7 +3047,11 @@ __global__ __launch_bounds__(256) void k_fit_sup_fu(BatchArgs a, Workspace w, in
 #define MDG_DYN_PIECES 4
 #endif
 constexpr int kDynPieces = MDG_DYN_PIECES;
+#ifdef MDG_DYN_DEBUG
+constexpr unsigned kDynSpins = 1u << 16;
+#else
 constexpr unsigned kDynSpins = 1u << 22;
+#endif
 
 __global__ __launch_bounds__(1024) void k_fit_plan(BatchArgs a, Workspace w) {
     __shared__ int pmax;
@@ -3105,18 +3109,26 @@ __global__ __launch_bounds__(256) void k_fit_sup_dyn(BatchArgs a, Workspace w, i
             int32_t* done = ctl + kFitDynCtl + ch;
             double acc = -0.0;
             if (k > 0) {
+                // every value the wave branches on is read into an SGPR (readfirstlane):
+                // the waits and the stores below stay wave-uniform control flow
                 const int need = it * kDynPieces + k;
                 unsigned spins = 0;
-                bool ok = true;
-                while (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+                int have = __builtin_amdgcn_readfirstlane(
+                    __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                while (have < need && spins < kDynSpins) {
                     __builtin_amdgcn_s_sleep(1);
-                    if (++spins > kDynSpins) {
-                        ok = false;
-                        break;
-                    }
+                    ++spins;
+                    have = __builtin_amdgcn_readfirstlane(
+                        __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
                 }
-                if (!ok) {  // never expected: bounds a protocol bug
-                    if (lane == 0) w.status[s] = MDG_ERR_HIP;
+                if (have < need) {  // never expected: bounds a protocol bug
+#ifdef MDG_DYN_DEBUG
+                    if (lane == 0)
+                        printf("dyn spin fail: it %d item j %d (queue %d, nx %d) k %d ch %d s %d c %d P %d need %d "
+                               "have %d CH %d block %d\n", it, j, x, nx, k, ch, s, c, P, need, have, CH,
+                               (int)blockIdx.x);
+#endif
+                    w.status[s] = MDG_ERR_HIP;
                     continue;
                 }
                 acc = __hip_atomic_load(part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3126,8 +3138,8 @@ __global__ __launch_bounds__(256) void k_fit_sup_dyn(BatchArgs a, Workspace w, i
             if (k < kDynPieces - 1) {
                 __hip_atomic_store(part, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (lane == 0)
-                    __hip_atomic_store(done, it * kDynPieces + k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                // every lane stores the same counter value: no lane-dependent branch
+                __hip_atomic_store(done, it * kDynPieces + k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else if (i < npts) {
                 w.ratio[3 * base + i] = w.ry[3 * base + i] / acc;  // fitter_analytical.rs:42-47
             }
