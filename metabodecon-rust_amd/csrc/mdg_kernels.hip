@@ -3043,10 +3043,7 @@ __global__ __launch_bounds__(256) void k_fit_sup_fu(BatchArgs a, Workspace w, in
 // ctl layout (int32): [0] chunks per spectrum; [64 + 32 * (slot * 8 + q)] queue
 // head q of iteration slot (it & 1), each on its own 128-B line; [kFitDynCtl + chunk]
 // the chunk's progress (it * K + pieces done; monotone, zeroed per pipeline).
-#ifndef MDG_DYN_PIECES
-#define MDG_DYN_PIECES 4
-#endif
-constexpr int kDynPieces = MDG_DYN_PIECES;
+constexpr int kDynPiecesDefault = 4;  // MDG_DYN_PIECES overrides (tuning)
 #ifdef MDG_DYN_DEBUG
 constexpr unsigned kDynSpins = 1u << 16;
 #else
@@ -3069,7 +3066,7 @@ __global__ __launch_bounds__(1024) void k_fit_plan(BatchArgs a, Workspace w) {
     for (int q = threadIdx.x; q < a.B * CH; q += blockDim.x) ctl[kFitDynCtl + q] = 0;
 }
 
-__global__ __launch_bounds__(256) void k_fit_sup_dyn(BatchArgs a, Workspace w, int it) {
+__global__ __launch_bounds__(256) void k_fit_sup_dyn(BatchArgs a, Workspace w, int it, int kDynPieces) {
     int32_t* ctl = w.fit_dyn;
     const int CH = ctl[0];
     const int nq = a.B * CH;
@@ -4322,6 +4319,10 @@ static std::string fit_choice(const BatchArgs& a) {
     return a.B == 1 ? "tw7" : a.B <= 2 ? "tf" : a.B <= 8 ? "dpp" : "plain";
 }
 bool fit_sup_dyn(const BatchArgs& a) { return fit_choice(a) == "dyn"; }
+static int dyn_pieces() {
+    const char* e = std::getenv("MDG_DYN_PIECES");
+    return e ? std::max(1, std::min(64, std::atoi(e))) : kDynPiecesDefault;
+}
 void launch_fit_plan(const BatchArgs& a, const Workspace& w, hipStream_t st) {
     launch_k(k_fit_plan, dim3(1), dim3(1024), 0, st, a, w);
 }
@@ -4387,8 +4388,12 @@ const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int i
         return "k_fit_sup_split<16, 128, 1024>";
     }
     if (f == "dyn") {
-        // persistent: 7 workgroups per CU (the SGPR-limited occupancy of the fold)
-        launch_k(k_fit_sup_dyn, dim3(256 * 7), dim3(256), 0, st, a, w, it);
+        // persistent: 7 workgroups per CU (the SGPR-limited occupancy of the fold);
+        // MDG_DYN_WPC / MDG_DYN_PIECES override the workgroups per CU and the pieces
+        // per fold (tuning; the pieces must not change within a pipeline run)
+        const char* e = std::getenv("MDG_DYN_WPC");
+        const int wpc = e ? std::max(1, std::min(16, std::atoi(e))) : 7;
+        launch_k(k_fit_sup_dyn, dim3(256 * wpc), dim3(256), 0, st, a, w, it, dyn_pieces());
         return "k_fit_sup_dyn";
     }
     if (f == "fu") {
