@@ -189,14 +189,16 @@ def median_rate(fn, units, reps=CPU_REPS):
     return units / statistics.median(ts), ts
 
 
-def pmc_traffic(tag, stage):
-    """HBM bytes per launch of `stage` from the newest committed PMC summary for
-    this workload tag (tools/pmc_summary.py), or (None, None)."""
+def pmc_traffic(tag, stage, kernel=None):
+    """HBM bytes per launch of `kernel` (else of `stage`) from the newest committed
+    PMC summary for this workload tag (tools/pmc_summary.py), or (None, None)."""
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{tag}.json")),
                        reverse=True):
         try:
-            return (json.load(open(path))["stages"][stage]["hbm_bytes_per_launch"],
-                    os.path.relpath(path, ROOT))
+            d = json.load(open(path))
+            if kernel in d.get("kernels", {}):
+                return d["kernels"][kernel]["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
+            return d["stages"][stage]["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
         except (OSError, KeyError, ValueError):
             continue
     return None, None
@@ -216,7 +218,7 @@ def roofline_from_stages(ctx, stages, work, tag, n):
         achieved, peak = amount / avg_s / 1e12, FP64_PEAK_TFLOPS
     else:
         achieved, peak = amount / avg_s / 1e9, HBM_PEAK_GBS
-    traffic, src = pmc_traffic(tag, dom)
+    traffic, src = pmc_traffic(tag, dom, ctx.stage_kernels().get(dom))
     limiter = {
         "smooth": ("sequential running sums (moving_average.rs:69-80): 2 dependent f64 adds "
                    "per point per pass, one CU per pass; not bandwidth-bound"),
