@@ -86,7 +86,7 @@ def test_configs2_256x131072_bit_exact():
     cap = 4096
     res = _device_batch(256, 131072, 2048, 1.0, cap)
     k = res["kernels"]
-    assert k["smooth"].startswith("k_smooth_chain<3, false>") and k["fit_superposition"] == "k_fit_sup"
+    assert k["smooth"].startswith("k_smooth_chain<3, false>") and k["fit_superposition"].startswith("k_fit_sup")
     counts = _compare(res, cap)
     assert counts.min() > 1900  # ~2k injected peaks survive selection and the fit
     res["ctx"].close()
