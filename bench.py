@@ -231,6 +231,20 @@ def roofline_from_stages(ctx, stages, work, tag, n):
          "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": src,
          "avg_launch_ms": avg_s * 1e3, "launches": launches, "algorithmic_per_launch": amount,
          "limiter": limiter}
+    if dom == "fit_superposition":
+        # the kernel's VALU issue from PMC counters at its measured clock (committed
+        # profile of k_fit_sup alone at B = 256: tools/pmc_clock.py)
+        for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_b256_fit_clock.json")),
+                           reverse=True):
+            try:
+                c = json.load(open(path))
+            except (OSError, ValueError):
+                continue
+            r["issue_pmc"] = {"kernel": c["kernel"], "batch": 256,
+                              "effective_clock_ghz": c["effective_clock_ghz"],
+                              "valu_issue_frac": c["valu_issue_frac"],
+                              "source": os.path.relpath(path, ROOT)}
+            break
     if dom == "smooth":
         # one pass is N ticks of two dependent FP64 adds on one wave; passes pipeline on
         # separate CUs, so a launch lasts about one pass (tools/ubench/eval_cost.hip floor)
