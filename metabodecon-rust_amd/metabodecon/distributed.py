@@ -33,14 +33,30 @@ def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
     return lo, lo + base + (1 if rank < rem else 0)
 
 
-def gather_tables(status, counts, mse, tables, n_total: int, group=None):
-    """All-gather one rank's block results (torch tensors, all on the collective's
-    device: CUDA for nccl, CPU for gloo) into global order on every rank.
+def _gather(out, inp, dst, group):
+    """all_gather_into_tensor, or (dst given) a gather of every rank's tensor to
+    rank ``dst`` only: one transfer per peer over its own link instead of a ring
+    through every rank. Returns the gathered tensor on the receiving ranks, else None."""
+    import torch.distributed as dist
+    if dst is None:
+        dist.all_gather_into_tensor(out, inp, group=group)
+        return out
+    if dist.get_rank(group) == dst:
+        dist.gather(inp, list(out.chunk(dist.get_world_size(group))), dst=dst, group=group)
+        return out
+    dist.gather(inp, None, dst=dst, group=group)
+    return None
+
+
+def gather_tables(status, counts, mse, tables, n_total: int, group=None, dst=None):
+    """Gather one rank's block results (torch tensors, all on the collective's
+    device: CUDA for nccl, CPU for gloo) into global order: on every rank
+    (all_gather, the default) or on rank ``dst`` only (the other ranks get None).
 
     status/counts: int32[b], mse: f64[b], tables: f64[b, w, 3] (rows past a
     spectrum's count are ignored). Returns (status, counts, mse, tables) of all
     ``n_total`` spectra, tables padded to the largest count over all ranks. Two
-    all_gathers (records, tables) and one all_reduce (the table width)."""
+    gathers (records, tables) and one all_reduce (the table width)."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
@@ -54,7 +70,7 @@ def gather_tables(status, counts, mse, tables, n_total: int, group=None):
     rec[:b, 1] = counts.to(torch.float64)
     rec[:b, 2] = mse
     all_rec = torch.empty((world * max_items, 3), dtype=torch.float64, device=dev)
-    dist.all_gather_into_tensor(all_rec, rec, group=group)
+    all_rec = _gather(all_rec, rec, dst, group)
     width = torch.tensor([int(tables.shape[1]) if b else 1], dtype=torch.int64, device=dev)
     dist.all_reduce(width, op=dist.ReduceOp.MAX, group=group)
     cap = max(int(width.item()), 1)
@@ -62,7 +78,9 @@ def gather_tables(status, counts, mse, tables, n_total: int, group=None):
     if b:
         tab[:b, : tables.shape[1]] = tables
     all_tab = torch.empty((world * max_items, cap, 3), dtype=torch.float64, device=dev)
-    dist.all_gather_into_tensor(all_tab, tab, group=group)
+    all_tab = _gather(all_tab, tab, dst, group)
+    if all_rec is None:
+        return None
     keep = torch.tensor([r * max_items + k for r, (lo, hi) in enumerate(per_rank)
                          for k in range(hi - lo)], dtype=torch.int64, device=dev)
     all_rec, all_tab = all_rec[keep], all_tab[keep]

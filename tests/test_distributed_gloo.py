@@ -130,3 +130,54 @@ def test_bench_rejects_gpus_world_mismatch():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
                         "--dry-run"], capture_output=True, text=True, timeout=120, env=env)
     assert p.returncode == 2
+
+
+def _gather_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "metabodecon-rust_amd")]
+    import torch
+    import torch.distributed as dist
+    from metabodecon.distributed import gather_tables, shard_range
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n = 7
+        lo, hi = shard_range(n, rank, world)
+        b = hi - lo
+        st = torch.tensor([10 * (lo + k) % 3 for k in range(b)], dtype=torch.int32)
+        cnt = torch.tensor([(lo + k) % 4 for k in range(b)], dtype=torch.int32)
+        mse = torch.tensor([0.5 * (lo + k) for k in range(b)], dtype=torch.float64)
+        w = 2 + rank  # ranks hold tables of different widths
+        tab = torch.arange(b * w * 3, dtype=torch.float64).reshape(b, w, 3) + 100 * rank
+        everyone = gather_tables(st, cnt, mse, tab, n)
+        root_only = gather_tables(st, cnt, mse, tab, n, dst=0)
+        if rank == 0:
+            same = all(torch.equal(a, c) for a, c in zip(everyone, root_only))
+        else:
+            same = root_only is None
+        q.put((rank, same, [t.tolist() for t in everyone[:3]]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_gather_tables_to_rank0_equals_all_gather():
+    """gather_tables(dst=0) (the bench's multi-rank gather: every peer sends to rank 0
+    over its own link) gives rank 0 exactly the all_gather result, in global order with
+    padded tables, and the other ranks None."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict((r, (same, recs)) for r, same, recs in (q.get(timeout=240) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got[0][0] and got[1][0]
+    status, counts, mse = got[0][1]
+    assert status == [10 * i % 3 for i in range(7)] and counts == [i % 4 for i in range(7)]
+    assert mse == [0.5 * i for i in range(7)]
