@@ -1,7 +1,7 @@
 #!/bin/bash
 # Full profile set for one round (GPU box): kernel traces + stats and the two PMC
 # passes (FETCH_SIZE, WRITE_SIZE; one counter per run) of
-#   q256         the headline: queue mode, 192-spectrum batches on 2 lanes
+#   q256         the headline: queue mode, 256-spectrum batches on 2 lanes
 #   b256         configs[2]: one 256-spectrum batch per step (stream mode, 1 context)
 #   b4096_n65536 configs[3] on one GPU
 # then tools/pmc_summary.py / tools/trace_summary.py turn them into profiles/.
