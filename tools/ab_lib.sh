@@ -20,10 +20,10 @@ for r in 1 2; do
   for which in base new; do
     if [ $which = base ]; then lib=(env MDGPU_LIB=$ROOT/build/libmdgpu_base.so MDGPU_ALLOW_STALE=1); else lib=(env); fi
     out=gpurun_out/ab/${which}_s20_r$r.json
-    [ "${AB_S1_ONLY:-0}" = 1 ] || timeout -k 10 180 "${lib[@]}" python bench.py --no-configs --no-cpu-baseline "$@" > $out 2> ${out%.json}.err || exit $?
+    [ "${AB_S1_ONLY:-0}" = 1 ] || timeout -k 10 180 "${lib[@]}" python bench.py --mode stream --no-configs --no-cpu-baseline "$@" > $out 2> ${out%.json}.err || exit $?
     [ "${AB_S1_ONLY:-0}" = 1 ] || summ $out "$which streams=20 r$r"
     out=gpurun_out/ab/${which}_s1_r$r.json
-    timeout -k 10 180 "${lib[@]}" python bench.py --no-configs --no-cpu-baseline --streams 1 --steps 40 "$@" > $out 2> ${out%.json}.err || exit $?
+    timeout -k 10 180 "${lib[@]}" python bench.py --mode stream --no-configs --no-cpu-baseline --streams 1 --steps 40 "$@" > $out 2> ${out%.json}.err || exit $?
     summ $out "$which streams=1 r$r"
   done
 done

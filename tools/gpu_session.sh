@@ -22,8 +22,8 @@ for step in "$@"; do
     driver) run driver_form 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     forcedist) run forcedist 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 1 --force-dist --steps 4 --warmup 1 --no-cpu-baseline ;;
     stream) run stream18 300 python bench.py --mode stream --no-configs --no-cpu-baseline ;;
-    bench64) run bench64 600 python bench.py --batch 64 --streams 1 --steps 5 --warmup 1 --no-cpu-baseline ;;
-    bench256) run bench256 600 python bench.py --batch 256 --streams 1 --steps 3 --warmup 1 --no-cpu-baseline ;;
+    bench64) run bench64 600 python bench.py --mode stream --batch 64 --streams 1 --steps 5 --warmup 1 --no-cpu-baseline ;;
+    bench256) run bench256 600 python bench.py --mode stream --batch 256 --streams 1 --steps 3 --warmup 1 --no-cpu-baseline ;;
     *) echo "unknown step $step" ;;
   esac
 done

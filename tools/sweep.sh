@@ -1,5 +1,5 @@
 #!/bin/bash
-# Parameterised headline sweep: one bench.py run per configuration, one summary line
+# Parameterised sweep of the round-2 stream mode (--mode stream): one bench.py run per configuration, one summary line
 # each. Replaces the round-2 one-off wrappers (stream_batch_sweep.sh, idle_streams.sh,
 # fit_stream_sweep.sh, ...).
 #
@@ -23,7 +23,7 @@ for cfg in "$@"; do
   i=$((i + 1))
   out=$dir/$i.json
   echo "== [$i] B=$B S=$S K=$K ${envs[*]} ${flags[*]}" >> "$dir/summary.txt"
-  timeout -k 10 240 env "${envs[@]}" python bench.py --batch "$B" --streams "$S" --steps "$K" \
+  timeout -k 10 240 env "${envs[@]}" python bench.py --mode stream --batch "$B" --streams "$S" --steps "$K" \
       --warmup 2 --no-configs --no-cpu-baseline --no-profile "${flags[@]}" > "$out" 2> "${out%.json}.err"
   rc=$?
   python - "$out" "$B" "$S" "$rc" "${envs[*]} ${flags[*]}" >> "$dir/summary.txt" <<'EOF'
