@@ -255,6 +255,11 @@ int mdg_queue_submit(mdg_queue* q, const double* d_x, const double* d_y, double 
                      int32_t* d_status);
 /* Launch the open (partial) batch. */
 int mdg_queue_flush(mdg_queue* q);
+/* Flush deadline: once the first submission of the open batch has waited `us`
+ * microseconds, a watcher thread of the queue launches the batch however full it
+ * is (0 = off, the default: batches launch when full or on flush). Bounds a
+ * submission's wait under light load; under full load batches fill first. */
+int mdg_queue_set_flush_us(mdg_queue* q, int64_t us);
 /* Flush, then wait until every submitted spectrum's outputs are written. */
 int mdg_queue_synchronize(mdg_queue* q);
 /* The engine context of lane `lane` (stage timing, kernel names; owned by the queue). */

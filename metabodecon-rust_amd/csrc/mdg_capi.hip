@@ -7,11 +7,14 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <cstdlib>
 #include <new>
 #include <vector>
@@ -1288,6 +1291,14 @@ struct mdg_queue {
     std::vector<QueueItem> open;  // the open batch
     uint64_t batches = 0, spectra = 0;
     int error = MDG_OK;  // first failure of an asynchronous batch launch (sticky)
+    // flush deadline (mdg_queue_set_flush_us): a watcher thread launches the open
+    // batch once its first submission has waited that long
+    std::chrono::steady_clock::time_point open_since{};
+    int64_t flush_us = 0;
+    bool stop = false;
+    std::condition_variable cv;
+    std::thread watcher;
+    uint64_t deadline_flushes = 0;
 };
 
 namespace {
@@ -1380,6 +1391,10 @@ int mdg_queue_submit(mdg_queue* q, const double* d_x, const double* d_y, double 
         return MDG_INVALID_ARGUMENT;
     std::lock_guard<std::mutex> g(q->mu);
     if (q->error) return q->error;
+    if (q->open.empty()) {
+        q->open_since = std::chrono::steady_clock::now();
+        if (q->flush_us > 0) q->cv.notify_one();
+    }
     q->open.push_back({d_x, d_y, sb0, sb1, (double*)d_out, (int64_t)cap, d_count, d_mse, d_status});
     if ((int)q->open.size() >= q->max_batch) {
         const int rc = queue_launch(q);
@@ -1409,6 +1424,35 @@ int mdg_queue_synchronize(mdg_queue* q) {
     return rc;
 }
 
+int mdg_queue_set_flush_us(mdg_queue* q, int64_t us) {
+    if (!q || us < 0) return MDG_INVALID_ARGUMENT;
+    std::unique_lock<std::mutex> g(q->mu);
+    q->flush_us = us;
+    if (us > 0 && !q->watcher.joinable()) {
+        q->watcher = std::thread([q] {
+            std::unique_lock<std::mutex> lk(q->mu);
+            while (!q->stop) {
+                if (q->flush_us <= 0 || q->open.empty()) {
+                    q->cv.wait(lk);
+                    continue;
+                }
+                const auto due = q->open_since + std::chrono::microseconds(q->flush_us);
+                if (std::chrono::steady_clock::now() < due) {
+                    q->cv.wait_until(lk, due);
+                    continue;
+                }
+                if (!q->error) {
+                    const int rc = queue_launch(q);  // under q->mu, like a submit's launch
+                    if (rc) q->error = rc;
+                    ++q->deadline_flushes;
+                }
+            }
+        });
+    }
+    q->cv.notify_one();
+    return MDG_OK;
+}
+
 int mdg_queue_lane(mdg_queue* q, int lane, mdg_ctx** ctx) {
     if (!q || !ctx || lane < 0 || lane >= (int)q->lanes.size()) return MDG_INVALID_ARGUMENT;
     *ctx = q->lanes[lane].ctx;
@@ -1426,6 +1470,14 @@ int mdg_queue_stats(mdg_queue* q, uint64_t* batches, uint64_t* spectra, size_t* 
 
 int mdg_queue_destroy(mdg_queue* q) {
     if (!q) return MDG_OK;
+    if (q->watcher.joinable()) {
+        {
+            std::lock_guard<std::mutex> g(q->mu);
+            q->stop = true;
+        }
+        q->cv.notify_one();
+        q->watcher.join();
+    }
     for (auto& L : q->lanes) {
         if (L.ctx) (void)mdg_ctx_synchronize(L.ctx);
         for (Buffer* b : {&L.x, &L.y, &L.sb, &L.out, &L.cnt, &L.mse, &L.st, &L.table})

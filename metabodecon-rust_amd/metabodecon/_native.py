@@ -47,7 +47,8 @@ EXPORTS = [
     "mdg_optimize_settings", "mdg_ordered_sum", "mdg_check_fast_division",
     "mdg_check_division", "mdg_division_hard_case", "mdg_ctx_stage_kernel", "mdg_ctx_get_stream",
     "mdg_synth_lorentzians_hw", "mdg_synth_batch_device_hw",
-    "mdg_queue_create", "mdg_queue_submit", "mdg_queue_flush", "mdg_queue_synchronize",
+    "mdg_queue_create", "mdg_queue_submit", "mdg_queue_flush", "mdg_queue_set_flush_us",
+    "mdg_queue_synchronize",
     "mdg_queue_lane", "mdg_queue_stats", "mdg_queue_destroy",
 ]
 
@@ -253,6 +254,7 @@ def _declare(L):
     L.mdg_queue_submit.argtypes = [_vp, _vp, _vp, ctypes.c_double, ctypes.c_double, _vp, _sz, _vp,
                                    _vp, _vp]
     L.mdg_queue_flush.argtypes = [_vp]
+    L.mdg_queue_set_flush_us.argtypes = [_vp, ctypes.c_int64]
     L.mdg_queue_synchronize.argtypes = [_vp]
     L.mdg_queue_lane.argtypes = [_vp, ctypes.c_int, ctypes.POINTER(_vp)]
     L.mdg_queue_stats.argtypes = [_vp, _u64p, _u64p, _szp]
@@ -419,6 +421,12 @@ class SpectrumQueue:
         st = lib().mdg_queue_flush(self.handle)
         if st:
             raise RuntimeError(f"mdg_queue_flush: {strerror(st)}")
+
+    def set_flush_us(self, us: int) -> None:
+        """Launch the open batch once its first submission has waited `us` µs (0: off)."""
+        st = lib().mdg_queue_set_flush_us(self.handle, int(us))
+        if st:
+            raise RuntimeError(f"mdg_queue_set_flush_us: {strerror(st)}")
 
     def synchronize(self) -> None:
         st = lib().mdg_queue_synchronize(self.handle)

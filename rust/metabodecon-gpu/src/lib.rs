@@ -217,6 +217,7 @@ pub mod ffi {
             d_status: *mut i32,
         ) -> c_int;
         pub fn mdg_queue_flush(q: *mut MdgQueue) -> c_int;
+        pub fn mdg_queue_set_flush_us(q: *mut MdgQueue, us: i64) -> c_int;
         pub fn mdg_queue_synchronize(q: *mut MdgQueue) -> c_int;
         pub fn mdg_queue_lane(q: *mut MdgQueue, lane: c_int, ctx: *mut *mut MdgCtx) -> c_int;
         pub fn mdg_queue_stats(
@@ -358,6 +359,12 @@ impl GpuSpectrumQueue {
     /// Launch the open (partial) batch.
     pub fn flush(&self) -> Result<()> {
         check(unsafe { ffi::mdg_queue_flush(self.q.as_ptr()) })
+    }
+
+    /// Launch the open batch once its first submission has waited `us`
+    /// microseconds (0: only full batches and explicit flushes launch).
+    pub fn set_flush_us(&self, us: i64) -> Result<()> {
+        check(unsafe { ffi::mdg_queue_set_flush_us(self.q.as_ptr(), us) })
     }
 
     /// Flush and wait until every submission's outputs are written.

@@ -61,6 +61,44 @@ def test_queue_blood_submissions_match_goldens():
         assert abs(float(mse[k]) - float(g["mse"])) <= MSE_RTOL * abs(float(g["mse"]))
 
 
+def test_queue_flush_deadline():
+    """With a flush deadline the queue's watcher thread launches a partial batch by
+    itself (no flush, no synchronize): 3 submissions to a 64-spectrum batch are
+    launched within the deadline, their results equal the goldens, and later
+    submissions start a new deadline."""
+    import time
+    torch = pytest.importorskip("torch")
+    names = ["blood_04", "blood_05", "blood_06", "blood_07"]
+    cases = [load_case(nm) for nm in names]
+    n = cases[0][1].size
+    X = torch.from_numpy(np.stack([c[0] for c in cases])).cuda()
+    Y = torch.from_numpy(np.stack([c[1] for c in cases])).cuda()
+    cap = n // 2 + 2
+    out, cnt, mse, st = _outputs(torch, 4, cap)
+    torch.cuda.synchronize()
+    q = nat.SpectrumQueue(0, n, 64, 2, nat.default_settings())
+    try:
+        q.set_flush_us(2000)
+        for k in range(3):
+            q.submit(X[k].data_ptr(), Y[k].data_ptr(), cases[k][2], out[k].data_ptr(), cap,
+                     cnt[k:].data_ptr(), mse[k:].data_ptr(), st[k:].data_ptr())
+        t0 = time.time()
+        while q.stats()["batches"] < 1 and time.time() - t0 < 10:
+            time.sleep(0.001)
+        assert q.stats() == {"batches": 1, "spectra": 3, "open": 0}
+        q.submit(X[3].data_ptr(), Y[3].data_ptr(), cases[3][2], out[3].data_ptr(), cap,
+                 cnt[3:].data_ptr(), mse[3:].data_ptr(), st[3:].data_ptr())
+        while q.stats()["batches"] < 2 and time.time() - t0 < 10:
+            time.sleep(0.001)
+        assert q.stats() == {"batches": 2, "spectra": 4, "open": 0}
+        q.synchronize()
+    finally:
+        q.close()
+    for k, nm in enumerate(names):
+        g = np.load(os.path.join(GOLDEN, "expected", f"{nm}.npz"))
+        assert int(st[k]) == 0 and np.array_equal(out[k, : int(cnt[k])].cpu().numpy(), g["params"])
+
+
 def test_queue_shared_axis_statuses_and_capacity():
     """A shared axis pointer (read in place), a spectrum that fails (no signal-free
     peaks: its status, count 0), and a submission whose own capacity is below its
