@@ -401,7 +401,9 @@ class Deconvoluter:
     # GPU_MAX_HW_QUEUES hardware queues (4 unless set) and two busy streams on one
     # queue serialise, so the lanes stay below it (one queue is left for the
     # caller's own stream); with the default 4 queues that is 3 lanes.
-    LANES = max(1, min(16, int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) - 1))
+    # (MDGPU_LANES overrides the count, still capped by the queues)
+    LANES = max(1, min(16, int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) - 1,
+                       int(os.environ.get("MDGPU_LANES", "16") or 16)))
 
     def _run_batch(self, ctx, spectra: list[Spectrum], idx: list[int], n: int, ign):
         b = len(idx)
