@@ -394,16 +394,19 @@ class Deconvoluter:
         return np.array(self._ignore, dtype=np.float64).reshape(-1)
 
     # Engine contexts (own HIP stream and workspace each) a call spreads its spectra
-    # over: a set of one length is cut into that many contiguous chunks (one
-    # spectrum each when the set is that small), each chunk one batched pipeline on
-    # its own lane, all lanes concurrently: each chunk's sequential smoother overlaps
-    # the others' fits. HIP maps streams round-robin onto
-    # GPU_MAX_HW_QUEUES hardware queues (4 unless set) and two busy streams on one
-    # queue serialise, so the lanes stay below it (one queue is left for the
-    # caller's own stream); with the default 4 queues that is 3 lanes.
-    # (MDGPU_LANES overrides the count, still capped by the queues)
+    # over, concurrently: a set of one length is cut into contiguous chunks (at least
+    # one per lane, at most CHUNK spectra each), dealt round-robin to the lanes, each
+    # chunk one batched pipeline; each lane's sequential smoother overlaps the other
+    # lane's fit. Two lanes measured best for the 16 blood spectra under both HIP's
+    # default 4 hardware queues and 32 (tools/c4_lanes.sh: 2.65-2.72 ms per set
+    # against 3.3-4.3 with 3-4 lanes, 3.9 with 16 lanes of one spectrum, 9.3-9.9 with
+    # one batch of 16, whose B > 8 fit leaves the chip mostly idle). HIP maps streams
+    # round-robin onto GPU_MAX_HW_QUEUES hardware queues and two busy streams on one
+    # queue serialise, so the lanes also stay below that count (one queue is left
+    # for the caller's own stream). MDGPU_LANES overrides the count.
     LANES = max(1, min(16, int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) - 1,
-                       int(os.environ.get("MDGPU_LANES", "16") or 16)))
+                       int(os.environ.get("MDGPU_LANES", "2") or 2)))
+    CHUNK = 256  # spectra per batched call (the host staging of one call stays bounded)
 
     def _run_batch(self, ctx, spectra: list[Spectrum], idx: list[int], n: int, ign):
         b = len(idx)
@@ -428,8 +431,9 @@ class Deconvoluter:
 
     def _run(self, spectra: list[Spectrum]) -> list[tuple[int, np.ndarray, float]]:
         """GPU results per spectrum, (status, params, mse) in input order: the
-        spectra of one length are cut into min(LANES, count) contiguous chunks that
-        run concurrently, one batched pipeline per lane context."""
+        spectra of one length are cut into contiguous chunks (at least one per lane,
+        at most CHUNK spectra), dealt round-robin to min(LANES, count) lane contexts
+        that run concurrently, one batched pipeline per chunk."""
         results: list = [None] * len(spectra)
         by_n: dict[int, list[int]] = {}
         for i, sp in enumerate(spectra):
@@ -437,22 +441,28 @@ class Deconvoluter:
                 raise TypeError("expected metabodecon.Spectrum")
             by_n.setdefault(len(sp), []).append(i)
         ign = self._ignore_array()
+        from .distributed import shard_range
         for n, idx in by_n.items():
-            k = min(self.LANES, len(idx))
-            if k <= 1:
-                res = self._run_batch(nat.context(self.device), spectra, idx, n, ign)
-                for i, r in zip(idx, res):
-                    results[i] = r
-                continue
-            from .distributed import shard_range
+            lanes_n = min(self.LANES, len(idx))
+            k = max(lanes_n, -(-len(idx) // self.CHUNK))
             chunks = [idx[lo:hi] for lo, hi in (shard_range(len(idx), r, k) for r in range(k))]
-            lanes = nat.lane_contexts(self.device, k)
+            if lanes_n <= 1:
+                for c in chunks:
+                    for i, r in zip(c, self._run_batch(nat.context(self.device), spectra, c, n, ign)):
+                        results[i] = r
+                continue
+            lanes = nat.lane_contexts(self.device, lanes_n)
             pool = _lane_pool(self.LANES)
-            futs = [pool.submit(self._run_batch, lanes[j], spectra, c, n, ign)
-                    for j, c in enumerate(chunks)]
-            for c, f in zip(chunks, futs):
-                for i, r in zip(c, f.result()):
-                    results[i] = r
+
+            def lane_work(j):  # lane j runs chunks j, j + lanes_n, ... one after another
+                out = []
+                for c in chunks[j::lanes_n]:
+                    out.append((c, self._run_batch(lanes[j], spectra, c, n, ign)))
+                return out
+            for f in [pool.submit(lane_work, j) for j in range(lanes_n)]:
+                for c, res in f.result():
+                    for i, r in zip(c, res):
+                        results[i] = r
         return results
 
     def _run_device(self, spectra: list[Spectrum]):

@@ -123,6 +123,22 @@ def test_concurrent_lanes_and_release(monkeypatch):
         assert not nat._lanes
 
 
+def test_chunked_lanes_bit_exact(monkeypatch):
+    """A set larger than a chunk: the 16 blood spectra in chunks of at most 3 (6
+    chunks) dealt round-robin to 2 lanes, each lane running its chunks one after
+    another; every result equals the golden."""
+    import metabodecon as md
+    monkeypatch.setattr(md.Deconvoluter, "LANES", 2)
+    monkeypatch.setattr(md.Deconvoluter, "CHUNK", 3)
+    spectra = md.Spectrum.read_bruker_set(os.path.join(GOLDEN, "bruker", "blood"), 10, 10,
+                                          (-2.2, 11.8))
+    decs = md.Deconvoluter().par_deconvolute_spectra(spectra)
+    for k, d in enumerate(decs):
+        g = np.load(os.path.join(GOLDEN, "expected", f"blood_{k + 1:02d}.npz"))
+        assert np.array_equal(d.params, g["params"]), k
+        assert abs(d.mse - float(g["mse"])) <= MSE_RTOL * abs(float(g["mse"]))
+
+
 def test_python_api_end_to_end():
     import metabodecon as md
     spectra = md.Spectrum.read_bruker_set(os.path.join(GOLDEN, "bruker", "blood"), 10, 10,
