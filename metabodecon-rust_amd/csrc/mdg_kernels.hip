@@ -3933,16 +3933,24 @@ __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int
                     const double sg = __builtin_sqrt(h);
                     const double isg = rcp_nr2(sg);
                     const double fq = f * id2;
-                    double cr = fq * (dm * isg), ci = -fq;
+                    const double cr = fq * (dm * isg), ci = -fq;
                     const double rq = rt * id2;
                     const double qr = rq * dm, qi = -(rq * sg);
+                    // y_k = Im(c q^k) by the real recurrence y_{k+2} = 2 Re(q) y_{k+1}
+                    // - |q|^2 y_k (roots q and conj(q), one modulus < 1/kLocR: an error
+                    // decays like the terms themselves; tools/mse_local_error.py 'rec'
+                    // matches the complex product to the last digit): 3 instructions
+                    // per power instead of the complex product's 5
+                    const double a2 = 2.0 * qr, b = __builtin_fma(qr, qr, qi * qi);
+                    double y0 = ci, y1 = __builtin_fma(cr, qi, ci * qr);
+                    L[0] += y0;
+                    L[1] += y1;
 #pragma unroll
-                    for (int k = 0; k < PK; ++k) {
-                        L[k] += ci;
-                        const double nr_ = __builtin_fma(cr, qr, -(ci * qi));
-                        const double ni_ = __builtin_fma(cr, qi, ci * qr);
-                        cr = nr_;
-                        ci = ni_;
+                    for (int k = 2; k < PK; ++k) {
+                        const double y2 = __builtin_fma(a2, y1, -(b * y0));
+                        L[k] += y2;
+                        y0 = y1;
+                        y1 = y2;
                     }
                 }
                 const uint64_t bal = __ballot(nr);

@@ -17,9 +17,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "metabodecon-rust_amd"), os.path.join(ROOT, "tests", "golden")]
 
 
-def local_sup(xs, P, TP=256, R=5.0, p=20):
+def local_sup(xs, P, TP=256, R=5.0, p=20, rec=False):
     """The kernel's arithmetic per tile: near Lorentzians direct, far ones as the
-    imaginary parts of -sum_k [sum_j a_j w_j (r w_j)^k] u^k."""
+    imaginary parts of -sum_k [sum_j a_j w_j (r w_j)^k] u^k. rec: the imaginary
+    parts y_k = Im(c q^k) by the real second-order recurrence
+    y_{k+2} = 2 Re(q) y_{k+1} - |q|^2 y_k (the roots q, conj(q) have one modulus,
+    so an error decays like the terms themselves)."""
     f, h, m = P[:, 0], P[:, 1], P[:, 2]
     sig = np.sqrt(h)
     a = f / sig
@@ -33,9 +36,18 @@ def local_sup(xs, P, TP=256, R=5.0, p=20):
         w = 1.0 / dz[far]
         c, q = a[far] * w, r * w
         L = np.zeros(p)
-        for k in range(p):
-            L[k] = -np.sum(c.imag)
-            c = c * q
+        if rec:
+            y0 = c.imag
+            y1 = c.real * q.imag + c.imag * q.real
+            a2, b = 2.0 * q.real, q.real * q.real + q.imag * q.imag
+            L[0], L[1] = -np.sum(y0), -np.sum(y1)
+            for k in range(2, p):
+                y0, y1 = y1, a2 * y1 - b * y0
+                L[k] = -np.sum(y1)
+        else:
+            for k in range(p):
+                L[k] = -np.sum(c.imag)
+                c = c * q
         u = (xt - t) / r if r > 0 else np.zeros_like(xt)
         S = np.zeros(xt.size)
         for k in range(p - 1, -1, -1):
@@ -61,16 +73,19 @@ def report(name, xs, ys, P, shapes):
     mref = float(np.mean((ref - ys) ** 2))
     d64 = direct(xs, P, np.float64)
     print(f"{name}: P={P.shape[0]} L={xs.size}  direct f64: MSE rel {float(np.mean((d64 - ys) ** 2)) / mref - 1:+.2e}")
-    for TP, R, p in shapes:
-        s = local_sup(xs, P, TP, R, p)
+    for TP, R, p, *rest in shapes:
+        rec = bool(rest and rest[0])
+        s = local_sup(xs, P, TP, R, p, rec)
         e = float(np.max(np.abs((s - ref) / ref)))
-        print(f"   tile {TP} R={R} terms {p}: sup rel {e:.2e}  MSE rel {float(np.mean((s - ys) ** 2)) / mref - 1:+.2e}")
+        print(f"   tile {TP} R={R} terms {p}{' rec' if rec else ''}: sup rel {e:.2e}  "
+              f"MSE rel {float(np.mean((s - ys) ** 2)) / mref - 1:+.2e}")
 
 
 def main():
     from cases import load_case, synth_spectrum
     import oracle
-    shapes = [(256, 5.0, 20), (256, 5.0, 16), (256, 4.0, 20), (128, 5.0, 20)]
+    shapes = [(256, 5.0, 20), (256, 5.0, 20, True), (512, 5.0, 20), (512, 5.0, 20, True),
+              (512, 4.0, 24, True)]
     names = sys.argv[1:] or ["blood_01", "blood_05", "blood_09", "sim_01", "synth"]
     for nm in names:
         if nm == "synth":
