@@ -3819,9 +3819,11 @@ __device__ __forceinline__ double sup_retained_direct(double x, const_f64_ptr pr
     return acc;
 }
 
+// NPT points per thread: a tile of kLocTP * NPT points shares one coefficient pass
+template <int NPT>
 __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int nparts, int near_cap) {
-    constexpr int BS = 256, NW = BS / 64, TP = kLocTP, PK = kLocP, PH = PK / 2;
-    static_assert(TP == BS && PK % 2 == 0 && PH * 16 <= BS, "tile shape");
+    constexpr int BS = 256, NW = BS / 64, TP = kLocTP * NPT, PK = kLocP, PH = PK / 2;
+    static_assert(kLocTP == BS && PK % 2 == 0 && PH * 16 <= BS, "tile shape");
     const int s = blockIdx.x % a.B, part = blockIdx.x / a.B;
     // LDS: the coefficient reduction (PH x BS) and, after the tile loop, the
     // partials of the final fold share one buffer
@@ -3876,16 +3878,27 @@ __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int
     const bool fast = w.x_ok[s] && !__syncthreads_or(uns);
     double acc = 0.0;
     for (int64_t v0 = (int64_t)part * TP; v0 < total; v0 += (int64_t)nparts * TP) {
-        const int64_t v = v0 + tid;
-        const bool ok = v < total;
-        const int64_t idx = mse_index(w, s, nig, ok ? v : 0);
-        const double xv = x[idx], yv = y[idx];
-        double sup;
+        double xv[NPT], yv[NPT], sup[NPT];
+        bool ok[NPT];
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) {  // point v0 + tid + i * BS: lanes stay consecutive
+            const int64_t v = v0 + tid + (int64_t)i * BS;
+            ok[i] = v < total;
+            const int64_t idx = mse_index(w, s, nig, ok[i] ? v : 0);
+            xv[i] = x[idx];
+            yv[i] = y[idx];
+        }
         if (!fast) {
-            sup = sup_retained_direct<false>(xv, prm, P);
+#pragma unroll
+            for (int i = 0; i < NPT; ++i) sup[i] = sup_retained_direct<false>(xv[i], prm, P);
         } else {
             // tile centre and half range over its valid points
-            double lo = ok ? xv : INFINITY, hi = ok ? xv : -INFINITY;
+            double lo = INFINITY, hi = -INFINITY;
+#pragma unroll
+            for (int i = 0; i < NPT; ++i) {
+                lo = ok[i] ? fmin(lo, xv[i]) : lo;
+                hi = ok[i] ? fmax(hi, xv[i]) : hi;
+            }
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) {
                 lo = fmin(lo, __shfl_xor(lo, o, 64));
@@ -3992,28 +4005,41 @@ __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int
                 __syncthreads();
             }
             if (nnear > near_cap) {
-                sup = sup_retained_direct<true>(xv, prm, P);
-            } else {
-                const double u = rt > 0.0 ? (xv - t) / rt : 0.0;
-                double S = coef[PK - 1];
 #pragma unroll
-                for (int k = PK - 2; k >= 0; --k) S = __builtin_fma(S, u, coef[k]);
+                for (int i = 0; i < NPT; ++i) sup[i] = sup_retained_direct<true>(xv[i], prm, P);
+            } else {
+                double nsum[NPT];
+#pragma unroll
+                for (int i = 0; i < NPT; ++i) {
+                    const double u = rt > 0.0 ? (xv[i] - t) / rt : 0.0;
+                    double S = coef[PK - 1];
+#pragma unroll
+                    for (int k = PK - 2; k >= 0; --k) S = __builtin_fma(S, u, coef[k]);
+                    sup[i] = S;
+                    nsum[i] = 0.0;
+                }
                 // near Lorentzians: four per division (quad_term), the rest one by one
-                double nsum = 0.0;
                 int j = 0;
                 for (; j + 4 <= nnear; j += 4) {
                     double c[12];
 #pragma unroll
                     for (int k = 0; k < 12; ++k) c[k] = nearp[3 * j + k];
-                    nsum += quad_term(xv, c);
+#pragma unroll
+                    for (int i = 0; i < NPT; ++i) nsum[i] += quad_term(xv[i], c);
                 }
                 for (; j < nnear; ++j)
-                    nsum += lorentz_mse<true>(xv, nearp[3 * j], nearp[3 * j + 1], nearp[3 * j + 2]);
-                sup = nsum + S;
+#pragma unroll
+                    for (int i = 0; i < NPT; ++i)
+                        nsum[i] += lorentz_mse<true>(xv[i], nearp[3 * j], nearp[3 * j + 1], nearp[3 * j + 2]);
+#pragma unroll
+                for (int i = 0; i < NPT; ++i) sup[i] = nsum[i] + sup[i];
             }
         }
-        const double d = sup - yv;
-        if (ok) acc += d * d;
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) {
+            const double d = sup[i] - yv[i];
+            if (ok[i]) acc += d * d;
+        }
         __syncthreads();  // LDS reuse by the next tile
     }
 #pragma unroll
@@ -4435,10 +4461,17 @@ static int mse_quad_npt(const BatchArgs& a) {
 }
 // k_mse_local compacts the retained Lorentzians itself (no k_retain launch)
 bool mse_fuses_retain() { return mse_kind() == "local"; }
+// k_mse_local points per thread: tiles of 256 (1) or 512 (2) points (MDG_MSE_NPT)
+static int mse_local_npt() {
+    const char* e = std::getenv("MDG_MSE_NPT");
+    return (e && std::atoi(e) == 2) ? 2 : 1;
+}
 int mse_nparts(const BatchArgs& a) {
     const std::string k = mse_kind();
-    if (k == "local")
-        return std::max(1, std::min({kMseMaxParts, (a.N + kLocTP - 1) / kLocTP, std::max(1, 8192 / a.B)}));
+    if (k == "local") {
+        const int tp = kLocTP * mse_local_npt();
+        return std::max(1, std::min({kMseMaxParts, (a.N + tp - 1) / tp, std::max(1, 8192 / a.B)}));
+    }
     if (k == "quad") {
         // one workgroup per 64 * NPT points (its four waves split the Lorentzians)
         const int pts = 64 * mse_quad_npt(a);
@@ -4454,8 +4487,12 @@ const char* launch_mse(const BatchArgs& a, const Workspace& w, int nparts, hipSt
         int cap = kLocNear;
         if (const char* e = std::getenv("MDG_MSE_NEARCAP")) cap = std::max(0, std::min(kLocNear, std::atoi(e)));
         // nparts tile workgroups per spectrum plus its retain workgroup
-        launch_k(k_mse_local, dim3((nparts + 1) * a.B), dim3(256), 0, st, a, w, nparts, cap);
-        return "k_mse_local";
+        if (mse_local_npt() == 2) {
+            launch_k(k_mse_local<2>, dim3((nparts + 1) * a.B), dim3(256), 0, st, a, w, nparts, cap);
+            return "k_mse_local<2>";
+        }
+        launch_k(k_mse_local<1>, dim3((nparts + 1) * a.B), dim3(256), 0, st, a, w, nparts, cap);
+        return "k_mse_local<1>";
     }
     if (mse_kind() == "quad") {
         if (mse_quad_npt(a) == 2) {

@@ -428,12 +428,16 @@ def test_fit_superposition_kernels_batch(ctx, path, monkeypatch):
 
 
 @pytest.mark.parametrize("kernel,near_cap", [("local", None), ("local", "8"), ("local", "0"),
+                                             ("local2", None), ("local2", "8"),
                                              ("quad", None), ("n", None), ("plain", None)])
 def test_mse_cases(ctx, kernel, near_cap, monkeypatch):
     """The MSE against the oracle: ignore regions (two in one spectrum), a short
     signal region (sim) and a batch whose spectra differ in peak count -- on every
     MSE kernel; for k_mse_local also with a tiny near-list capacity (crowded tiles
     take the direct sum) and none at all (every tile direct)."""
+    if kernel == "local2":  # k_mse_local with 512-point tiles (two points per thread)
+        monkeypatch.setenv("MDG_MSE_NPT", "2")
+        kernel = "local"
     monkeypatch.setenv("MDG_MSE", kernel)
     if near_cap is not None:
         monkeypatch.setenv("MDG_MSE_NEARCAP", near_cap)
@@ -609,7 +613,7 @@ def test_graph_key_follows_kernel_overrides(monkeypatch):
         assert np.array_equal(out[0, : int(cnt[0])].cpu().numpy(), o.params)
         assert abs(float(mse[0]) - o.mse) <= MSE_RTOL * abs(o.mse)
     c.close()
-    assert seen[0][0] == "k_mse_local" and seen[1][0].startswith("k_mse_quad")
+    assert seen[0][0].startswith("k_mse_local") and seen[1][0].startswith("k_mse_quad")
     assert seen[2][1] == "k_fit_sup_dpp" and seen[3] == seen[0]
 
 
