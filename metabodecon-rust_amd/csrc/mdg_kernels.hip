@@ -4461,10 +4461,13 @@ static int mse_quad_npt(const BatchArgs& a) {
 }
 // k_mse_local compacts the retained Lorentzians itself (no k_retain launch)
 bool mse_fuses_retain() { return mse_kind() == "local"; }
-// k_mse_local points per thread: tiles of 256 (1) or 512 (2) points (MDG_MSE_NPT)
+// k_mse_local points per thread: tiles of 512 (2, default) or 256 (1) points
+// (MDG_MSE_NPT). Measured in the queue (256 x 2): MSE 3.83-3.86 against 5.05-5.14 us
+// per spectrum, 15.27-15.39k against 15.03-15.07k spectra/s; the far-field pass is
+// shared by twice the points while the near list grows (tools/gpu_s9.sh)
 static int mse_local_npt() {
     const char* e = std::getenv("MDG_MSE_NPT");
-    return (e && std::atoi(e) == 2) ? 2 : 1;
+    return (e && std::atoi(e) == 1) ? 1 : 2;
 }
 int mse_nparts(const BatchArgs& a) {
     const std::string k = mse_kind();

@@ -428,15 +428,15 @@ def test_fit_superposition_kernels_batch(ctx, path, monkeypatch):
 
 
 @pytest.mark.parametrize("kernel,near_cap", [("local", None), ("local", "8"), ("local", "0"),
-                                             ("local2", None), ("local2", "8"),
+                                             ("local1", None), ("local1", "8"),
                                              ("quad", None), ("n", None), ("plain", None)])
 def test_mse_cases(ctx, kernel, near_cap, monkeypatch):
     """The MSE against the oracle: ignore regions (two in one spectrum), a short
     signal region (sim) and a batch whose spectra differ in peak count -- on every
     MSE kernel; for k_mse_local also with a tiny near-list capacity (crowded tiles
     take the direct sum) and none at all (every tile direct)."""
-    if kernel == "local2":  # k_mse_local with 512-point tiles (two points per thread)
-        monkeypatch.setenv("MDG_MSE_NPT", "2")
+    if kernel == "local1":  # k_mse_local with 256-point tiles (one point per thread)
+        monkeypatch.setenv("MDG_MSE_NPT", "1")
         kernel = "local"
     monkeypatch.setenv("MDG_MSE", kernel)
     if near_cap is not None:
