@@ -27,8 +27,9 @@ def main():
         x, y, _ = synth_spectrum(seed)
         o = oracle.deconvolute(x, y, (11.8, -2.2), threads=16)
         cases.append((f"synth_{seed}", x, y, (11.8, -2.2), oracle.default_settings(), (), o.mse))
-    for kind in ("local", "quad", "n", "plain"):
-        os.environ["MDG_MSE"] = kind
+    for kind in ("local", "local1", "quad", "n", "plain"):
+        os.environ["MDG_MSE"] = "local" if kind.startswith("local") else kind
+        os.environ["MDG_MSE_NPT"] = "1" if kind == "local1" else "2"
         worst, wname = 0.0, None
         for name, x, y, sb, st, ign, ref in cases:
             status, counts, out, mse = gpu_batch(ctx, x, y[None, :], [sb], st, ign)
