@@ -99,6 +99,51 @@ def test_queue_flush_deadline():
         assert int(st[k]) == 0 and np.array_equal(out[k, : int(cnt[k])].cpu().numpy(), g["params"])
 
 
+def test_queue_concurrent_submitters():
+    """mdg_queue_submit is thread-safe: four host threads submit interleaved (ctypes
+    drops the GIL in the call) into batches of 7 on 2 lanes, with a flush deadline
+    running beside them; every one of the 48 results equals its golden."""
+    import threading
+    torch = pytest.importorskip("torch")
+    names = [f"blood_{i:02d}" for i in range(1, 17)]
+    cases = [load_case(nm) for nm in names]
+    n = cases[0][1].size
+    X = torch.from_numpy(np.stack([c[0] for c in cases])).cuda()
+    Y = torch.from_numpy(np.stack([c[1] for c in cases])).cuda()
+    cap = n // 2 + 2
+    K = 48
+    out, cnt, mse, st = _outputs(torch, K, cap)
+    torch.cuda.synchronize()
+    q = nat.SpectrumQueue(0, n, 7, 2, nat.default_settings())
+    errors = []
+
+    def worker(t):
+        try:
+            for k in range(t, K, 4):
+                i = k % 16
+                q.submit(X[i].data_ptr(), Y[i].data_ptr(), cases[i][2], out[k].data_ptr(), cap,
+                         cnt[k:].data_ptr(), mse[k:].data_ptr(), st[k:].data_ptr())
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(e)
+
+    try:
+        q.set_flush_us(500)
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        q.synchronize()
+        assert not errors, errors
+        assert q.stats()["spectra"] == K
+    finally:
+        q.close()
+    for k in range(K):
+        g = np.load(os.path.join(GOLDEN, "expected", f"{names[k % 16]}.npz"))
+        assert int(st[k]) == 0 and np.array_equal(out[k, : int(cnt[k])].cpu().numpy(), g["params"]), k
+        assert abs(float(mse[k]) - float(g["mse"])) <= MSE_RTOL * abs(float(g["mse"]))
+
+
 def test_queue_shared_axis_statuses_and_capacity():
     """A shared axis pointer (read in place), a spectrum that fails (no signal-free
     peaks: its status, count 0), and a submission whose own capacity is below its
