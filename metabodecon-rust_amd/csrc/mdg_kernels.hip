@@ -4368,7 +4368,9 @@ const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int i
     const std::string f = fit_choice(a);
     if (f.rfind("tw", 0) == 0) {
         // 63 points per workgroup: 98 workgroups at P = 2048, grid-stride beyond
-        const int g = std::max(2, 128 / a.B);
+        // MDG_TW_G (tuning): workgroups per spectrum (tiles beyond them grid-stride)
+        const char* tg = std::getenv("MDG_TW_G");
+        const int g = tg ? std::max(1, std::atoi(tg)) : std::max(2, 128 / a.B);
         if (f == "tw4") {  // 4 evaluator waves: 2 peak blocks x 2 point subsets (Q = 60)
             using SH = TwShape<60, 2, 2>;
             launch_k(k_fit_sup_tw<SH>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
@@ -4400,7 +4402,8 @@ const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int i
     }
     if (f == "tf") {
         // 24 points per workgroup: 256 workgroups at P = 2048, grid-stride beyond
-        const int g = std::max(2, 256 / a.B);
+        const char* tg = std::getenv("MDG_TW_G");
+        const int g = tg ? std::max(1, std::atoi(tg)) : std::max(2, 256 / a.B);
         launch_k(k_fit_sup_tf, dim3(g, a.B), dim3(64 * (kTfEW + 1)), 0, st, a, w, it);
         return "k_fit_sup_tf";
     } else if (f == "dpp") {
