@@ -4348,9 +4348,15 @@ void launch_fit_init(const BatchArgs& a, const Workspace& w, int gx, hipStream_t
 static std::string fit_choice(const BatchArgs& a) {
     const char* force = std::getenv("MDG_FITSUP");
     if (force && *force) return force;
-    // B > 8: k_fit_sup + k_fit_update ("plain"); the fused k_fit_sup_fu ("fu") is as
-    // fast alone but slower in the queue (14.8k against 15.1k spectra/s)
-    return a.B == 1 ? "tw7" : a.B <= 2 ? "tf" : a.B <= 8 ? "dpp" : "plain";
+    // By batch size, fit time per spectrum alone (tools/fit_by_batch2.sh):
+    // B <= 2 the 24-point term fold over one workgroup per tile ("tf": 214 / 149 us
+    // at B = 1 / 2, latency 0.88 ms at B = 1 against 0.95 for "tw7", the round-2
+    // choice for 18 concurrent B = 1 streams); B <= 24 the 63-point term fold over
+    // one workgroup per tile ("tw7": 120 / 113 / 93 us at B = 4 / 8 / 16 against 167 /
+    // 187 / 118 for "dpp" / "dpp" / "plain"); beyond, one point per lane with the
+    // update separate ("plain": 79 / 57 us at B = 32 / 256). The fused k_fit_sup_fu
+    // ("fu") is as fast as "plain" alone but slower in the queue.
+    return a.B <= 2 ? "tf" : a.B <= 24 ? "tw7" : "plain";
 }
 bool fit_sup_dyn(const BatchArgs& a) { return fit_choice(a) == "dyn"; }
 static int dyn_pieces() {
@@ -4369,8 +4375,11 @@ const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int i
     if (f.rfind("tw", 0) == 0) {
         // 63 points per workgroup: 98 workgroups at P = 2048, grid-stride beyond
         // MDG_TW_G (tuning): workgroups per spectrum (tiles beyond them grid-stride)
+        // one workgroup per 63-point tile of a 2048-peak spectrum (98; more tiles
+        // grid-stride): every spectrum of a small batch spreads over the CUs.
+        // (Round 2 used max(2, 128 / B) for 18 concurrent B = 1 streams.)
         const char* tg = std::getenv("MDG_TW_G");
-        const int g = tg ? std::max(1, std::atoi(tg)) : std::max(2, 128 / a.B);
+        const int g = tg ? std::max(1, std::atoi(tg)) : (3 * 2048 + 62) / 63;
         if (f == "tw4") {  // 4 evaluator waves: 2 peak blocks x 2 point subsets (Q = 60)
             using SH = TwShape<60, 2, 2>;
             launch_k(k_fit_sup_tw<SH>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
@@ -4402,8 +4411,9 @@ const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int i
     }
     if (f == "tf") {
         // 24 points per workgroup: 256 workgroups at P = 2048, grid-stride beyond
+        // one workgroup per 24-point tile of a 2048-peak spectrum (256)
         const char* tg = std::getenv("MDG_TW_G");
-        const int g = tg ? std::max(1, std::atoi(tg)) : std::max(2, 256 / a.B);
+        const int g = tg ? std::max(1, std::atoi(tg)) : (3 * 2048 + 23) / 24;
         launch_k(k_fit_sup_tf, dim3(g, a.B), dim3(64 * (kTfEW + 1)), 0, st, a, w, it);
         return "k_fit_sup_tf";
     } else if (f == "dpp") {
