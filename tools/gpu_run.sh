@@ -1,0 +1,49 @@
+#!/bin/bash
+# One GPU session of fixed steps (GPU box). Every step runs under its own time limit;
+# the session stops at the first GPU fault, abort or timeout (exit codes other than
+# 0/1; a plain test failure, 1, does not stop it). Logs: gpurun_out/run/<step>.log.
+#
+# Usage: bash tools/gpu_run.sh <step> ...
+#   smoke        __graft_entry__.smoke()
+#   tests        pytest -m gpu, stop at the first failure
+#   tests_all    pytest -m gpu, every test
+#   tests:<expr> pytest -m gpu -k <expr>
+#   driver       bench.py as the driver runs it (--gpus 1 --steps 20 --warmup 5)
+#   default      bench.py with no arguments
+#   forcedist    bench.py under torch.distributed.run at world 1 (RCCL gather, configs_dist)
+#   prof         the round's profile set (tools/prof_all.sh)
+#   c4           configs[4] by lanes and hardware queues (bench.py --c4-only)
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out/run
+log=gpurun_out/run/session.log
+run() {  # run <name> <timeout> <cmd...>
+  local name=$1 t=$2; shift 2
+  echo "== $name: $*" | tee -a $log
+  timeout -k 10 "$t" "$@" > "gpurun_out/run/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" | tee -a $log
+  tail -4 "gpurun_out/run/$name.log" | cut -c1-600 | tee -a $log
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP after $name (rc=$rc)" | tee -a $log; exit $rc; fi
+  return 0
+}
+PYT=(python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread)
+for step in "$@"; do
+  case "$step" in
+    smoke) run smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) run pytest_gpu 1200 "${PYT[@]}" -x ;;
+    tests_all) run pytest_gpu 1200 "${PYT[@]}" ;;
+    tests:*) run pytest_k 1200 "${PYT[@]}" -x -k "${step#tests:}" ;;
+    driver) run driver_form 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    default) run default 600 python bench.py ;;
+    forcedist) run forcedist 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+        --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 1 --force-dist --steps 4 --warmup 1 --no-cpu-baseline ;;
+    prof) run prof_all 1200 bash tools/prof_all.sh ;;
+    c4)
+      cfgs=()
+      for q in 4 32; do for l in 1 2 3 4 8 16; do
+        [ $l -ge $q ] || cfgs+=("q${q}_l$l GPU_MAX_HW_QUEUES=$q MDGPU_LANES=$l --c4-only")
+      done; done
+      run c4 1200 bash tools/ab.sh c4 "${cfgs[@]}" ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
