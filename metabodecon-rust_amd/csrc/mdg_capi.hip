@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
@@ -49,6 +50,7 @@ struct mdg_ctx {
     int device = 0;
     hipStream_t own = nullptr;
     hipStream_t stream = nullptr;
+    bool counted = false;  // in g_live_ctx (has run a pipeline)
     std::mutex mu;
     // workspace arena
     Buffer arena;
@@ -430,6 +432,13 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
 // uploaded only when the regions differ from the ones it holds (the usual caller
 // passes the same Deconvoluter's regions every call): no host-to-device copy, and
 // no pageable-copy stall, in a stream of calls.
+// Engine contexts per device that have run a pipeline (and are not destroyed):
+// the B = 1 fit kernel differs when the spectrum is likely to have the GPU to
+// itself (fit_choice). A context counts from its first pipeline on,
+// so the idle lanes of a Deconvoluter do not.
+constexpr int kMaxDevices = 64;
+static std::atomic<int> g_live_ctx[kMaxDevices];
+
 int fill_args(mdg_ctx* c, BatchArgs& a, size_t b, size_t n, const double* x, size_t xs, const double* y,
               size_t ys, const double* sb, const double* ignore, size_t n_ignore, double* out,
               size_t cap, int32_t* cnt, double* mse, int32_t* status) {
@@ -442,6 +451,11 @@ int fill_args(mdg_ctx* c, BatchArgs& a, size_t b, size_t n, const double* x, siz
     a.y_stride = (int64_t)ys;
     a.sb = sb;
     a.n_ignore = (int)n_ignore;
+    if (!c->counted && c->device < kMaxDevices) {
+        c->counted = true;
+        g_live_ctx[c->device].fetch_add(1);
+    }
+    a.contexts = c->counted ? g_live_ctx[c->device].load() : 2;
     a.ignore = nullptr;
     if (n_ignore > 0) {
         const size_t cnt = 2 * n_ignore;
@@ -659,6 +673,7 @@ int mdg_ctx_destroy(mdg_ctx* c) {
             if (b->p) (void)hipFree(b->p);
         if (c->own) (void)hipStreamDestroy(c->own);
     }
+    if (c->counted) g_live_ctx[c->device].fetch_sub(1);
     delete c;
     return MDG_OK;
 }

@@ -4348,14 +4348,18 @@ void launch_fit_init(const BatchArgs& a, const Workspace& w, int gx, hipStream_t
 static std::string fit_choice(const BatchArgs& a) {
     const char* force = std::getenv("MDG_FITSUP");
     if (force && *force) return force;
-    // By batch size, fit time per spectrum alone (tools/fit_by_batch2.sh):
-    // B <= 2 the 24-point term fold over one workgroup per tile ("tf": 214 / 149 us
-    // at B = 1 / 2, latency 0.88 ms at B = 1 against 0.95 for "tw7", the round-2
-    // choice for 18 concurrent B = 1 streams); B <= 24 the 63-point term fold over
+    // By batch size, fit time per spectrum alone: B <= 2 the 24-point
+    // term fold over one workgroup per tile ("tf": 212 / 149 us at B = 1 / 2, latency
+    // 0.88 ms at B = 1 against 0.95 for "tw7"); B <= 24 the 63-point term fold over
     // one workgroup per tile ("tw7": 120 / 113 / 93 us at B = 4 / 8 / 16 against 167 /
     // 187 / 118 for "dpp" / "dpp" / "plain"); beyond, one point per lane with the
     // update separate ("plain": 79 / 57 us at B = 32 / 256). The fused k_fit_sup_fu
     // ("fu") is as fast as "plain" alone but slower in the queue.
+    // When other engine contexts on the device have run pipelines, B = 1 keeps "tw7":
+    // "tf"'s lead alone is gone as soon as a second context has been used (latency
+    // 0.95 ms either way, the spectrum still alone on the GPU), and 18 concurrent
+    // B = 1 pipelines run 6.6k spectra/s with "tf" against 7.8-8.1k with "tw7".
+    if (a.B == 1 && a.contexts > 1) return "tw7";
     return a.B <= 2 ? "tf" : a.B <= 24 ? "tw7" : "plain";
 }
 bool fit_sup_dyn(const BatchArgs& a) { return fit_choice(a) == "dyn"; }
