@@ -10,6 +10,7 @@
  *   mdg_deconvolute_batch      <- Deconvoluter::{deconvolute_spectra,par_deconvolute_spectra}
  *                                 deconvoluter.rs:651-661 / :700-710 (per-spectrum status;
  *                                 the caller reproduces the fail-fast Result collect)
+ *   mdg_deconvolute_rows       same, one pointer per spectrum row (no caller-side stacking)
  *   mdg_deconvolute_batch_device  same, inputs/outputs resident in HBM (no PCIe in the call)
  *   mdg_superposition_vec      <- Lorentzian::{superposition_vec,par_superposition_vec}
  *                                 deconvolution/lorentzian.rs:631-663
@@ -156,6 +157,18 @@ int mdg_deconvolute_batch(mdg_ctx* ctx, size_t b, size_t n, const double* x, siz
                           const mdg_settings* s, const double* ignore, size_t n_ignore,
                           mdg_lorentzian* out, size_t cap, size_t* counts, double* mse,
                           int* status);
+
+/* Same, each spectrum's arrays where the caller keeps them: row i of x / y is
+ * x_rows[i] / y_rows[i] (n doubles each; one pointer repeated = one shared axis,
+ * uploaded once). Replaces the same reference interfaces as mdg_deconvolute_batch
+ * (deconvoluter.rs:651-661 / :700-710 take &[Spectrum], each Spectrum holding its
+ * rows as Arc<[f64]>, spectrum.rs:101-105, clones sharing one axis): the binding
+ * passes those slices' pointers, no caller-side stacking copy is made, and HIP
+ * copies straight from the rows. */
+int mdg_deconvolute_rows(mdg_ctx* ctx, size_t b, size_t n, const double* const* x_rows,
+                         const double* const* y_rows, const double* sb, const mdg_settings* s,
+                         const double* ignore, size_t n_ignore, mdg_lorentzian* out, size_t cap,
+                         size_t* counts, double* mse, int* status);
 
 /* Same, every array resident on the context's device (d_ prefix); enqueued on
  * the context stream without any host synchronisation (capturable). d_counts and

@@ -952,21 +952,19 @@ int mdg_deconvolute_batch_device(mdg_ctx* c, size_t b, size_t n, const double* d
     return run_pipeline_graphed(c, a, s);
 }
 
-int mdg_deconvolute_batch(mdg_ctx* c, size_t b, size_t n, const double* x, size_t x_stride,
-                          const double* y, size_t y_stride, const double* sb,
-                          const mdg_settings* s, const double* ignore, size_t n_ignore,
-                          mdg_lorentzian* out, size_t cap, size_t* counts, double* mse,
-                          int* status) {
-    if (!c) return MDG_INVALID_ARGUMENT;
-    int v = validate_common(s, n_ignore, ignore);
-    if (v) return v;
-    if (b == 0) return MDG_OK;
-    if (n < 2 || n > (size_t)INT32_MAX / 2 || b > (size_t)INT32_MAX) return MDG_INVALID_ARGUMENT;
-    if (!x || !y || !sb || !counts || !mse || !status || (!out && cap)) return MDG_INVALID_ARGUMENT;
+}  // extern "C"
+
+// Host-buffer batch: staging buffers, the caller's uploads (upload(dx, dy, st)
+// enqueues the H2D copies of x and y into the staging rows), the pipeline, and the
+// results back (only the rows the spectra filled). shared_x: one axis row.
+template <typename Upload>
+static int batch_host(mdg_ctx* c, size_t b, size_t n, bool shared_x, Upload upload, const double* sb,
+                      const mdg_settings* s, const double* ignore, size_t n_ignore, mdg_lorentzian* out,
+                      size_t cap, size_t* counts, double* mse, int* status) {
     std::lock_guard<std::mutex> g(c->mu);
     HIPCHK(hipSetDevice(c->device));
     hipStream_t st = c->stream;
-    const size_t xrows = x_stride ? b : 1;
+    const size_t xrows = shared_x ? 1 : b;
     int rc;
     if ((rc = ensure(c->st_x, xrows * n * 8))) return rc;
     if ((rc = ensure(c->st_y, b * n * 8))) return rc;
@@ -977,19 +975,10 @@ int mdg_deconvolute_batch(mdg_ctx* c, size_t b, size_t n, const double* x, size_
     if ((rc = ensure(c->st_status, b * 4))) return rc;
     double* dx = (double*)c->st_x.p;
     double* dy = (double*)c->st_y.p;
-    if (x_stride == 0 || x_stride == n) {
-        HIPCHK(hipMemcpyAsync(dx, x, xrows * n * 8, hipMemcpyHostToDevice, st));
-    } else {
-        HIPCHK(hipMemcpy2DAsync(dx, n * 8, x, x_stride * 8, n * 8, b, hipMemcpyHostToDevice, st));
-    }
-    if (y_stride == n) {
-        HIPCHK(hipMemcpyAsync(dy, y, b * n * 8, hipMemcpyHostToDevice, st));
-    } else {
-        HIPCHK(hipMemcpy2DAsync(dy, n * 8, y, y_stride * 8, n * 8, b, hipMemcpyHostToDevice, st));
-    }
+    HIPCHK(upload(dx, dy, st));
     HIPCHK(hipMemcpyAsync(c->st_sb.p, sb, b * 16, hipMemcpyHostToDevice, st));
     BatchArgs a;
-    if ((rc = fill_args(c, a, b, n, dx, x_stride ? n : 0, dy, n, (const double*)c->st_sb.p, ignore,
+    if ((rc = fill_args(c, a, b, n, dx, shared_x ? 0 : n, dy, n, (const double*)c->st_sb.p, ignore,
                         n_ignore, (double*)c->st_out.p, cap, (int32_t*)c->st_cnt.p, (double*)c->st_mse.p,
                         (int32_t*)c->st_status.p)))
         return rc;
@@ -1016,6 +1005,60 @@ int mdg_deconvolute_batch(mdg_ctx* c, size_t b, size_t n, const double* x, size_
         if (first == MDG_OK && stv[i] != MDG_OK) first = stv[i];
     }
     return first;
+}
+
+extern "C" {
+
+int mdg_deconvolute_batch(mdg_ctx* c, size_t b, size_t n, const double* x, size_t x_stride,
+                          const double* y, size_t y_stride, const double* sb,
+                          const mdg_settings* s, const double* ignore, size_t n_ignore,
+                          mdg_lorentzian* out, size_t cap, size_t* counts, double* mse,
+                          int* status) {
+    if (!c) return MDG_INVALID_ARGUMENT;
+    int v = validate_common(s, n_ignore, ignore);
+    if (v) return v;
+    if (b == 0) return MDG_OK;
+    if (n < 2 || n > (size_t)INT32_MAX / 2 || b > (size_t)INT32_MAX) return MDG_INVALID_ARGUMENT;
+    if (!x || !y || !sb || !counts || !mse || !status || (!out && cap)) return MDG_INVALID_ARGUMENT;
+    const size_t xrows = x_stride ? b : 1;
+    auto upload = [&](double* dx, double* dy, hipStream_t st) -> hipError_t {
+        hipError_t e = (x_stride == 0 || x_stride == n)
+                           ? hipMemcpyAsync(dx, x, xrows * n * 8, hipMemcpyHostToDevice, st)
+                           : hipMemcpy2DAsync(dx, n * 8, x, x_stride * 8, n * 8, b, hipMemcpyHostToDevice, st);
+        if (e != hipSuccess) return e;
+        return y_stride == n ? hipMemcpyAsync(dy, y, b * n * 8, hipMemcpyHostToDevice, st)
+                             : hipMemcpy2DAsync(dy, n * 8, y, y_stride * 8, n * 8, b, hipMemcpyHostToDevice, st);
+    };
+    return batch_host(c, b, n, x_stride == 0, upload, sb, s, ignore, n_ignore, out, cap, counts, mse, status);
+}
+
+int mdg_deconvolute_rows(mdg_ctx* c, size_t b, size_t n, const double* const* x_rows,
+                         const double* const* y_rows, const double* sb, const mdg_settings* s,
+                         const double* ignore, size_t n_ignore, mdg_lorentzian* out, size_t cap,
+                         size_t* counts, double* mse, int* status) {
+    if (!c) return MDG_INVALID_ARGUMENT;
+    int v = validate_common(s, n_ignore, ignore);
+    if (v) return v;
+    if (b == 0) return MDG_OK;
+    if (n < 2 || n > (size_t)INT32_MAX / 2 || b > (size_t)INT32_MAX) return MDG_INVALID_ARGUMENT;
+    if (!x_rows || !y_rows || !sb || !counts || !mse || !status || (!out && cap)) return MDG_INVALID_ARGUMENT;
+    bool shared = true;
+    for (size_t i = 0; i < b; ++i) {
+        if (!x_rows[i] || !y_rows[i]) return MDG_INVALID_ARGUMENT;
+        shared = shared && x_rows[i] == x_rows[0];
+    }
+    auto upload = [&](double* dx, double* dy, hipStream_t st) -> hipError_t {
+        for (size_t i = 0; i < (shared ? 1 : b); ++i) {
+            hipError_t e = hipMemcpyAsync(dx + i * n, x_rows[i], n * 8, hipMemcpyHostToDevice, st);
+            if (e != hipSuccess) return e;
+        }
+        for (size_t i = 0; i < b; ++i) {
+            hipError_t e = hipMemcpyAsync(dy + i * n, y_rows[i], n * 8, hipMemcpyHostToDevice, st);
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    };
+    return batch_host(c, b, n, shared, upload, sb, s, ignore, n_ignore, out, cap, counts, mse, status);
 }
 
 int mdg_deconvolute(mdg_ctx* c, const double* x, const double* y, size_t n, double sb0,

@@ -410,24 +410,29 @@ class Deconvoluter:
 
     def _run_batch(self, ctx, spectra: list[Spectrum], idx: list[int], n: int, ign):
         b = len(idx)
-        x = np.stack([spectra[i].chemical_shifts for i in idx])
-        y = np.stack([spectra[i].intensities for i in idx])
         sb = np.array([spectra[i].signal_boundaries for i in idx], dtype=np.float64)
         cap = n // 2 + 2
-        out = np.empty((b, cap, 3))
         counts = np.zeros(b, dtype=np.uintp)
         mse = np.zeros(b)
         status = np.zeros(b, dtype=np.intc)
+        # each spectrum's own rows (kept by the Spectrum, so HIP copies from memory it
+        # has seen before): no stacking copy (mdg_deconvolute_rows)
+        xr = np.array([spectra[i].chemical_shifts.ctypes.data for i in idx], dtype=np.uintp)
+        yr = np.array([spectra[i].intensities.ctypes.data for i in idx], dtype=np.uintp)
         with ctx.lock:  # ctypes drops the GIL for the call: lanes run concurrently
-            rc = nat.lib().mdg_deconvolute_batch(
-                ctx.handle, b, n, nat.ptr(x), n, nat.ptr(y), n, nat.ptr(sb),
+            # the result rows: the context's own host buffer, kept across calls
+            out = ctx.host_rows("out", (b, cap, 3))
+            rc = nat.lib().mdg_deconvolute_rows(
+                ctx.handle, b, n, xr.ctypes.data_as(ctypes.POINTER(nat._dp)),
+                yr.ctypes.data_as(ctypes.POINTER(nat._dp)), nat.ptr(sb),
                 ctypes.byref(self._s), nat.ptr(ign) if ign.size else None, ign.size // 2,
                 nat.ptr(out), cap, nat.ptr(counts, nat._szp), nat.ptr(mse),
                 status.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
-        if rc >= 100 or rc == nat.INVALID_ARGUMENT:
-            raise exc.UnexpectedError(f"GPU engine failure: {nat.strerror(rc)}")
-        return [(int(status[k]), out[k, : int(counts[k])].copy(), float(mse[k]))
-                for k in range(b)]
+            if rc >= 100 or rc == nat.INVALID_ARGUMENT:
+                raise exc.UnexpectedError(f"GPU engine failure: {nat.strerror(rc)}")
+            # copied out while the rows are still this call's
+            return [(int(status[k]), out[k, : int(counts[k])].copy(), float(mse[k]))
+                    for k in range(b)]
 
     def _run(self, spectra: list[Spectrum]) -> list[tuple[int, np.ndarray, float]]:
         """GPU results per spectrum, (status, params, mse) in input order: the

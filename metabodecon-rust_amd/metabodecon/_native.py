@@ -41,7 +41,7 @@ EXPORTS = [
     "mdg_ignore_region_add", "mdg_synth_lorentzians", "mdg_synth_noise", "mdg_device_count",
     "mdg_ctx_create", "mdg_ctx_destroy", "mdg_ctx_set_stream", "mdg_ctx_synchronize",
     "mdg_ctx_set_profiling", "mdg_ctx_stage_times", "mdg_ctx_reset_stage_times",
-    "mdg_deconvolute", "mdg_deconvolute_batch", "mdg_deconvolute_batch_device",
+    "mdg_deconvolute", "mdg_deconvolute_batch", "mdg_deconvolute_rows", "mdg_deconvolute_batch_device",
     "mdg_superposition_vec", "mdg_superposition_vec_device", "mdg_synth_batch_device",
     "mdg_ctx_last_peaks", "mdg_ctx_last_smoothed", "mdg_ctx_set_profiling_mask",
     "mdg_optimize_settings", "mdg_ordered_sum", "mdg_check_fast_division",
@@ -233,6 +233,8 @@ def _declare(L):
                                   _sz, _dp, _sz, _szp, _dp]
     L.mdg_deconvolute_batch.argtypes = [_vp, _sz, _sz, _dp, _sz, _dp, _sz, _dp, sp, _dp, _sz,
                                         _dp, _sz, _szp, _dp, ctypes.POINTER(ctypes.c_int)]
+    L.mdg_deconvolute_rows.argtypes = [_vp, _sz, _sz, ctypes.POINTER(_dp), ctypes.POINTER(_dp), _dp,
+                                       sp, _dp, _sz, _dp, _sz, _szp, _dp, ctypes.POINTER(ctypes.c_int)]
     L.mdg_deconvolute_batch_device.argtypes = [_vp, _sz, _sz, _vp, _sz, _vp, _sz, _vp, sp, _dp,
                                                _sz, _vp, _sz, _vp, _vp, _vp]
     L.mdg_superposition_vec.argtypes = [_vp, _dp, _sz, _dp, _sz, _dp]
@@ -299,6 +301,24 @@ class Context:
         self.handle = h
         self.device = device
         self.lock = threading.Lock()
+        self._host: dict[str, np.ndarray] = {}
+
+    def host_rows(self, name: str, shape: tuple, dtype=np.float64) -> np.ndarray:
+        """A C-contiguous host array of `shape` for this context's host-buffer calls
+        (use it under self.lock), backed by a buffer kept across calls and grown
+        geometrically. Fresh arrays of tens of MiB each call cost page faults, and a
+        pageable copy into or out of memory HIP has not seen before is slow: a
+        16-spectrum call with fresh stacked inputs and result rows spent ~8 ms there
+        against ~1.2 ms of GPU time. Only the pages a call touches
+        become resident."""
+        dt = np.dtype(dtype)
+        need = int(np.prod(shape)) * dt.itemsize
+        buf = self._host.get(name)
+        if buf is None or buf.nbytes < need:
+            size = max(need, 2 * buf.nbytes if buf is not None else 0)
+            buf = np.empty(size, dtype=np.uint8)
+            self._host[name] = buf
+        return buf[:need].view(dt).reshape(shape)
 
     def close(self):
         if getattr(self, "handle", None):

@@ -148,6 +148,22 @@ pub mod ffi {
             mse: *mut f64,
             status: *mut c_int,
         ) -> c_int;
+        pub fn mdg_deconvolute_rows(
+            ctx: *mut MdgCtx,
+            b: usize,
+            n: usize,
+            x_rows: *const *const f64,
+            y_rows: *const *const f64,
+            sb: *const f64,
+            s: *const MdgSettings,
+            ignore: *const f64,
+            n_ignore: usize,
+            out: *mut MdgLorentzian,
+            cap: usize,
+            counts: *mut usize,
+            mse: *mut f64,
+            status: *mut c_int,
+        ) -> c_int;
         pub fn mdg_deconvolute_batch_device(
             ctx: *mut MdgCtx,
             b: usize,
@@ -582,11 +598,13 @@ impl GpuDeconvoluter for Deconvoluter {
                 .filter(|&i| spectra[i].as_ref().len() == n)
                 .collect();
             let b = idx.len();
-            let (mut x, mut y, mut sb) = (Vec::with_capacity(b * n), Vec::with_capacity(b * n), Vec::new());
+            // the spectra's own rows (Arc<[f64]>, spectrum.rs:101-105), no stacking copy;
+            // spectra sharing one axis Arc pass one pointer, uploaded once
+            let (mut x, mut y, mut sb) = (Vec::with_capacity(b), Vec::with_capacity(b), Vec::new());
             for &i in &idx {
                 let sp = spectra[i].as_ref();
-                x.extend_from_slice(sp.chemical_shifts());
-                y.extend_from_slice(sp.intensities());
+                x.push(sp.chemical_shifts().as_ptr());
+                y.push(sp.intensities().as_ptr());
                 let (a, c) = sp.signal_boundaries();
                 sb.extend_from_slice(&[a, c]);
             }
@@ -596,14 +614,12 @@ impl GpuDeconvoluter for Deconvoluter {
             let mut mse = vec![0f64; b];
             let mut status = vec![0 as c_int; b];
             let rc = unsafe {
-                ffi::mdg_deconvolute_batch(
+                ffi::mdg_deconvolute_rows(
                     ctx.raw(),
                     b,
                     n,
                     x.as_ptr(),
-                    n,
                     y.as_ptr(),
-                    n,
                     sb.as_ptr(),
                     &s,
                     opt_ptr(&ig),

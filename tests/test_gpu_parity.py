@@ -86,6 +86,52 @@ def test_blood_batch_all_16(ctx):
         assert np.array_equal(ctx.last_peaks(k, "selected").astype(np.int64), g["selected"])
 
 
+def gpu_rows(ctx, x_rows, y_rows, sbs, settings):
+    """mdg_deconvolute_rows: one pointer per spectrum row (as the Rust shim binds it)."""
+    b, n = len(y_rows), len(y_rows[0])
+    xr = np.array([r.ctypes.data for r in x_rows], dtype=np.uintp)
+    yr = np.array([r.ctypes.data for r in y_rows], dtype=np.uintp)
+    sbs = np.ascontiguousarray(np.asarray(sbs, dtype=np.float64).reshape(b, 2))
+    s = nat.Settings()
+    for f, _ in nat.Settings._fields_:
+        setattr(s, f, getattr(settings, f))
+    cap = n // 2 + 2
+    out = np.zeros((b, cap, 3))
+    counts = np.zeros(b, dtype=np.uintp)
+    mse = np.zeros(b)
+    status = np.zeros(b, dtype=np.intc)
+    rc = nat.lib().mdg_deconvolute_rows(
+        ctx.handle, b, n, xr.ctypes.data_as(ctypes.POINTER(nat._dp)),
+        yr.ctypes.data_as(ctypes.POINTER(nat._dp)), nat.ptr(sbs), ctypes.byref(s), None, 0,
+        nat.ptr(out), cap, nat.ptr(counts, nat._szp), nat.ptr(mse),
+        status.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+    assert rc < 100, nat.strerror(rc)
+    return status, counts.astype(int), out, mse
+
+
+def test_rows_entry_blood_16_and_shared_axis(ctx):
+    """mdg_deconvolute_rows (row pointers, no stacking) on the 16 blood spectra, in
+    a scrambled order with every row its own array: the goldens bit for bit. Then
+    spectrum 1's axis passed for every spectrum (one pointer repeated, uploaded
+    once) against mdg_deconvolute_batch with x_stride 0 on the same inputs."""
+    names = [f"blood_{i:02d}" for i in range(1, 17)]
+    order = [5, 0, 15, 3, 9, 1, 12, 7, 2, 14, 8, 4, 11, 6, 13, 10]
+    data = [load_case(names[k]) for k in order]
+    xs = [np.array(d[0]) for d in data]
+    ys = [np.array(d[1]) for d in data]
+    sbs = [d[2] for d in data]
+    status, counts, out, mse = gpu_rows(ctx, xs, ys, sbs, data[0][3])
+    for j, k in enumerate(order):
+        g = np.load(os.path.join(GOLDEN, "expected", f"{names[k]}.npz"))
+        check_against(g["params"], float(g["mse"]), status[j], counts[j], out[j], mse[j])
+    x0 = xs[0]
+    st1, c1, o1, m1 = gpu_rows(ctx, [x0] * 16, ys, sbs, data[0][3])
+    st2, c2, o2, m2 = gpu_batch(ctx, x0, np.stack(ys), sbs, data[0][3])
+    assert np.array_equal(st1, st2) and np.array_equal(c1, c2) and np.array_equal(m1, m2)
+    for j in range(16):
+        assert np.array_equal(o1[j, : c1[j]], o2[j, : c2[j]])
+
+
 @pytest.mark.parametrize("path", ["fused", "MDG_PEAKS_NOSCORE", "MDG_PEAKS_2PASS"])
 def test_detected_peaks_match_oracle(ctx, path, monkeypatch):
     """Detected triples equal the oracle's; the selection (which reads the noise

@@ -33,7 +33,9 @@ RUST_TO_C = {
 def c_type(rt: str) -> str:
     rt = rt.strip()
     if rt.startswith("*const "):
-        return "const " + c_type(rt[len("*const "):]) + "*"
+        inner = c_type(rt[len("*const "):])
+        # *const *const f64 -> const double* const*
+        return inner + " const*" if inner.endswith("*") else "const " + inner + "*"
     if rt.startswith("*mut "):
         inner = c_type(rt[len("*mut "):])
         return inner + "*"
@@ -135,8 +137,8 @@ def shim():
 def test_shim_declares_the_hot_path(shim):
     externs, structs, _ = shim
     names = {e[0] for e in externs}
-    assert {"mdg_deconvolute", "mdg_deconvolute_batch", "mdg_deconvolute_batch_device",
-            "mdg_superposition_vec", "mdg_optimize_settings", "mdg_ctx_create",
+    assert {"mdg_deconvolute", "mdg_deconvolute_batch", "mdg_deconvolute_rows",
+            "mdg_deconvolute_batch_device", "mdg_superposition_vec", "mdg_optimize_settings", "mdg_ctx_create",
             "mdg_ctx_destroy"} <= names
     assert set(structs) == {"MdgSettings", "MdgLorentzian"}
     header = open(os.path.join(INCLUDE, "mdgpu.h")).read()
@@ -159,6 +161,7 @@ def test_shim_signatures_compile_against_header_and_run(shim, tmp_path):
 @pytest.mark.parametrize("mutation", [
     ("mdg_deconvolute", "cap", "u32"),            # usize -> u32
     ("mdg_deconvolute_batch", "status", "*mut u64"),
+    ("mdg_deconvolute_rows", "x_rows", "*const f64"),  # one row, not row pointers
     ("mdg_superposition_vec", "out", "*mut i32"),
 ])
 def test_mutated_signature_fails_to_compile(shim, tmp_path, mutation):
