@@ -204,6 +204,34 @@ def pmc_traffic(tag, stage, kernel=None):
     return None, None
 
 
+def hbm_pipeline(tag, batch, iterations, value, n):
+    """Whole-pipeline HBM traffic per spectrum from the newest committed PMC summary
+    of this workload tag (per-launch bytes of every kernel a batch launches, x its
+    launches per pipeline, / the batch size), and the rate it implies at `value`
+    spectra/s -- the BASELINE metric's "achieved HBM GB/s" for the mode that
+    produces `value`. None when no summary is committed."""
+    launches = {"k_queue_gather": 1, "k_smooth_chain<3, false>": 1, "k_flags": 1, "k_peaks": 1,
+                "k_select<1024>": 1, "k_fit_sup": iterations, "k_fit_update": iterations,
+                "k_mse_local": 1, "k_queue_scatter": 1}
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{tag}.json")),
+                       reverse=True):
+        try:
+            kern = json.load(open(path))["kernels"]
+            per = {k: kern[k]["hbm_bytes_per_launch"] * m / batch for k, m in launches.items()}
+        except (OSError, KeyError, ValueError):
+            continue
+        total = sum(per.values())
+        return {"bytes_per_spectrum": total, "achieved": total * value / 1e9, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": total * value / 1e9 / HBM_PEAK_GBS,
+                "algorithmic_bytes_per_spectrum": 8 * n,
+                "mb_per_spectrum": {k: round(v / 1e6, 3) for k, v in per.items()},
+                "source": (f"{os.path.relpath(path, ROOT)}: PMC HBM bytes per launch (2 x FETCH_SIZE "
+                           "+ WRITE_SIZE) of each kernel of a batch, x launches per pipeline, / "
+                           f"batch {batch}; x value. Algorithmic: the intensity row in (8 N; the "
+                           "shared axis and the result rows are < 5%)")}
+    return None
+
+
 def roofline_from_stages(ctx, stages, work, tag, n):
     """Roofline of the dominant stage of a profiled pass: `stages` = stage ->
     (ms, launches) from hipEvents around every launch on the context stream;
@@ -1111,6 +1139,8 @@ def queue_line(args, h, world, nat):
         "rccl_gather_ms": h["gather_ms"],
         "roofline": roof,
         "roofline_pipeline": pipe,
+        "hbm_pipeline": hbm_pipeline(f"q{args.max_batch}", args.max_batch,
+                                     args.fit_iterations or 10, value, args.n),
         "stages_ms_per_spectrum": h["stages_ms_per_spectrum"],
         "stages_source": (f"separate profiled pass: one batch of {args.max_batch} on lane 0 "
                           "(hipEvents around every stage), per spectrum"),
