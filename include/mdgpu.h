@@ -163,8 +163,9 @@ int mdg_deconvolute_batch(mdg_ctx* ctx, size_t b, size_t n, const double* x, siz
  * uploaded once). Replaces the same reference interfaces as mdg_deconvolute_batch
  * (deconvoluter.rs:651-661 / :700-710 take &[Spectrum], each Spectrum holding its
  * rows as Arc<[f64]>, spectrum.rs:101-105, clones sharing one axis): the binding
- * passes those slices' pointers, no caller-side stacking copy is made, and HIP
- * copies straight from the rows. */
+ * passes those slices' pointers and no caller-side stacking copy is made; the
+ * engine gathers the rows into its page-locked ring (two slots of up to 32 MiB per
+ * context) and sends one asynchronous DMA per slot. */
 int mdg_deconvolute_rows(mdg_ctx* ctx, size_t b, size_t n, const double* const* x_rows,
                          const double* const* y_rows, const double* sb, const mdg_settings* s,
                          const double* ignore, size_t n_ignore, mdg_lorentzian* out, size_t cap,

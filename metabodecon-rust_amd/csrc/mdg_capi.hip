@@ -87,6 +87,13 @@ struct mdg_ctx {
     Workspace w{};
     // staging for the host-pointer API
     Buffer st_x, st_y, st_sb, st_out, st_cnt, st_mse, st_status, st_L, st_sup, st_flag;
+    // page-locked host ring for mdg_deconvolute_rows: the rows are gathered into a
+    // slot and sent with one asynchronous DMA per slot (upload_rows)
+    void* ring[2] = {nullptr, nullptr};
+    size_t ring_bytes = 0;
+    hipEvent_t ring_ev[2] = {nullptr, nullptr};
+    bool ring_used[2] = {false, false};
+    int ring_next = 0;  // the slot the next upload fills (uploads alternate slots)
     // profiling
     uint32_t profile_mask = 0;  // stages timed with hipEvents (bit = stage)
     std::vector<Pending> pending;
@@ -671,6 +678,10 @@ int mdg_ctx_destroy(mdg_ctx* c) {
         for (Buffer* b : {&c->arena, &c->chain, &c->chain_flags, &c->ign, &c->st_x, &c->st_y, &c->st_sb, &c->st_out, &c->st_cnt,
                           &c->st_mse, &c->st_status, &c->st_L, &c->st_sup, &c->st_flag})
             if (b->p) (void)hipFree(b->p);
+        for (int k = 0; k < 2; ++k) {
+            if (c->ring[k]) (void)hipHostFree(c->ring[k]);
+            if (c->ring_ev[k]) (void)hipEventDestroy(c->ring_ev[k]);
+        }
         if (c->own) (void)hipStreamDestroy(c->own);
     }
     if (c->counted) g_live_ctx[c->device].fetch_sub(1);
@@ -954,6 +965,56 @@ int mdg_deconvolute_batch_device(mdg_ctx* c, size_t b, size_t n, const double* d
 
 }  // extern "C"
 
+// Copies b host rows of `row_bytes` each (rows[i], anywhere in pageable memory) to
+// the contiguous device range dst on st through the context's page-locked ring: a
+// slot (<= kRingSlot bytes) is filled with memcpy, sent with one asynchronous DMA,
+// and refilled once its event says the DMA has read it; the two slots alternate, so
+// the host copy of one overlaps the DMA of the other. One pageable hipMemcpyAsync per
+// row instead costs a host wait per row, and on a stream sharing its hardware queue
+// with another lane's kernels each of those waits behind them (configs[4] at the
+// default 4 queues: ~4.0k spectra/s with per-row copies against ~5.5-6.1k with one
+// copy of a stacked buffer).
+constexpr size_t kRingSlot = 32u << 20;
+static int upload_rows(mdg_ctx* c, hipStream_t st, char* dst, const double* const* rows, size_t b,
+                       size_t row_bytes) {
+    const size_t total = b * row_bytes;
+    if (total == 0) return MDG_OK;
+    const size_t want = std::min(kRingSlot, (total + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1));
+    if (c->ring_bytes < want) {
+        for (int k = 0; k < 2; ++k) {
+            if (c->ring_used[k]) HIPCHK(hipEventSynchronize(c->ring_ev[k]));
+            if (c->ring[k]) HIPCHK(hipHostFree(c->ring[k]));
+            c->ring[k] = nullptr;
+            c->ring_used[k] = false;
+        }
+        c->ring_bytes = 0;
+        for (int k = 0; k < 2; ++k) {
+            HIPCHK(hipHostMalloc(&c->ring[k], want, hipHostMallocDefault));
+            if (!c->ring_ev[k]) HIPCHK(hipEventCreateWithFlags(&c->ring_ev[k], hipEventDisableTiming));
+        }
+        c->ring_bytes = want;
+    }
+    int slot = c->ring_next;
+    for (size_t off = 0; off < total; off += c->ring_bytes) {
+        const size_t len = std::min(c->ring_bytes, total - off);
+        if (c->ring_used[slot]) HIPCHK(hipEventSynchronize(c->ring_ev[slot]));
+        char* buf = (char*)c->ring[slot];
+        // the rows overlapping [off, off + len)
+        for (size_t r = off / row_bytes, done = 0; done < len; ++r) {
+            const size_t in = (off + done) - r * row_bytes;
+            const size_t k = std::min(row_bytes - in, len - done);
+            std::memcpy(buf + done, (const char*)rows[r] + in, k);
+            done += k;
+        }
+        HIPCHK(hipMemcpyAsync(dst + off, buf, len, hipMemcpyHostToDevice, st));
+        HIPCHK(hipEventRecord(c->ring_ev[slot], st));
+        c->ring_used[slot] = true;
+        slot ^= 1;
+    }
+    c->ring_next = slot;
+    return MDG_OK;
+}
+
 // Host-buffer batch: staging buffers, the caller's uploads (upload(dx, dy, st)
 // enqueues the H2D copies of x and y into the staging rows), the pipeline, and the
 // results back (only the rows the spectra filled). shared_x: one axis row.
@@ -975,7 +1036,7 @@ static int batch_host(mdg_ctx* c, size_t b, size_t n, bool shared_x, Upload uplo
     if ((rc = ensure(c->st_status, b * 4))) return rc;
     double* dx = (double*)c->st_x.p;
     double* dy = (double*)c->st_y.p;
-    HIPCHK(upload(dx, dy, st));
+    if ((rc = upload(dx, dy, st))) return rc;
     HIPCHK(hipMemcpyAsync(c->st_sb.p, sb, b * 16, hipMemcpyHostToDevice, st));
     BatchArgs a;
     if ((rc = fill_args(c, a, b, n, dx, shared_x ? 0 : n, dy, n, (const double*)c->st_sb.p, ignore,
@@ -1021,13 +1082,13 @@ int mdg_deconvolute_batch(mdg_ctx* c, size_t b, size_t n, const double* x, size_
     if (n < 2 || n > (size_t)INT32_MAX / 2 || b > (size_t)INT32_MAX) return MDG_INVALID_ARGUMENT;
     if (!x || !y || !sb || !counts || !mse || !status || (!out && cap)) return MDG_INVALID_ARGUMENT;
     const size_t xrows = x_stride ? b : 1;
-    auto upload = [&](double* dx, double* dy, hipStream_t st) -> hipError_t {
-        hipError_t e = (x_stride == 0 || x_stride == n)
-                           ? hipMemcpyAsync(dx, x, xrows * n * 8, hipMemcpyHostToDevice, st)
-                           : hipMemcpy2DAsync(dx, n * 8, x, x_stride * 8, n * 8, b, hipMemcpyHostToDevice, st);
-        if (e != hipSuccess) return e;
-        return y_stride == n ? hipMemcpyAsync(dy, y, b * n * 8, hipMemcpyHostToDevice, st)
-                             : hipMemcpy2DAsync(dy, n * 8, y, y_stride * 8, n * 8, b, hipMemcpyHostToDevice, st);
+    auto upload = [&](double* dx, double* dy, hipStream_t st) -> int {
+        HIPCHK((x_stride == 0 || x_stride == n)
+                   ? hipMemcpyAsync(dx, x, xrows * n * 8, hipMemcpyHostToDevice, st)
+                   : hipMemcpy2DAsync(dx, n * 8, x, x_stride * 8, n * 8, b, hipMemcpyHostToDevice, st));
+        HIPCHK(y_stride == n ? hipMemcpyAsync(dy, y, b * n * 8, hipMemcpyHostToDevice, st)
+                             : hipMemcpy2DAsync(dy, n * 8, y, y_stride * 8, n * 8, b, hipMemcpyHostToDevice, st));
+        return MDG_OK;
     };
     return batch_host(c, b, n, x_stride == 0, upload, sb, s, ignore, n_ignore, out, cap, counts, mse, status);
 }
@@ -1047,16 +1108,9 @@ int mdg_deconvolute_rows(mdg_ctx* c, size_t b, size_t n, const double* const* x_
         if (!x_rows[i] || !y_rows[i]) return MDG_INVALID_ARGUMENT;
         shared = shared && x_rows[i] == x_rows[0];
     }
-    auto upload = [&](double* dx, double* dy, hipStream_t st) -> hipError_t {
-        for (size_t i = 0; i < (shared ? 1 : b); ++i) {
-            hipError_t e = hipMemcpyAsync(dx + i * n, x_rows[i], n * 8, hipMemcpyHostToDevice, st);
-            if (e != hipSuccess) return e;
-        }
-        for (size_t i = 0; i < b; ++i) {
-            hipError_t e = hipMemcpyAsync(dy + i * n, y_rows[i], n * 8, hipMemcpyHostToDevice, st);
-            if (e != hipSuccess) return e;
-        }
-        return hipSuccess;
+    auto upload = [&](double* dx, double* dy, hipStream_t st) -> int {
+        int rc = upload_rows(c, st, (char*)dx, x_rows, shared ? 1 : b, n * 8);
+        return rc ? rc : upload_rows(c, st, (char*)dy, y_rows, b, n * 8);
     };
     return batch_host(c, b, n, shared, upload, sb, s, ignore, n_ignore, out, cap, counts, mse, status);
 }

@@ -415,8 +415,8 @@ class Deconvoluter:
         counts = np.zeros(b, dtype=np.uintp)
         mse = np.zeros(b)
         status = np.zeros(b, dtype=np.intc)
-        # each spectrum's own rows (kept by the Spectrum, so HIP copies from memory it
-        # has seen before): no stacking copy (mdg_deconvolute_rows)
+        # each spectrum's own rows, by pointer (mdg_deconvolute_rows gathers them into
+        # its page-locked ring and sends one DMA per slot): no stacking copy here
         xr = np.array([spectra[i].chemical_shifts.ctypes.data for i in idx], dtype=np.uintp)
         yr = np.array([spectra[i].intensities.ctypes.data for i in idx], dtype=np.uintp)
         with ctx.lock:  # ctypes drops the GIL for the call: lanes run concurrently
