@@ -1119,11 +1119,14 @@ int mdg_deconvolute(mdg_ctx* c, const double* x, const double* y, size_t n, doub
                     double sb1, const mdg_settings* s, const double* ignore, size_t n_ignore,
                     mdg_lorentzian* out, size_t cap, size_t* out_count, double* out_mse) {
     if (!out_count || !out_mse) return MDG_INVALID_ARGUMENT;
+    if (!x || !y) return MDG_INVALID_ARGUMENT;
     const double sb[2] = {sb0, sb1};
     int status = 0;
-    int rc = mdg_deconvolute_batch(c, 1, n, x, 0, y, n, sb, s, ignore, n_ignore, out, cap,
-                                   out_count, out_mse, &status);
-    return rc;
+    // through the page-locked ring (mdg_deconvolute_rows), not pageable copies
+    const double* const xr[1] = {x};
+    const double* const yr[1] = {y};
+    return mdg_deconvolute_rows(c, 1, n, xr, yr, sb, s, ignore, n_ignore, out, cap, out_count, out_mse,
+                                &status);
 }
 
 int mdg_superposition_vec_device(mdg_ctx* c, const double* d_x, size_t n, const mdg_lorentzian* d_L,

@@ -132,6 +132,32 @@ def test_rows_entry_blood_16_and_shared_axis(ctx):
         assert np.array_equal(o1[j, : c1[j]], o2[j, : c2[j]])
 
 
+def test_single_spectrum_entry(ctx):
+    """mdg_deconvolute (the Rust shim's gpu_deconvolute_spectrum) on blood_01 and
+    blood_02: the goldens bit for bit; a capacity below P_kept reports MDG_CAPACITY
+    with the count (the shim's two-phase size query)."""
+    for name in ("blood_01", "blood_02"):
+        x, y, sb, st, _ = load_case(name)
+        x, y = np.ascontiguousarray(x), np.ascontiguousarray(y)
+        s = nat.Settings()
+        for f, _ in nat.Settings._fields_:
+            setattr(s, f, getattr(st, f))
+        cap = len(y) // 2 + 2
+        out = np.zeros((cap, 3))
+        cnt = ctypes.c_size_t(0)
+        mse = ctypes.c_double(0.0)
+        rc = nat.lib().mdg_deconvolute(ctx.handle, nat.ptr(x), nat.ptr(y), len(y), sb[0], sb[1],
+                                       ctypes.byref(s), None, 0, nat.ptr(out), cap,
+                                       ctypes.byref(cnt), ctypes.byref(mse))
+        g = np.load(os.path.join(GOLDEN, "expected", f"{name}.npz"))
+        check_against(g["params"], float(g["mse"]), rc, cnt.value, out, mse.value)
+        small = np.zeros((8, 3))
+        rc = nat.lib().mdg_deconvolute(ctx.handle, nat.ptr(x), nat.ptr(y), len(y), sb[0], sb[1],
+                                       ctypes.byref(s), None, 0, nat.ptr(small), 8,
+                                       ctypes.byref(cnt), ctypes.byref(mse))
+        assert rc == nat.CAPACITY and cnt.value == g["params"].shape[0]
+
+
 @pytest.mark.parametrize("path", ["fused", "MDG_PEAKS_NOSCORE", "MDG_PEAKS_2PASS"])
 def test_detected_peaks_match_oracle(ctx, path, monkeypatch):
     """Detected triples equal the oracle's; the selection (which reads the noise
