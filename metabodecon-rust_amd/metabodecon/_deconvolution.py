@@ -494,8 +494,18 @@ class Deconvoluter:
         parts = []
         for n, idx in by_n.items():
             b = len(idx)
-            x = torch.from_numpy(np.stack([spectra[i].chemical_shifts for i in idx])).to(dev)
-            y = torch.from_numpy(np.stack([spectra[i].intensities for i in idx])).to(dev)
+            # host rows gathered into the context's page-locked buffers, then one
+            # asynchronous DMA each (not a pageable copy of freshly stacked arrays)
+            with ctx.lock:
+                hx = ctx.pinned_rows("x", (b, n))
+                hy = ctx.pinned_rows("y", (b, n))
+                nx, ny = hx.numpy(), hy.numpy()
+                for r, i in enumerate(idx):
+                    nx[r] = spectra[i].chemical_shifts
+                    ny[r] = spectra[i].intensities
+                x = hx.to(dev, non_blocking=True)
+                y = hy.to(dev, non_blocking=True)
+                torch.cuda.current_stream(dev).synchronize()  # the buffers are reused
             sb = torch.tensor([spectra[i].signal_boundaries for i in idx], dtype=torch.float64,
                               device=dev)
             cap = n // 2 + 2

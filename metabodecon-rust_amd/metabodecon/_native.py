@@ -301,7 +301,7 @@ class Context:
         self.handle = h
         self.device = device
         self.lock = threading.Lock()
-        self._host: dict[str, np.ndarray] = {}
+        self._host: dict = {}  # host_rows / pinned_rows buffers
 
     def host_rows(self, name: str, shape: tuple, dtype=np.float64) -> np.ndarray:
         """A C-contiguous host array of `shape` for this context's host-buffer calls
@@ -319,6 +319,20 @@ class Context:
             buf = np.empty(size, dtype=np.uint8)
             self._host[name] = buf
         return buf[:need].view(dt).reshape(shape)
+
+    def pinned_rows(self, name: str, shape: tuple):
+        """A page-locked torch f64 CPU tensor of `shape` kept across calls (grown
+        geometrically), for host rows that torch sends to the device
+        (`Deconvoluter._run_device`): an asynchronous DMA instead of a pageable
+        copy from freshly stacked arrays."""
+        import torch
+        need = int(np.prod(shape)) * 8
+        buf = self._host.get("pinned:" + name)
+        if buf is None or buf.numel() < need:
+            size = max(need, 2 * buf.numel() if buf is not None else 0)
+            buf = torch.empty(size, dtype=torch.uint8, pin_memory=True)
+            self._host["pinned:" + name] = buf
+        return buf[:need].view(torch.float64).view(shape)
 
     def close(self):
         if getattr(self, "handle", None):
