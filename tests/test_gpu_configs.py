@@ -57,10 +57,11 @@ def _device_batch(B, n, peaks, hw_scale, cap, seed0=0, sigma=1.0e3):
     return res
 
 
-def _compare(res, cap):
+def _compare(res, cap, inner_threads=1):
     B, n = res["y"].shape
     st, counts, params, mse = oracle.deconvolute_batch(res["x"], res["y"], np.array([SB] * B),
-                                                       threads=host_threads(), cap=cap)
+                                                       threads=host_threads(), cap=cap,
+                                                       inner_threads=inner_threads)
     assert np.array_equal(res["status"], st), np.nonzero(res["status"] != st)
     assert np.array_equal(res["cnt"].astype(np.int64), counts)
     bad = [s for s in range(B)
@@ -89,6 +90,19 @@ def test_configs2_256x131072_bit_exact():
     assert k["smooth"].startswith("k_smooth_chain<3, false>") and k["fit_superposition"].startswith("k_fit_sup")
     counts = _compare(res, cap)
     assert counts.min() > 1900  # ~2k injected peaks survive selection and the fit
+    res["ctx"].close()
+
+
+def test_long_spectra_bit_exact():
+    """Two 4 000 037-point spectra (odd length, 30x configs[1]; 2048 injected
+    Lorentzians): row lengths far past every other test -- 62 501 mask words, 245
+    peak chunks, ~760k detected peaks, ~19k selected and fitted (P^2 = 3.6e8 terms
+    per fit point set), a 2 000 020-peak capacity -- against the oracle, bit for bit."""
+    n = 4000037
+    cap = n // 2 + 2
+    res = _device_batch(2, n, 2048, 1.0, cap, seed0=11)
+    counts = _compare(res, cap, inner_threads=max(1, host_threads() // 2))
+    assert counts.min() > 10000  # the noise peaks of 4M points pass the noise-score filter
     res["ctx"].close()
 
 
