@@ -835,8 +835,51 @@ def test_par_deconvolute_spectra_rccl_world1():
                            (-2.2, 11.8))
         with pytest.raises(mexc.NoPeaksDetected):
             par_deconvolute_spectra(md.Deconvoluter(), [spectra[1], flat, spectra[2]])
+        # ragged lengths through the same path: one device batch per length
+        ragged, expect = _ragged_set()
+        decs = par_deconvolute_spectra(md.Deconvoluter(), ragged)
+        for d, (params, mse) in zip(decs, expect):
+            assert np.array_equal(d.params, params)
+            assert abs(d.mse - mse) <= MSE_RTOL * abs(mse)
     finally:
         dist.destroy_process_group()
+
+
+def _ragged_set():
+    """Spectra of four lengths interleaved: blood (131072 points), sim (2048-point
+    simulated), blood_05 cut to its first 100 001 points, blood_06 cut to 70 001;
+    expected (params, mse) from the goldens or the oracle."""
+    import metabodecon as md
+    spectra, expect = [], []
+    for k in range(1, 5):
+        for name in (f"blood_{k:02d}", f"sim_{k:02d}"):
+            x, y, sb, _, _ = load_case(name)
+            g = np.load(os.path.join(GOLDEN, "expected", f"{name}.npz"))
+            spectra.append(md.Spectrum(x, y, sb))
+            expect.append((g["params"], float(g["mse"])))
+        if k <= 2:
+            x, y, _, _, _ = load_case(f"blood_{k + 4:02d}")
+            m = 100001 if k == 1 else 70001
+            x, y = x[:m].copy(), y[:m].copy()
+            sb = (11.8, float(x[-1]) + 1.0)
+            o = oracle.deconvolute(x, y, sb, threads=16)
+            assert o.status == 0
+            spectra.append(md.Spectrum(x, y, sb))
+            expect.append((o.params, o.mse))
+    return spectra, expect
+
+
+def test_ragged_lengths_through_the_python_surface():
+    """Deconvoluter.par_deconvolute_spectra on a set of four interleaved lengths
+    (one batched pipeline per length, each cut over the lanes): every result in
+    input order, bit for bit."""
+    import metabodecon as md
+    spectra, expect = _ragged_set()
+    decs = md.Deconvoluter().par_deconvolute_spectra(spectra)
+    assert len(decs) == len(spectra)
+    for d, (params, mse) in zip(decs, expect):
+        assert np.array_equal(d.params, params)
+        assert abs(d.mse - mse) <= MSE_RTOL * abs(mse)
 
 
 def test_graph_repoint_in_flight_bit_exact(monkeypatch):
