@@ -114,6 +114,16 @@ int mdg_synth_noise(uint64_t seed, size_t n, double sigma, double* out);
 
 /* ---- device contexts ------------------------------------------------------ */
 int mdg_device_count(int* count);
+/* Page-locked host memory for spectrum rows and result tables (the storage behind
+ * the reference's Spectrum rows, Arc<[f64]> in spectrum.rs:101-105, and the
+ * Deconvolution's Vec<Lorentzian>, deconvolution.rs:45-60): the host-buffer entry
+ * points DMA straight from / into it instead of staging through a bounce buffer.
+ * Blocks are carved from 64 MiB slabs pinned on `device` (portable to every device)
+ * and reused by size after mdg_host_free; the total is capped by MDGPU_PINNED_MAX
+ * (bytes, default 8 GiB): beyond it, and without a device, MDG_ERR_OUT_OF_MEMORY /
+ * MDG_ERR_NO_DEVICE, and the caller keeps ordinary memory. */
+int mdg_host_alloc(int device, size_t bytes, void** out);
+int mdg_host_free(void* p);
 int mdg_ctx_create(int device, mdg_ctx** out);
 int mdg_ctx_destroy(mdg_ctx* ctx);
 /* Run subsequent work on this hipStream_t (NULL = the context's own stream). */
@@ -165,7 +175,9 @@ int mdg_deconvolute_batch(mdg_ctx* ctx, size_t b, size_t n, const double* x, siz
  * rows as Arc<[f64]>, spectrum.rs:101-105, clones sharing one axis): the binding
  * passes those slices' pointers and no caller-side stacking copy is made; the
  * engine gathers the rows into its page-locked ring (two slots of up to 32 MiB per
- * context) and sends one asynchronous DMA per slot. */
+ * context) and sends one asynchronous DMA per slot. When every row lies in memory
+ * from mdg_host_alloc, the rows are sent straight from there (one DMA per run of
+ * adjacent rows, no host copy); `out` from mdg_host_alloc is filled by DMA too. */
 int mdg_deconvolute_rows(mdg_ctx* ctx, size_t b, size_t n, const double* const* x_rows,
                          const double* const* y_rows, const double* sb, const mdg_settings* s,
                          const double* ignore, size_t n_ignore, mdg_lorentzian* out, size_t cap,

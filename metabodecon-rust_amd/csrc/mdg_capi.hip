@@ -13,6 +13,7 @@
 #include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -94,6 +95,11 @@ struct mdg_ctx {
     hipEvent_t ring_ev[2] = {nullptr, nullptr};
     bool ring_used[2] = {false, false};
     int ring_next = 0;  // the slot the next upload fills (uploads alternate slots)
+    // page-locked scratch of the host-buffer calls: boundaries in, counts / statuses /
+    // MSEs out (pageable small copies each cost a staged, host-blocking transfer)
+    void* hsmall = nullptr;
+    size_t hsmall_bytes = 0;
+    bool hsmall_busy = false;  // a call that failed midway may still have copies in flight
     // profiling
     uint32_t profile_mask = 0;  // stages timed with hipEvents (bit = stage)
     std::vector<Pending> pending;
@@ -175,6 +181,97 @@ void drain_timers(mdg_ctx* c) {
 }
 
 size_t align256(size_t v) { return (v + 255) & ~size_t(255); }
+
+// ---- page-locked host blocks (mdg_host_alloc) ----------------------------------
+// Blocks are carved from 64 MiB slabs (hipHostMalloc, portable) and kept on a free
+// list per size when released; the slabs stay pinned for the process's life. The
+// live map answers "is this row page-locked" for the host-buffer entry points,
+// which then DMA straight from the caller's rows (upload_rows).
+struct PinnedPool {
+    std::mutex mu;
+    std::map<uintptr_t, size_t> live;                  // block start -> bytes
+    std::map<size_t, std::vector<void*>> free_blocks;  // bytes -> released blocks
+    char* cur = nullptr;                                // bump pointer in the newest slab
+    size_t cur_left = 0;
+    size_t pinned = 0;                                  // bytes of all slabs
+};
+PinnedPool& pinned_pool() {
+    static PinnedPool* p = new PinnedPool();  // never destroyed: blocks may be freed at exit
+    return *p;
+}
+constexpr size_t kPinnedSlab = 64u << 20;
+
+size_t pinned_limit() {
+    static const size_t lim = [] {
+        const char* e = std::getenv("MDGPU_PINNED_MAX");
+        return e && *e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)8 << 30;
+    }();
+    return lim;
+}
+
+int pinned_alloc(int device, size_t bytes, void** out) {
+    const size_t sz = (bytes + 4095) & ~size_t(4095);
+    PinnedPool& P = pinned_pool();
+    std::lock_guard<std::mutex> g(P.mu);
+    auto it = P.free_blocks.find(sz);
+    if (it != P.free_blocks.end() && !it->second.empty()) {
+        void* p = it->second.back();
+        it->second.pop_back();
+        P.live[(uintptr_t)p] = sz;
+        *out = p;
+        return MDG_OK;
+    }
+    if (P.cur_left < sz) {
+        const size_t slab = std::max(sz, kPinnedSlab);
+        if (P.pinned + slab > pinned_limit()) return MDG_ERR_OUT_OF_MEMORY;
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return MDG_ERR_NO_DEVICE;
+        if (device < 0 || device >= n) return MDG_ERR_NO_DEVICE;
+        int prev = 0;
+        HIPCHK(hipGetDevice(&prev));
+        HIPCHK(hipSetDevice(device));
+        void* s = nullptr;
+        const hipError_t e = hipHostMalloc(&s, slab, hipHostMallocPortable);
+        (void)hipSetDevice(prev);
+        if (e != hipSuccess) return MDG_ERR_OUT_OF_MEMORY;
+        if (P.cur_left) P.free_blocks[P.cur_left].push_back(P.cur);  // the old slab's tail
+        P.cur = (char*)s;
+        P.cur_left = slab;
+        P.pinned += slab;
+    }
+    void* p = P.cur;
+    P.cur += sz;
+    P.cur_left -= sz;
+    P.live[(uintptr_t)p] = sz;
+    *out = p;
+    return MDG_OK;
+}
+
+int pinned_free(void* p) {
+    if (!p) return MDG_OK;
+    PinnedPool& P = pinned_pool();
+    std::lock_guard<std::mutex> g(P.mu);
+    auto it = P.live.find((uintptr_t)p);
+    if (it == P.live.end()) return MDG_INVALID_ARGUMENT;
+    P.free_blocks[it->second].push_back(p);
+    P.live.erase(it);
+    return MDG_OK;
+}
+
+// every [rows[i], rows[i] + bytes) inside one live page-locked block
+bool pinned_rows(const double* const* rows, size_t b, size_t bytes) {
+    PinnedPool& P = pinned_pool();
+    std::lock_guard<std::mutex> g(P.mu);
+    if (P.live.empty()) return false;
+    for (size_t i = 0; i < b; ++i) {
+        const uintptr_t a = (uintptr_t)rows[i];
+        auto it = P.live.upper_bound(a);
+        if (it == P.live.begin()) return false;
+        --it;
+        if (a + bytes > it->first + it->second) return false;
+    }
+    return true;
+}
 
 int ensure_workspace(mdg_ctx* c, int B, int N, int n_ignore) {
     const int igcap = std::max(kIgnoreRow, (n_ignore + kIgnoreRow - 1) / kIgnoreRow * kIgnoreRow);
@@ -641,6 +738,14 @@ int mdg_device_count(int* count) {
     return MDG_OK;
 }
 
+int mdg_host_alloc(int device, size_t bytes, void** out) {
+    if (!out || bytes == 0) return MDG_INVALID_ARGUMENT;
+    *out = nullptr;
+    return pinned_alloc(device, bytes, out);
+}
+
+int mdg_host_free(void* p) { return pinned_free(p); }
+
 int mdg_ctx_create(int device, mdg_ctx** out) {
     if (!out) return MDG_INVALID_ARGUMENT;
     *out = nullptr;
@@ -682,6 +787,7 @@ int mdg_ctx_destroy(mdg_ctx* c) {
             if (c->ring[k]) (void)hipHostFree(c->ring[k]);
             if (c->ring_ev[k]) (void)hipEventDestroy(c->ring_ev[k]);
         }
+        if (c->hsmall) (void)hipHostFree(c->hsmall);
         if (c->own) (void)hipStreamDestroy(c->own);
     }
     if (c->counted) g_live_ctx[c->device].fetch_sub(1);
@@ -979,6 +1085,19 @@ static int upload_rows(mdg_ctx* c, hipStream_t st, char* dst, const double* cons
                        size_t row_bytes) {
     const size_t total = b * row_bytes;
     if (total == 0) return MDG_OK;
+    if (pinned_rows(rows, b, row_bytes)) {
+        // rows in mdg_host_alloc memory: DMA straight from them, one copy per run of
+        // adjacent rows (the call synchronises before it returns, so the rows are
+        // read before the caller can release them)
+        for (size_t r = 0; r < b;) {
+            size_t e = r + 1;
+            while (e < b && (const char*)rows[e] == (const char*)rows[e - 1] + row_bytes) ++e;
+            HIPCHK(hipMemcpyAsync(dst + r * row_bytes, rows[r], (e - r) * row_bytes,
+                                  hipMemcpyHostToDevice, st));
+            r = e;
+        }
+        return MDG_OK;
+    }
     const size_t want = std::min(kRingSlot, (total + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1));
     if (c->ring_bytes < want) {
         for (int k = 0; k < 2; ++k) {
@@ -1036,8 +1155,30 @@ static int batch_host(mdg_ctx* c, size_t b, size_t n, bool shared_x, Upload uplo
     if ((rc = ensure(c->st_status, b * 4))) return rc;
     double* dx = (double*)c->st_x.p;
     double* dy = (double*)c->st_y.p;
+    // page-locked scratch: [sb: 16 b][mse: 8 b][counts: 4 b][statuses: 4 b]
+    const size_t hs_need = b * 32;
+    if (c->hsmall_busy) {
+        HIPCHK(hipStreamSynchronize(st));
+        c->hsmall_busy = false;
+    }
+    if (c->hsmall_bytes < hs_need) {
+        if (c->hsmall) {
+            HIPCHK(hipHostFree(c->hsmall));
+            c->hsmall = nullptr;
+            c->hsmall_bytes = 0;
+        }
+        const size_t want = std::max<size_t>(hs_need, 64 * 32);
+        HIPCHK(hipHostMalloc(&c->hsmall, want, hipHostMallocDefault));
+        c->hsmall_bytes = want;
+    }
+    double* h_sb = (double*)c->hsmall;
+    double* h_mse = h_sb + 2 * b;
+    int32_t* h_cnt = (int32_t*)(h_mse + b);
+    int32_t* h_st = h_cnt + b;
     if ((rc = upload(dx, dy, st))) return rc;
-    HIPCHK(hipMemcpyAsync(c->st_sb.p, sb, b * 16, hipMemcpyHostToDevice, st));
+    std::memcpy(h_sb, sb, b * 16);
+    c->hsmall_busy = true;
+    HIPCHK(hipMemcpyAsync(c->st_sb.p, h_sb, b * 16, hipMemcpyHostToDevice, st));
     BatchArgs a;
     if ((rc = fill_args(c, a, b, n, dx, shared_x ? 0 : n, dy, n, (const double*)c->st_sb.p, ignore,
                         n_ignore, (double*)c->st_out.p, cap, (int32_t*)c->st_cnt.p, (double*)c->st_mse.p,
@@ -1045,11 +1186,14 @@ static int batch_host(mdg_ctx* c, size_t b, size_t n, bool shared_x, Upload uplo
         return rc;
     rc = run_pipeline(c, a, s);
     if (rc) return rc;
-    std::vector<int32_t> cnt(b), stv(b);
-    HIPCHK(hipMemcpyAsync(cnt.data(), c->st_cnt.p, b * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(stv.data(), c->st_status.p, b * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(mse, c->st_mse.p, b * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(h_cnt, c->st_cnt.p, b * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(h_st, c->st_status.p, b * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(h_mse, c->st_mse.p, b * 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    c->hsmall_busy = false;
+    std::memcpy(mse, h_mse, b * 8);
+    const int32_t* cnt = h_cnt;
+    const int32_t* stv = h_st;
     // only the rows the spectra filled travel back (cap is usually N/2 + 2 rows,
     // 1.5 MiB per 131072-point spectrum, against ~24 KiB of Lorentzians)
     size_t rows = 0;

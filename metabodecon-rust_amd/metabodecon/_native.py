@@ -9,6 +9,7 @@ from __future__ import annotations
 import ctypes
 import os
 import threading
+import weakref
 
 import numpy as np
 
@@ -39,6 +40,7 @@ STAGE_NAMES = ["prep", "smooth", "detect", "select", "fit_init", "fit_superposit
 EXPORTS = [
     "mdg_abi_version", "mdg_build_info", "mdg_strerror", "mdg_settings_default", "mdg_settings_validate",
     "mdg_ignore_region_add", "mdg_synth_lorentzians", "mdg_synth_noise", "mdg_device_count",
+    "mdg_host_alloc", "mdg_host_free",
     "mdg_ctx_create", "mdg_ctx_destroy", "mdg_ctx_set_stream", "mdg_ctx_synchronize",
     "mdg_ctx_set_profiling", "mdg_ctx_stage_times", "mdg_ctx_reset_stage_times",
     "mdg_deconvolute", "mdg_deconvolute_batch", "mdg_deconvolute_rows", "mdg_deconvolute_batch_device",
@@ -219,6 +221,8 @@ def _declare(L):
                                            ctypes.c_double, _dp]
     L.mdg_synth_noise.argtypes = [ctypes.c_uint64, _sz, ctypes.c_double, _dp]
     L.mdg_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
+    L.mdg_host_alloc.argtypes = [ctypes.c_int, _sz, ctypes.POINTER(_vp)]
+    L.mdg_host_free.argtypes = [_vp]
     L.mdg_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(_vp)]
     L.mdg_ctx_destroy.argtypes = [_vp]
     L.mdg_ctx_set_stream.argtypes = [_vp, _vp]
@@ -284,6 +288,51 @@ def ptr(a: np.ndarray, t=_dp):
     return a.ctypes.data_as(t)
 
 
+_pinned_off = False  # no engine library or no device: ordinary memory from now on
+
+
+def pinned_empty(shape, dtype=np.float64, device: int | None = None) -> np.ndarray | None:
+    """An uninitialised C-contiguous array in page-locked host memory
+    (mdg_host_alloc), released when the last view of it goes; None without the engine
+    library or a device, or beyond MDGPU_PINNED_MAX, and the caller then keeps
+    ordinary memory. The host-buffer calls DMA straight from and into such arrays
+    (no bounce copy through the context's ring)."""
+    global _pinned_off
+    if _pinned_off:
+        return None
+    dt = np.dtype(dtype)
+    count = int(np.prod(shape))
+    nbytes = count * dt.itemsize
+    if nbytes == 0:
+        return None
+    try:
+        L = lib()
+        if device is None:
+            device = default_device()
+    except (NativeLibraryError, OSError):
+        _pinned_off = True
+        return None
+    p = _vp()
+    st = L.mdg_host_alloc(device, nbytes, ctypes.byref(p))
+    if st:
+        if st == ERR_NO_DEVICE:
+            _pinned_off = True
+        return None
+    buf = (ctypes.c_char * nbytes).from_address(p.value)
+    weakref.finalize(buf, L.mdg_host_free, _vp(p.value))
+    return np.frombuffer(buf, dtype=dt, count=count).reshape(shape)
+
+
+def pinned_copy(a) -> np.ndarray:
+    """A C-contiguous f64 copy of `a`, page-locked when pinned_empty can give it."""
+    src = np.asarray(a, dtype=np.float64).reshape(-1)
+    out = pinned_empty(src.shape)
+    if out is None:
+        return np.array(src, dtype=np.float64, copy=True)
+    out[...] = src
+    return out
+
+
 class Context:
     """One device context (stream + reusable HBM workspace) of libmdgpu."""
 
@@ -316,7 +365,10 @@ class Context:
         buf = self._host.get(name)
         if buf is None or buf.nbytes < need:
             size = max(need, 2 * buf.nbytes if buf is not None else 0)
-            buf = np.empty(size, dtype=np.uint8)
+            # page-locked when possible: the results come back by DMA
+            buf = pinned_empty((size,), np.uint8, self.device)
+            if buf is None:
+                buf = np.empty(size, dtype=np.uint8)
             self._host[name] = buf
         return buf[:need].view(dt).reshape(shape)
 

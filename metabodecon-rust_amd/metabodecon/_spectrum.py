@@ -17,6 +17,7 @@ import operator
 
 import numpy as np
 
+from . import _native
 from . import _serde as serde
 from . import exceptions as exc
 from ._bruker import MetadataError, bruker_set_paths, read_bruker_arrays
@@ -99,8 +100,10 @@ def _validate_boundaries(sb, cs: np.ndarray, mono: str) -> tuple[float, float]:
 
 class Spectrum:
     def __init__(self, chemical_shifts, intensities, signal_boundaries):
-        cs = np.array(chemical_shifts, dtype=np.float64, copy=True).reshape(-1)
-        it = np.array(intensities, dtype=np.float64, copy=True).reshape(-1)
+        # the spectrum's own rows, page-locked when the engine can give such memory:
+        # the host-buffer calls then DMA straight from them (mdg_host_alloc)
+        cs = _native.pinned_copy(chemical_shifts)
+        it = _native.pinned_copy(intensities)
         # validate_lengths (spectrum.rs:779-799)
         if cs.size == 0 or it.size == 0:
             raise exc.EmptyData(
