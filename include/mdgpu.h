@@ -11,6 +11,8 @@
  *                                 deconvoluter.rs:651-661 / :700-710 (per-spectrum status;
  *                                 the caller reproduces the fail-fast Result collect)
  *   mdg_deconvolute_rows       same, one pointer per spectrum row (no caller-side stacking)
+ *   mdg_deconvolute_rows_i32   same, rows in the Bruker reader's compact form (int32 samples,
+ *                                axis formula; spectrum/formats/bruker.rs:278-280, :459-470)
  *   mdg_deconvolute_batch_device  same, inputs/outputs resident in HBM (no PCIe in the call)
  *   mdg_superposition_vec      <- Lorentzian::{superposition_vec,par_superposition_vec}
  *                                 deconvolution/lorentzian.rs:631-663
@@ -182,6 +184,21 @@ int mdg_deconvolute_rows(mdg_ctx* ctx, size_t b, size_t n, const double* const* 
                          const double* const* y_rows, const double* sb, const mdg_settings* s,
                          const double* ignore, size_t n_ignore, mdg_lorentzian* out, size_t cap,
                          size_t* counts, double* mse, int* status);
+
+/* Same with the rows in the compact form the Bruker reader builds them from, decoded
+ * on the device bit for bit (the reference builds the f64 rows on the host,
+ * spectrum/formats/bruker.rs:278-280 and :459-470, then calls the same
+ * deconvoluter.rs:651-661 / :700-710): spectrum i's axis is
+ *   x_j = axes[3i] - ((double)j * axes[3i+1]) / axes[3i+2]   (maximum, width, SI - 1),
+ * evaluated in that operation order, and its intensities y_j = (double)y_rows[i][j] *
+ * y_scale[i] (the 1r int32 samples times 2^NC_proc). A quarter of the bytes of
+ * mdg_deconvolute_rows cross PCIe (n int32 per spectrum, no axis row); page-locked
+ * rows (mdg_host_alloc) go by DMA straight from where they are. */
+int mdg_deconvolute_rows_i32(mdg_ctx* ctx, size_t b, size_t n, const double* axes,
+                             const int32_t* const* y_rows, const double* y_scale, const double* sb,
+                             const mdg_settings* s, const double* ignore, size_t n_ignore,
+                             mdg_lorentzian* out, size_t cap, size_t* counts, double* mse,
+                             int* status);
 
 /* Same, every array resident on the context's device (d_ prefix); enqueued on
  * the context stream without any host synchronisation (capturable). d_counts and

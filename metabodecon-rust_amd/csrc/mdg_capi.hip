@@ -88,6 +88,7 @@ struct mdg_ctx {
     Workspace w{};
     // staging for the host-pointer API
     Buffer st_x, st_y, st_sb, st_out, st_cnt, st_mse, st_status, st_L, st_sup, st_flag;
+    Buffer st_raw, st_desc;  // mdg_deconvolute_rows_i32: int32 rows and their descriptors
     // page-locked host ring for mdg_deconvolute_rows: the rows are gathered into a
     // slot and sent with one asynchronous DMA per slot (upload_rows)
     void* ring[2] = {nullptr, nullptr};
@@ -259,7 +260,7 @@ int pinned_free(void* p) {
 }
 
 // every [rows[i], rows[i] + bytes) inside one live page-locked block
-bool pinned_rows(const double* const* rows, size_t b, size_t bytes) {
+bool pinned_rows(const void* const* rows, size_t b, size_t bytes) {
     PinnedPool& P = pinned_pool();
     std::lock_guard<std::mutex> g(P.mu);
     if (P.live.empty()) return false;
@@ -781,7 +782,8 @@ int mdg_ctx_destroy(mdg_ctx* c) {
         for (Buffer& b : c->opt)
             if (b.p) (void)hipFree(b.p);
         for (Buffer* b : {&c->arena, &c->chain, &c->chain_flags, &c->ign, &c->st_x, &c->st_y, &c->st_sb, &c->st_out, &c->st_cnt,
-                          &c->st_mse, &c->st_status, &c->st_L, &c->st_sup, &c->st_flag})
+                          &c->st_mse, &c->st_status, &c->st_L, &c->st_sup, &c->st_flag, &c->st_raw,
+                          &c->st_desc})
             if (b->p) (void)hipFree(b->p);
         for (int k = 0; k < 2; ++k) {
             if (c->ring[k]) (void)hipHostFree(c->ring[k]);
@@ -1081,7 +1083,7 @@ int mdg_deconvolute_batch_device(mdg_ctx* c, size_t b, size_t n, const double* d
 // default 4 queues: ~4.0k spectra/s with per-row copies against ~5.5-6.1k with one
 // copy of a stacked buffer).
 constexpr size_t kRingSlot = 32u << 20;
-static int upload_rows(mdg_ctx* c, hipStream_t st, char* dst, const double* const* rows, size_t b,
+static int upload_rows(mdg_ctx* c, hipStream_t st, char* dst, const void* const* rows, size_t b,
                        size_t row_bytes) {
     const size_t total = b * row_bytes;
     if (total == 0) return MDG_OK;
@@ -1155,8 +1157,9 @@ static int batch_host(mdg_ctx* c, size_t b, size_t n, bool shared_x, Upload uplo
     if ((rc = ensure(c->st_status, b * 4))) return rc;
     double* dx = (double*)c->st_x.p;
     double* dy = (double*)c->st_y.p;
-    // page-locked scratch: [sb: 16 b][mse: 8 b][counts: 4 b][statuses: 4 b]
-    const size_t hs_need = b * 32;
+    // page-locked scratch: [sb: 16 b][mse: 8 b][counts: 4 b][statuses: 4 b][the
+    // upload's own descriptors: 32 b (mdg_deconvolute_rows_i32)]
+    const size_t hs_need = b * 64;
     if (c->hsmall_busy) {
         HIPCHK(hipStreamSynchronize(st));
         c->hsmall_busy = false;
@@ -1167,7 +1170,7 @@ static int batch_host(mdg_ctx* c, size_t b, size_t n, bool shared_x, Upload uplo
             c->hsmall = nullptr;
             c->hsmall_bytes = 0;
         }
-        const size_t want = std::max<size_t>(hs_need, 64 * 32);
+        const size_t want = std::max<size_t>(hs_need, 64 * 64);
         HIPCHK(hipHostMalloc(&c->hsmall, want, hipHostMallocDefault));
         c->hsmall_bytes = want;
     }
@@ -1175,9 +1178,9 @@ static int batch_host(mdg_ctx* c, size_t b, size_t n, bool shared_x, Upload uplo
     double* h_mse = h_sb + 2 * b;
     int32_t* h_cnt = (int32_t*)(h_mse + b);
     int32_t* h_st = h_cnt + b;
+    c->hsmall_busy = true;
     if ((rc = upload(dx, dy, st))) return rc;
     std::memcpy(h_sb, sb, b * 16);
-    c->hsmall_busy = true;
     HIPCHK(hipMemcpyAsync(c->st_sb.p, h_sb, b * 16, hipMemcpyHostToDevice, st));
     BatchArgs a;
     if ((rc = fill_args(c, a, b, n, dx, shared_x ? 0 : n, dy, n, (const double*)c->st_sb.p, ignore,
@@ -1253,8 +1256,48 @@ int mdg_deconvolute_rows(mdg_ctx* c, size_t b, size_t n, const double* const* x_
         shared = shared && x_rows[i] == x_rows[0];
     }
     auto upload = [&](double* dx, double* dy, hipStream_t st) -> int {
-        int rc = upload_rows(c, st, (char*)dx, x_rows, shared ? 1 : b, n * 8);
-        return rc ? rc : upload_rows(c, st, (char*)dy, y_rows, b, n * 8);
+        int rc = upload_rows(c, st, (char*)dx, (const void* const*)x_rows, shared ? 1 : b, n * 8);
+        return rc ? rc : upload_rows(c, st, (char*)dy, (const void* const*)y_rows, b, n * 8);
+    };
+    return batch_host(c, b, n, shared, upload, sb, s, ignore, n_ignore, out, cap, counts, mse, status);
+}
+
+int mdg_deconvolute_rows_i32(mdg_ctx* c, size_t b, size_t n, const double* axes,
+                             const int32_t* const* y_rows, const double* y_scale, const double* sb,
+                             const mdg_settings* s, const double* ignore, size_t n_ignore,
+                             mdg_lorentzian* out, size_t cap, size_t* counts, double* mse, int* status) {
+    if (!c) return MDG_INVALID_ARGUMENT;
+    int v = validate_common(s, n_ignore, ignore);
+    if (v) return v;
+    if (b == 0) return MDG_OK;
+    if (n < 2 || n > (size_t)INT32_MAX / 2 || b > (size_t)INT32_MAX) return MDG_INVALID_ARGUMENT;
+    if (!axes || !y_rows || !y_scale || !sb || !counts || !mse || !status || (!out && cap))
+        return MDG_INVALID_ARGUMENT;
+    bool shared = true;
+    for (size_t i = 0; i < b; ++i) {
+        if (!y_rows[i]) return MDG_INVALID_ARGUMENT;
+        for (int k = 0; k < 3; ++k)
+            if (!std::isfinite(axes[3 * i + k])) return MDG_INVALID_ARGUMENT;
+        if (axes[3 * i + 2] == 0.0 || !std::isfinite(y_scale[i])) return MDG_INVALID_ARGUMENT;
+        shared = shared && std::memcmp(axes + 3 * i, axes, 3 * sizeof(double)) == 0;
+    }
+    auto upload = [&](double* dx, double* dy, hipStream_t st) -> int {
+        int rc;
+        if ((rc = ensure(c->st_raw, b * n * 4))) return rc;
+        if ((rc = ensure(c->st_desc, b * 32))) return rc;
+        if ((rc = upload_rows(c, st, (char*)c->st_raw.p, (const void* const*)y_rows, b, n * 4))) return rc;
+        double* h = (double*)c->hsmall + 4 * b;  // batch_host's scratch, descriptor part
+        for (size_t i = 0; i < b; ++i) {
+            h[4 * i] = axes[3 * i];
+            h[4 * i + 1] = axes[3 * i + 1];
+            h[4 * i + 2] = axes[3 * i + 2];
+            h[4 * i + 3] = y_scale[i];
+        }
+        HIPCHK(hipMemcpyAsync(c->st_desc.p, h, b * 32, hipMemcpyHostToDevice, st));
+        launch_decode_rows_i32((const int32_t*)c->st_raw.p, (const double*)c->st_desc.p, (int)b,
+                               (int64_t)n, shared ? 1 : 0, dx, dy, st);
+        HIPCHK(hipGetLastError());
+        return MDG_OK;
     };
     return batch_host(c, b, n, shared, upload, sb, s, ignore, n_ignore, out, cap, counts, mse, status);
 }

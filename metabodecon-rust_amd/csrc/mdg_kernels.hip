@@ -4612,6 +4612,35 @@ void launch_queue_scatter(const QueueItem* items, int B, const double* out, int6
                        mse, status);
 }
 
+// Compact host rows (mdg_deconvolute_rows_i32) decoded into the staging rows, bit for
+// bit what the Bruker reader builds on the host (bruker.rs:278-280, :459-470):
+// x_i = maximum - (i * width) / divisor in that operation order (three IEEE
+// operations, none contracted: the build has -ffp-contract=off), and y_i = raw_i *
+// scale (int32 -> f64 exact, scale a power of two: exact). desc holds per spectrum
+// {maximum, width, divisor, scale}; only the first spectrum's axis when shared_x.
+__global__ __launch_bounds__(256) void k_decode_rows_i32(const int32_t* __restrict__ raw,
+                                                         const double* __restrict__ desc, int64_t n,
+                                                         int shared_x, double* __restrict__ x_rows,
+                                                         double* __restrict__ y_rows) {
+    const int s = blockIdx.y;
+    const double mx = desc[4 * s], wd = desc[4 * s + 1], dv = desc[4 * s + 2], sc = desc[4 * s + 3];
+    const int32_t* r = raw + (size_t)s * n;
+    double* yr = y_rows + (size_t)s * n;
+    double* xr = x_rows + (size_t)s * n;
+    const bool do_x = !shared_x || s == 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        yr[i] = (double)r[i] * sc;
+        if (do_x) xr[i] = mx - ((double)i * wd) / dv;
+    }
+}
+void launch_decode_rows_i32(const int32_t* raw, const double* desc, int B, int64_t n, int shared_x,
+                            double* x_rows, double* y_rows, hipStream_t st) {
+    const unsigned gx = std::max(1u, std::min(cdiv(n, 1024), 128u));
+    hipLaunchKernelGGL(k_decode_rows_i32, dim3(gx, B), dim3(256), 0, st, raw, desc, n, shared_x,
+                       x_rows, y_rows);
+}
+
 }  // namespace mdg
 
 #ifdef MDG_DIAG

@@ -192,5 +192,9 @@ void launch_queue_gather(const QueueItem* items, int B, int64_t n, int gather_x,
 void launch_queue_scatter(const QueueItem* items, int B, const double* out, int64_t stage_cap,
                           const int32_t* counts, const double* mse, const int32_t* status,
                           hipStream_t st);
+// compact host rows (mdg_deconvolute_rows_i32) into B x n f64 staging rows: the
+// Bruker axis from {maximum, width, divisor} and int32 samples times a power of two
+void launch_decode_rows_i32(const int32_t* raw, const double* desc, int B, int64_t n, int shared_x,
+                            double* x_rows, double* y_rows, hipStream_t st);
 
 }  // namespace mdg

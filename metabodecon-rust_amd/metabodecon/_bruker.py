@@ -73,6 +73,12 @@ def read_bruker_arrays(path: str, experiment: int, processing: int):
             raise MetadataError("MissingData", one_r_path, "1r")
         intensities = raw.astype(np.float64)
     meta = {"nucleus": acqus["nucleus"], "frequency": acqus["frequency"]}
+    if procs["data_type"] == 0:
+        # the compact form the rows were built from (mdg_deconvolute_rows_i32 decodes
+        # it on the device bit for bit): int32 samples, their power-of-two scale, and
+        # the axis operands (maximum, width, SI - 1) of the formula above
+        meta["raw"] = (raw.astype(np.int32, copy=False), float(2.0 ** procs["exponent"]),
+                       (float(procs["maximum"]), float(acqus["width"]), float(si) - 1.0))
     return chemical_shifts, intensities, meta
 
 

@@ -415,19 +415,35 @@ class Deconvoluter:
         counts = np.zeros(b, dtype=np.uintp)
         mse = np.zeros(b)
         status = np.zeros(b, dtype=np.intc)
-        # each spectrum's own rows, by pointer (mdg_deconvolute_rows gathers them into
-        # its page-locked ring and sends one DMA per slot): no stacking copy here
-        xr = np.array([spectra[i].chemical_shifts.ctypes.data for i in idx], dtype=np.uintp)
-        yr = np.array([spectra[i].intensities.ctypes.data for i in idx], dtype=np.uintp)
+        raws = [spectra[i]._raw for i in idx]
+        compact = all(r is not None for r in raws)
+        if compact:
+            # Bruker rows in the compact form they were read from (int32 samples, the
+            # axis formula): a quarter of the bytes, decoded on the device bit for bit
+            yr = np.array([r[0].ctypes.data for r in raws], dtype=np.uintp)
+            axes = np.array([r[2] for r in raws], dtype=np.float64)
+            scale = np.array([r[1] for r in raws], dtype=np.float64)
+        else:
+            # each spectrum's own rows, by pointer (page-locked rows go by DMA straight
+            # from where they are, others through the context's page-locked ring): no
+            # stacking copy here
+            xr = np.array([spectra[i].chemical_shifts.ctypes.data for i in idx], dtype=np.uintp)
+            yr = np.array([spectra[i].intensities.ctypes.data for i in idx], dtype=np.uintp)
         with ctx.lock:  # ctypes drops the GIL for the call: lanes run concurrently
             # the result rows: the context's own host buffer, kept across calls
             out = ctx.host_rows("out", (b, cap, 3))
-            rc = nat.lib().mdg_deconvolute_rows(
-                ctx.handle, b, n, xr.ctypes.data_as(ctypes.POINTER(nat._dp)),
-                yr.ctypes.data_as(ctypes.POINTER(nat._dp)), nat.ptr(sb),
-                ctypes.byref(self._s), nat.ptr(ign) if ign.size else None, ign.size // 2,
-                nat.ptr(out), cap, nat.ptr(counts, nat._szp), nat.ptr(mse),
-                status.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+            ig = (nat.ptr(ign) if ign.size else None, ign.size // 2)
+            tail = (nat.ptr(out), cap, nat.ptr(counts, nat._szp), nat.ptr(mse),
+                    status.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+            if compact:
+                rc = nat.lib().mdg_deconvolute_rows_i32(
+                    ctx.handle, b, n, nat.ptr(axes), yr.ctypes.data_as(ctypes.POINTER(nat._i32p)),
+                    nat.ptr(scale), nat.ptr(sb), ctypes.byref(self._s), *ig, *tail)
+            else:
+                rc = nat.lib().mdg_deconvolute_rows(
+                    ctx.handle, b, n, xr.ctypes.data_as(ctypes.POINTER(nat._dp)),
+                    yr.ctypes.data_as(ctypes.POINTER(nat._dp)), nat.ptr(sb),
+                    ctypes.byref(self._s), *ig, *tail)
             if rc >= 100 or rc == nat.INVALID_ARGUMENT:
                 raise exc.UnexpectedError(f"GPU engine failure: {nat.strerror(rc)}")
             # copied out while the rows are still this call's

@@ -102,8 +102,26 @@ class Spectrum:
     def __init__(self, chemical_shifts, intensities, signal_boundaries):
         # the spectrum's own rows, page-locked when the engine can give such memory:
         # the host-buffer calls then DMA straight from them (mdg_host_alloc)
-        cs = _native.pinned_copy(chemical_shifts)
-        it = _native.pinned_copy(intensities)
+        self._init(_native.pinned_copy(chemical_shifts), _native.pinned_copy(intensities),
+                   signal_boundaries)
+
+    @classmethod
+    def _adopt(cls, cs: np.ndarray, it: np.ndarray, signal_boundaries) -> "Spectrum":
+        """A Spectrum that takes `cs` / `it` as its own rows (fresh f64 arrays the
+        caller gives up), validated like the constructor; no copy."""
+        s = cls.__new__(cls)
+        s._init(cs, it, signal_boundaries)
+        return s
+
+    def _set_raw(self, row: np.ndarray, scale: float, axis: tuple) -> None:
+        """The compact form the Bruker reader built the rows from: intensities =
+        row * scale, chemical shifts = axis[0] - (i * axis[1]) / axis[2] (bruker.rs:
+        278-280, :459-470). The host-buffer calls send it instead of the f64 rows."""
+        row.setflags(write=False)
+        self._raw = (row, float(scale), tuple(float(v) for v in axis))
+
+    def _init(self, cs: np.ndarray, it: np.ndarray, signal_boundaries) -> None:
+        self._raw = None
         # validate_lengths (spectrum.rs:779-799)
         if cs.size == 0 or it.size == 0:
             raise exc.EmptyData(
@@ -233,7 +251,18 @@ class Spectrum:
             cs, it, meta = read_bruker_arrays(path, experiment, processing)
         except MetadataError as e:
             raise getattr(exc, e.kind, exc.SpectrumError)(str(e)) from None
-        s = Spectrum(cs, it, signal_boundaries)
+        raw = meta.get("raw")
+        if raw is not None:  # the GPU reads the compact rows: x / y stay ordinary memory
+            s = Spectrum._adopt(np.asarray(cs, dtype=np.float64), np.asarray(it, dtype=np.float64),
+                                signal_boundaries)
+            row = _native.pinned_empty(raw[0].shape, np.int32)
+            if row is None:
+                row = np.array(raw[0], dtype=np.int32)
+            else:
+                row[...] = raw[0]
+            s._set_raw(row, raw[1], raw[2])
+        else:
+            s = Spectrum(cs, it, signal_boundaries)
         s.nucleus = meta["nucleus"]
         s.frequency = meta["frequency"]
         return s
@@ -241,8 +270,13 @@ class Spectrum:
     @staticmethod
     def read_bruker_set(path: str, experiment: int, processing: int,
                         signal_boundaries) -> list["Spectrum"]:
-        return [Spectrum.read_bruker(p, experiment, processing, signal_boundaries)
-                for p in bruker_set_paths(path)]
+        arrays = []
+        for p in bruker_set_paths(path):
+            try:
+                arrays.append(read_bruker_arrays(p, experiment, processing))
+            except MetadataError as e:
+                raise getattr(exc, e.kind, exc.SpectrumError)(str(e)) from None
+        return _set_of_rows(arrays, signal_boundaries)
 
 
     @staticmethod
@@ -361,3 +395,52 @@ class Spectrum:
     def __repr__(self) -> str:
         return (f"Spectrum(n={self._cs.size}, range=({self._cs[0]}, {self._cs[-1]}), "
                 f"signal_boundaries={self._sb})")
+
+
+def _set_of_rows(arrays, signal_boundaries) -> list[Spectrum]:
+    """Spectra of a set read together ((chemical shifts, intensities, meta) each),
+    their rows laid out in one page-locked block per length, so consecutive spectra
+    of a batch are adjacent rows and travel in one DMA (mdg_deconvolute_rows[_i32]):
+    the int32 sample rows of Bruker data [r_0 .. r_k-1] (the f64 rows then stay
+    ordinary memory), else [x_0 .. x_k-1][y_0 .. y_k-1]. Ordinary copies without
+    the engine's memory."""
+    by_n: dict[tuple, list[int]] = {}
+    for i, (cs, it, meta) in enumerate(arrays):
+        if cs.ndim == 1 and cs.size == it.size and cs.size > 0:
+            by_n.setdefault((cs.size, meta.get("raw") is not None), []).append(i)
+    rows: dict[int, tuple] = {}  # spectrum -> its rows in a shared block
+    for (n, compact), idx in by_n.items():
+        if len(idx) < 2:
+            continue
+        blk = _native.pinned_empty((len(idx), n), np.int32) if compact else \
+            _native.pinned_empty((2, len(idx), n))
+        if blk is not None:
+            for r, i in enumerate(idx):
+                rows[i] = (blk[r],) if compact else (blk[0, r], blk[1, r])
+    out = []
+    for i, (cs, it, meta) in enumerate(arrays):  # in order: the first error is raised
+        raw = meta.get("raw")
+        if raw is not None:
+            s = Spectrum._adopt(np.asarray(cs, dtype=np.float64), np.asarray(it, dtype=np.float64),
+                                signal_boundaries)
+            if i in rows:
+                row = rows[i][0]
+                row[...] = raw[0]
+            else:
+                row = _native.pinned_empty(raw[0].shape, np.int32)
+                if row is None:
+                    row = np.array(raw[0], dtype=np.int32)
+                else:
+                    row[...] = raw[0]
+            s._set_raw(row, raw[1], raw[2])
+        elif i in rows:
+            xr, yr = rows[i]
+            xr[...] = cs
+            yr[...] = it
+            s = Spectrum._adopt(xr, yr, signal_boundaries)
+        else:
+            s = Spectrum(cs, it, signal_boundaries)
+        s.nucleus = meta["nucleus"]
+        s.frequency = meta["frequency"]
+        out.append(s)
+    return out

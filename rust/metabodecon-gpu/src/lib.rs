@@ -111,6 +111,8 @@ pub mod ffi {
             n_out: *mut usize,
         ) -> c_int;
         pub fn mdg_device_count(count: *mut c_int) -> c_int;
+        pub fn mdg_host_alloc(device: c_int, bytes: usize, out: *mut *mut c_void) -> c_int;
+        pub fn mdg_host_free(p: *mut c_void) -> c_int;
         pub fn mdg_ctx_create(device: c_int, out: *mut *mut MdgCtx) -> c_int;
         pub fn mdg_ctx_destroy(ctx: *mut MdgCtx) -> c_int;
         pub fn mdg_ctx_set_stream(ctx: *mut MdgCtx, hip_stream: *mut c_void) -> c_int;
@@ -154,6 +156,23 @@ pub mod ffi {
             n: usize,
             x_rows: *const *const f64,
             y_rows: *const *const f64,
+            sb: *const f64,
+            s: *const MdgSettings,
+            ignore: *const f64,
+            n_ignore: usize,
+            out: *mut MdgLorentzian,
+            cap: usize,
+            counts: *mut usize,
+            mse: *mut f64,
+            status: *mut c_int,
+        ) -> c_int;
+        pub fn mdg_deconvolute_rows_i32(
+            ctx: *mut MdgCtx,
+            b: usize,
+            n: usize,
+            axes: *const f64,
+            y_rows: *const *const i32,
+            y_scale: *const f64,
             sb: *const f64,
             s: *const MdgSettings,
             ignore: *const f64,

@@ -42,23 +42,113 @@ def _check(decs, which):
 
 
 @pytest.mark.parametrize("lanes", [1, 2])
-def test_pinned_pageable_and_mixed_rows_match_goldens(lanes, monkeypatch):
-    """The 16 blood spectra three ways: every row page-locked (direct DMA), every
-    row in ordinary memory (the ring), and the two mixed in one call (the ring);
-    one batch of 16 (1 lane) and two concurrent lanes of 8."""
+def test_compact_pinned_pageable_and_mixed_rows_match_goldens(lanes, monkeypatch):
+    """The 16 blood spectra four ways: as read (the int32 sample rows in one
+    page-locked block, mdg_deconvolute_rows_i32 decoding them on the device), as f64
+    rows in page-locked memory (direct DMA), as f64 rows in ordinary memory (the
+    ring), and compact and f64 spectra mixed in one call (the f64 rows path); one
+    batch of 16 (1 lane) and two concurrent lanes of 8."""
     import metabodecon as md
     monkeypatch.setattr(md.Deconvoluter, "LANES", lanes)
-    pinned = _blood(md)
-    assert all(_pinned(s.chemical_shifts) and _pinned(s.intensities) for s in pinned)
+    read = _blood(md)
+    assert all(s._raw is not None and _pinned(s._raw[0]) for s in read)
+    _check(md.Deconvoluter().par_deconvolute_spectra(read), range(16))
+    pinned = [md.Spectrum(s.chemical_shifts, s.intensities, s.signal_boundaries) for s in read]
+    assert all(s._raw is None and _pinned(s.intensities) for s in pinned)
     _check(md.Deconvoluter().par_deconvolute_spectra(pinned), range(16))
     monkeypatch.setattr(nat, "_pinned_off", True)
-    plain = _blood(md)
+    plain = [md.Spectrum(s.chemical_shifts, s.intensities, s.signal_boundaries) for s in read]
     assert not any(_pinned(s.intensities) for s in plain)
     _check(md.Deconvoluter().par_deconvolute_spectra(plain), range(16))
-    mixed = [pinned[k] if k % 3 else plain[k] for k in range(16)]
+    mixed = [read[k] if k % 3 else plain[k] for k in range(16)]
     _check(md.Deconvoluter().par_deconvolute_spectra(mixed), range(16))
-    # one spectrum through deconvolute_spectrum (mdg_deconvolute_rows with b = 1)
-    _check([md.Deconvoluter().deconvolute_spectrum(pinned[5])], [5])
+    # one spectrum through deconvolute_spectrum (b = 1), compact and f64
+    _check([md.Deconvoluter().deconvolute_spectrum(read[5])], [5])
+    _check([md.Deconvoluter().deconvolute_spectrum(plain[5])], [5])
+
+
+def test_compact_rows_decode_bit_exact():
+    """The device decode of the compact rows equals the reader's f64 rows: the
+    smoothed rows of mdg_deconvolute_rows_i32 equal the oracle's moving average of
+    the reader's intensities, and every result equals mdg_deconvolute_rows' on the
+    reader's f64 rows (a shared axis in one call, distinct axes in another)."""
+    import metabodecon as md
+    import oracle
+    read = _blood(md)
+    single = md.Spectrum.read_bruker(os.path.join(GOLDEN, "bruker", "blood", "blood_03"), 10, 10,
+                                     (-2.2, 11.8))
+    assert single._raw is not None and np.array_equal(single.intensities, read[2].intensities)
+    ctx = nat.context()
+    s = md.Deconvoluter().settings
+    n = len(read[0])
+    cap = n // 2 + 2
+    for group in ([0, 1, 2, 3], [2, 2, 2]):
+        spectra = [read[k] for k in group]
+        b = len(spectra)
+        sb = np.array([sp.signal_boundaries for sp in spectra], dtype=np.float64)
+
+        def run(compact):
+            out = np.zeros((b, cap, 3))
+            counts = np.zeros(b, dtype=np.uintp)
+            mse = np.zeros(b)
+            status = np.zeros(b, dtype=np.intc)
+            tail = (nat.ptr(out), cap, nat.ptr(counts, nat._szp), nat.ptr(mse),
+                    status.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+            if compact:
+                yr = np.array([sp._raw[0].ctypes.data for sp in spectra], dtype=np.uintp)
+                axes = np.array([sp._raw[2] for sp in spectra], dtype=np.float64)
+                scale = np.array([sp._raw[1] for sp in spectra], dtype=np.float64)
+                rc = nat.lib().mdg_deconvolute_rows_i32(
+                    ctx.handle, b, n, nat.ptr(axes), yr.ctypes.data_as(ctypes.POINTER(nat._i32p)),
+                    nat.ptr(scale), nat.ptr(sb), ctypes.byref(s), None, 0, *tail)
+            else:
+                xr = np.array([sp.chemical_shifts.ctypes.data for sp in spectra], dtype=np.uintp)
+                yr = np.array([sp.intensities.ctypes.data for sp in spectra], dtype=np.uintp)
+                rc = nat.lib().mdg_deconvolute_rows(
+                    ctx.handle, b, n, xr.ctypes.data_as(ctypes.POINTER(nat._dp)),
+                    yr.ctypes.data_as(ctypes.POINTER(nat._dp)), nat.ptr(sb), ctypes.byref(s),
+                    None, 0, *tail)
+            assert rc == 0 and not status.any()
+            return out, counts, mse
+        with ctx.lock:
+            c_out, c_counts, c_mse = run(True)
+            smoothed = [ctx.last_smoothed(k, n) for k in range(b)]
+            f_out, f_counts, f_mse = run(False)
+        for k, sp in enumerate(spectra):
+            assert np.array_equal(smoothed[k], oracle.moving_average(sp.intensities, s.smooth_iterations,
+                                                                     s.smooth_window)), k
+        assert np.array_equal(c_counts, f_counts) and np.array_equal(c_mse, f_mse)
+        assert np.array_equal(c_out, f_out)
+
+
+def test_compact_rows_reject_bad_descriptors():
+    """A zero divisor, a non-finite axis operand or scale, or a null row: invalid
+    argument, nothing run."""
+    import metabodecon as md
+    sp = _blood(md)[0]
+    ctx = nat.context()
+    n = len(sp)
+    cap = n // 2 + 2
+    out = np.zeros((1, cap, 3))
+    counts = np.zeros(1, dtype=np.uintp)
+    mse = np.zeros(1)
+    status = np.zeros(1, dtype=np.intc)
+    sb = np.array([sp.signal_boundaries], dtype=np.float64)
+    good_ax = np.array([sp._raw[2]], dtype=np.float64)
+    for ax, scale, row in ((good_ax * [1, 1, 0], 1.0, sp._raw[0].ctypes.data),
+                           (good_ax * [np.nan, 1, 1], 1.0, sp._raw[0].ctypes.data),
+                           (good_ax, np.inf, sp._raw[0].ctypes.data),
+                           (good_ax, 1.0, 0)):
+        yr = np.array([row], dtype=np.uintp)
+        sc = np.array([scale])
+        with ctx.lock:
+            rc = nat.lib().mdg_deconvolute_rows_i32(
+                ctx.handle, 1, n, nat.ptr(np.ascontiguousarray(ax)),
+                yr.ctypes.data_as(ctypes.POINTER(nat._i32p)), nat.ptr(sc), nat.ptr(sb),
+                ctypes.byref(md.Deconvoluter().settings), None, 0, nat.ptr(out), cap,
+                nat.ptr(counts, nat._szp), nat.ptr(mse),
+                status.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+        assert rc == nat.INVALID_ARGUMENT
 
 
 def test_pinned_blocks_are_reused_and_rows_released():
