@@ -37,14 +37,14 @@ ign = dec._ignore_array()
 n = len(S[0])
 for rep in range(3):
     print(f"rep {rep}: lanes {dec.LANES} par_deconvolute_spectra 16: %.3f ms" % med(lambda: dec.par_deconvolute_spectra(S)))
-    for b in (8, 16):
+    for b in (1, 8, 16):
         sub = S[:b]
         print(f"  B={b} stack x+y: %.3f ms" % med(lambda: (np.stack([s.chemical_shifts for s in sub]),
                                                          np.stack([s.intensities for s in sub]))))
         print(f"  B={b} _run_batch (one context): %.3f ms" % med(lambda: dec._run_batch(ctx, sub, list(range(b)), n, ign)))
         print(f"  B={b} deconvolute_spectra: %.3f ms" % med(lambda: dec.deconvolute_spectra(sub)))
 
-for b in (8, 16):
+for b in (1, 8, 16):
     sub = S[:b]
     ctx.reset_stage_times()
     ctx.set_profiling(True)
