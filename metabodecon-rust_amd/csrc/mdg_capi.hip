@@ -1152,9 +1152,12 @@ static int batch_host(mdg_ctx* c, size_t b, size_t n, bool shared_x, Upload uplo
     if ((rc = ensure(c->st_y, b * n * 8))) return rc;
     if ((rc = ensure(c->st_sb, b * 16))) return rc;
     if ((rc = ensure(c->st_out, std::max<size_t>(1, b * cap) * 24))) return rc;
-    if ((rc = ensure(c->st_cnt, b * 4))) return rc;
-    if ((rc = ensure(c->st_mse, b * 8))) return rc;
-    if ((rc = ensure(c->st_status, b * 4))) return rc;
+    // the per-spectrum results in one device row, [mse: 8 b][counts: 4 b][statuses:
+    // 4 b] like the host scratch below, so they come back in one copy
+    if ((rc = ensure(c->st_mse, b * 16))) return rc;
+    double* d_mse = (double*)c->st_mse.p;
+    int32_t* d_cnt = (int32_t*)(d_mse + b);
+    int32_t* d_st = d_cnt + b;
     double* dx = (double*)c->st_x.p;
     double* dy = (double*)c->st_y.p;
     // page-locked scratch: [sb: 16 b][mse: 8 b][counts: 4 b][statuses: 4 b][the
@@ -1184,14 +1187,11 @@ static int batch_host(mdg_ctx* c, size_t b, size_t n, bool shared_x, Upload uplo
     HIPCHK(hipMemcpyAsync(c->st_sb.p, h_sb, b * 16, hipMemcpyHostToDevice, st));
     BatchArgs a;
     if ((rc = fill_args(c, a, b, n, dx, shared_x ? 0 : n, dy, n, (const double*)c->st_sb.p, ignore,
-                        n_ignore, (double*)c->st_out.p, cap, (int32_t*)c->st_cnt.p, (double*)c->st_mse.p,
-                        (int32_t*)c->st_status.p)))
+                        n_ignore, (double*)c->st_out.p, cap, d_cnt, d_mse, d_st)))
         return rc;
     rc = run_pipeline(c, a, s);
     if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(h_cnt, c->st_cnt.p, b * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(h_st, c->st_status.p, b * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(h_mse, c->st_mse.p, b * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(h_mse, d_mse, b * 16, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     c->hsmall_busy = false;
     std::memcpy(mse, h_mse, b * 8);
