@@ -200,6 +200,14 @@ int mdg_deconvolute_rows_i32(mdg_ctx* ctx, size_t b, size_t n, const double* axe
                              mdg_lorentzian* out, size_t cap, size_t* counts, double* mse,
                              int* status);
 
+/* The decode step of mdg_deconvolute_rows_i32 alone, device to device (for callers
+ * that keep inputs and results in HBM, e.g. the multi-GPU path before
+ * mdg_deconvolute_batch_device): d_raw b x n int32 samples, d_desc b x 4 doubles
+ * {maximum, width, divisor, scale}; writes the b x n rows d_x and d_y. Enqueued on
+ * the context stream, no host synchronisation. */
+int mdg_decode_rows_i32_device(mdg_ctx* ctx, size_t b, size_t n, const int32_t* d_raw,
+                               const double* d_desc, double* d_x, double* d_y);
+
 /* Same, every array resident on the context's device (d_ prefix); enqueued on
  * the context stream without any host synchronisation (capturable). d_counts and
  * d_status are int32. Call mdg_ctx_synchronize before reading outputs. */

@@ -1273,6 +1273,7 @@ int mdg_deconvolute_rows_i32(mdg_ctx* c, size_t b, size_t n, const double* axes,
     if (n < 2 || n > (size_t)INT32_MAX / 2 || b > (size_t)INT32_MAX) return MDG_INVALID_ARGUMENT;
     if (!axes || !y_rows || !y_scale || !sb || !counts || !mse || !status || (!out && cap))
         return MDG_INVALID_ARGUMENT;
+    if (b > 65535) return MDG_INVALID_ARGUMENT;  // the decode grid's y dimension
     bool shared = true;
     for (size_t i = 0; i < b; ++i) {
         if (!y_rows[i]) return MDG_INVALID_ARGUMENT;
@@ -1300,6 +1301,19 @@ int mdg_deconvolute_rows_i32(mdg_ctx* c, size_t b, size_t n, const double* axes,
         return MDG_OK;
     };
     return batch_host(c, b, n, shared, upload, sb, s, ignore, n_ignore, out, cap, counts, mse, status);
+}
+
+int mdg_decode_rows_i32_device(mdg_ctx* c, size_t b, size_t n, const int32_t* d_raw,
+                               const double* d_desc, double* d_x, double* d_y) {
+    if (!c) return MDG_INVALID_ARGUMENT;
+    if (b == 0) return MDG_OK;
+    if (n < 2 || n > (size_t)INT32_MAX / 2 || b > 65535) return MDG_INVALID_ARGUMENT;
+    if (!d_raw || !d_desc || !d_x || !d_y) return MDG_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    launch_decode_rows_i32(d_raw, d_desc, (int)b, (int64_t)n, 0, d_x, d_y, c->stream);
+    HIPCHK(hipGetLastError());
+    return MDG_OK;
 }
 
 int mdg_deconvolute(mdg_ctx* c, const double* x, const double* y, size_t n, double sb0,

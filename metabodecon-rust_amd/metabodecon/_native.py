@@ -44,7 +44,7 @@ EXPORTS = [
     "mdg_ctx_create", "mdg_ctx_destroy", "mdg_ctx_set_stream", "mdg_ctx_synchronize",
     "mdg_ctx_set_profiling", "mdg_ctx_stage_times", "mdg_ctx_reset_stage_times",
     "mdg_deconvolute", "mdg_deconvolute_batch", "mdg_deconvolute_rows", "mdg_deconvolute_batch_device",
-    "mdg_deconvolute_rows_i32",
+    "mdg_deconvolute_rows_i32", "mdg_decode_rows_i32_device",
     "mdg_superposition_vec", "mdg_superposition_vec_device", "mdg_synth_batch_device",
     "mdg_ctx_last_peaks", "mdg_ctx_last_smoothed", "mdg_ctx_set_profiling_mask",
     "mdg_optimize_settings", "mdg_ordered_sum", "mdg_check_fast_division",
@@ -243,6 +243,7 @@ def _declare(L):
     L.mdg_deconvolute_rows_i32.argtypes = [_vp, _sz, _sz, _dp, ctypes.POINTER(_i32p), _dp, _dp, sp,
                                            _dp, _sz, _dp, _sz, _szp, _dp,
                                            ctypes.POINTER(ctypes.c_int)]
+    L.mdg_decode_rows_i32_device.argtypes = [_vp, _sz, _sz, _vp, _vp, _vp, _vp]
     L.mdg_deconvolute_batch_device.argtypes = [_vp, _sz, _sz, _vp, _sz, _vp, _sz, _vp, sp, _dp,
                                                _sz, _vp, _sz, _vp, _vp, _vp]
     L.mdg_superposition_vec.argtypes = [_vp, _dp, _sz, _dp, _sz, _dp]

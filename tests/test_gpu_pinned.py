@@ -199,3 +199,27 @@ def test_pinned_rows_with_an_offset_into_a_block():
         g = np.load(os.path.join(GOLDEN, "expected", f"blood_{k + 1:02d}.npz"))
         assert np.array_equal(out[k, : int(counts[k])], g["params"]), k
         assert abs(mse[k] - float(g["mse"])) <= MSE_RTOL * abs(float(g["mse"]))
+
+
+def test_device_decode_equals_reader_rows():
+    """mdg_decode_rows_i32_device rebuilds every blood spectrum's axis and
+    intensities bit for bit as the reader computed them on the host
+    (maximum - (i * width) / (SI - 1) and sample * 2^NC_proc)."""
+    torch = pytest.importorskip("torch")
+    import metabodecon as md
+    read = _blood(md)
+    n, b = len(read[0]), len(read)
+    raw = torch.from_numpy(np.stack([s._raw[0] for s in read])).to("cuda")
+    desc = torch.tensor([[*s._raw[2], s._raw[1]] for s in read], dtype=torch.float64,
+                        device="cuda")
+    x = torch.empty((b, n), dtype=torch.float64, device="cuda")
+    y = torch.empty((b, n), dtype=torch.float64, device="cuda")
+    ctx = nat.context()
+    torch.cuda.synchronize()
+    assert nat.lib().mdg_decode_rows_i32_device(ctx.handle, b, n, raw.data_ptr(), desc.data_ptr(),
+                                                x.data_ptr(), y.data_ptr()) == 0
+    ctx.synchronize()
+    assert np.array_equal(x.cpu().numpy(), np.stack([s.chemical_shifts for s in read]))
+    assert np.array_equal(y.cpu().numpy(), np.stack([s.intensities for s in read]))
+    assert nat.lib().mdg_decode_rows_i32_device(ctx.handle, b, n, None, desc.data_ptr(),
+                                                x.data_ptr(), y.data_ptr()) == nat.INVALID_ARGUMENT
