@@ -270,12 +270,25 @@ class Spectrum:
     @staticmethod
     def read_bruker_set(path: str, experiment: int, processing: int,
                         signal_boundaries) -> list["Spectrum"]:
-        arrays = []
-        for p in bruker_set_paths(path):
+        # the files are read by a few threads at once (the reads and the int32
+        # decode release the GIL); the first error in directory order is raised,
+        # as the reference's sequential collect does (bruker.rs:300-321)
+        paths = bruker_set_paths(path)
+
+        def one(p):
             try:
-                arrays.append(read_bruker_arrays(p, experiment, processing))
+                return read_bruker_arrays(p, experiment, processing)
             except MetadataError as e:
-                raise getattr(exc, e.kind, exc.SpectrumError)(str(e)) from None
+                return e
+        if len(paths) > 1:
+            from concurrent.futures import ThreadPoolExecutor
+            with ThreadPoolExecutor(max_workers=min(8, len(paths))) as pool:
+                arrays = list(pool.map(one, paths))
+        else:
+            arrays = [one(p) for p in paths]
+        for a in arrays:
+            if isinstance(a, MetadataError):
+                raise getattr(exc, a.kind, exc.SpectrumError)(str(a)) from None
         return _set_of_rows(arrays, signal_boundaries)
 
 
