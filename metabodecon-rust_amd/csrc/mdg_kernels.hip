@@ -2862,11 +2862,6 @@ struct TwShape {
 };
 using TwDefault = TwShape<63, 2, 3>;
 
-#ifndef MDG_TW_PF
-#define MDG_TW_PF 1
-#endif
-constexpr int kTwPrefetch = MDG_TW_PF;  // chunks of peak parameters loaded ahead
-static_assert(kTwPrefetch >= 1, "prefetch depth");
 
 template <bool FAST, class SH>
 __device__ __forceinline__ void fit_tw_body(const Workspace& w, int s, int P, int it, double* T) {
@@ -2891,30 +2886,20 @@ __device__ __forceinline__ void fit_tw_body(const Workspace& w, int s, int P, in
 #pragma unroll
             for (int q = 0; q < QS; ++q) xq[q] = rx[q];
             const int jl = pb * 64 + lane;
-            // the peak parameters of the next kTwPrefetch chunks are in flight while a
-            // chunk is evaluated (a chunk's terms take less time than a load from L2)
-            double f[kTwPrefetch], h[kTwPrefetch], m[kTwPrefetch];
-#pragma unroll
-            for (int k = 0; k < kTwPrefetch; ++k) {
-                const int j = min(k * J + jl, P - 1);
-                f[k] = params[3 * j];
-                h[k] = params[3 * j + 1];
-                m[k] = params[3 * j + 2];
-            }
+            int j = min(jl, P - 1);
+            double f = params[3 * j], h = params[3 * j + 1], m = params[3 * j + 2];
             for (int c = 0; c <= nch; ++c) {
                 if (c < nch) {
                     double* Tb = T + (c & 1) * QQ * RS + ps * QS * RS + jl;
-                    const double cf = f[0], ch = h[0], cm = m[0];
-#pragma unroll
-                    for (int k = 0; k + 1 < kTwPrefetch; ++k) {
-                        f[k] = f[k + 1];
-                        h[k] = h[k + 1];
-                        m[k] = m[k + 1];
-                    }
-                    const int j = min((c + kTwPrefetch) * J + jl, P - 1);
-                    f[kTwPrefetch - 1] = params[3 * j];
-                    h[kTwPrefetch - 1] = params[3 * j + 1];
-                    m[kTwPrefetch - 1] = params[3 * j + 2];
+                    const double cf = f, ch = h, cm = m;
+                    // the next chunk's peak, in flight while this chunk is evaluated; the
+                    // compiler copies it into f/h/m at the loop's back edge, so the copy
+                    // waits for it there (the small-batch fit is bound by
+                    // this load's latency, not by its FP64 issue)
+                    j = min((c + 1) * J + jl, P - 1);
+                    f = params[3 * j];
+                    h = params[3 * j + 1];
+                    m = params[3 * j + 2];
 #pragma unroll
                     for (int q = 0; q < QS; ++q) Tb[q * RS] = lorentz_t<FAST>(xq[q], cf, ch, cm);
                 }
