@@ -66,7 +66,9 @@ BLOOD = os.path.join(ROOT, "tests", "golden", "bruker", "blood")
 CPU_REPS = 5
 
 
-def parse():
+def parse(argv=None):
+    """The command line (argv None: sys.argv). tests/test_gpu_queue.py takes the
+    headline's defaults from parse([]), so the test checks the shape bench.py times."""
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=24,
@@ -115,7 +117,7 @@ def parse():
                          "this way under GPU_MAX_HW_QUEUES=32 for the second environment)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: exercise the launcher, rendezvous and gather (gloo)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 # ------------------------------------------------------------------ launcher
@@ -1142,7 +1144,7 @@ def queue_line(args, h, world, nat):
                    "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "unset (HIP default 4)"),
                    "selected_peaks": h["selected_peaks"], "kept_peaks": h["kept_peaks"],
                    "parallelism": f"dp{world}" if world > 1 else "single"},
-        "verified": h["verified"],
+        "verified_detail": h["verified"],
         "rccl_gather_ms": h["gather_ms"],
         "roofline": roof,
         "roofline_pipeline": pipe,
@@ -1270,6 +1272,11 @@ def finish(args, line, value, nat, torch, dist, dev, rank, world, local):
                 if key in configs and ref[0] in cb:
                     configs[key]["speedup_vs_cpu"] = configs[key]["value"] / cb[ref[0]][ref[1]]
     if rank == 0:
+        # the driver keeps only the tail of stdout: the parity and roofline summary go last
+        v = line.get("verified_detail")
+        roof = line.get("roofline") or {}
+        line["roofline_frac"] = roof.get("frac")
+        line["verified"] = v["verified"] if isinstance(v, dict) else None
         print(json.dumps(line), flush=True)
     if world > 1 or args.force_dist:
         dist.destroy_process_group()

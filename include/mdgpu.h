@@ -76,9 +76,20 @@ typedef struct mdg_settings {
     int32_t scoring;           /* MDG_SCORE_* */
     uint32_t fit_iterations;
     int32_t fitter;            /* MDG_FIT_* */
-    int32_t reserved;          /* must be 0 */
+    int32_t options;           /* MDG_OPTION_* bits (engine options; 0 = the defaults) */
     double threshold;
 } mdg_settings;
+
+/* mdg_settings.options. MDG_OPTION_EXACT_MSE: the MSE is computed in the reference's
+ * operation order (compute_mse, deconvoluter.rs:828-862: each point's superposition
+ * the in-order left fold of Lorentzian::superposition_vec, lorentzian.rs:606-611, the
+ * squared residuals folded left to right per MSE region, the region sums in region
+ * order), so Deconvolution::mse and the `mse` field of the serialized Deconvolution
+ * (serialized_deconvolution.rs:18-31) equal the reference's bit for bit. Off: the
+ * engine's MSE (local expansions and fixed-order trees), within 1e-12 relative of it
+ *  and cheaper. Lorentzians, counts and statuses are the same either
+ * way. Other bits must be 0 (MDG_INVALID_ARGUMENT). */
+enum { MDG_OPTION_EXACT_MSE = 1 };
 
 /* Lorentzian in transformed parameters (lorentzian.rs:138-145), repr(C). */
 typedef struct mdg_lorentzian {
@@ -318,6 +329,10 @@ int mdg_queue_lane(mdg_queue* q, int lane, mdg_ctx** ctx);
 /* Batches launched, spectra launched, submissions waiting in the open batch. */
 int mdg_queue_stats(mdg_queue* q, uint64_t* batches, uint64_t* spectra, size_t* open);
 int mdg_queue_destroy(mdg_queue* q);
+/* Test support: the queue's next batch launch fails with `status` (nonzero) before
+ * anything is enqueued, as an allocation or launch failure would; the failure is
+ * then sticky like any other (every later call returns it, destroy still works). */
+int mdg_queue_fail_next_launch(mdg_queue* q, int status);
 
 #ifdef __cplusplus
 }

@@ -62,6 +62,7 @@ struct mdg_ctx {
     // once and left at zero by every run (k_flags), so no run has to clear them
     Buffer chain_flags;
     Buffer ign;  // the call's merged ignore regions (ppm pairs, device row)
+    Buffer exact;  // MDG_OPTION_EXACT_MSE: B x N squared residuals (allocated on first use)
     std::vector<double> ign_last;  // the regions the device row holds now
     int ws_igcap = 0;  // ignore-region pairs per spectrum row of the arena
     // optimize_settings: per-spectrum overrides for the next run_pipeline, buffers
@@ -301,8 +302,6 @@ int ensure_workspace(mdg_ctx* c, int B, int N, int n_ignore) {
         const size_t o_xok = take(Bs * 4), o_unsafe = take(Bs * 16), o_uk = take(Bs * 4);
         const size_t o_pcnt = take(Bs * 2 * ((W + 255) / 256) * 4);
         const size_t o_mcnt = take(Bs * 4);
-        const size_t o_fdyn = take((kFitDynCtl + Bs * (3 * capD / 64 + 2)) * 4);
-        const size_t o_fpart = take(Bs * (3 * capD + 64) * 8);
 
         if (c->arena.p) (void)hipFree(c->arena.p);
         c->arena.p = nullptr;
@@ -345,9 +344,7 @@ int ensure_workspace(mdg_ctx* c, int B, int N, int n_ignore) {
         w.unsafe_kept = (int32_t*)(base + o_uk);
         w.peak_cnt = (int32_t*)(base + o_pcnt);
         w.mse_done = (int32_t*)(base + o_mcnt);
-        w.fit_dyn = (int32_t*)(base + o_fdyn);
-        w.fit_part = (double*)(base + o_fpart);
-        // k_mse_partial_n's arrival counters start (and are always left) at zero
+        // k_mse_local's arrival counters start (and are always left) at zero
         HIPCHK(hipMemset(w.mse_done, 0, Bs * 4));
 
         c->ws_B = nB;
@@ -356,6 +353,15 @@ int ensure_workspace(mdg_ctx* c, int B, int N, int n_ignore) {
         ++c->ws_gen;
     }
     return MDG_OK;
+}
+
+// the exact-order MSE's residual rows (B x N doubles), bumping the workspace
+// generation when the buffer moves (cached graphs bake its address)
+int ensure_exact(mdg_ctx* c, int B, int N) {
+    const void* old = c->exact.p;
+    const int rc = ensure(c->exact, (size_t)B * (size_t)N * 8);
+    if (c->exact.p != old) ++c->ws_gen;
+    return rc;
 }
 
 // ensure() for the chain smoother buffer, bumping the workspace generation when
@@ -445,15 +451,19 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
             w.chain_P = P;
         }
     }
-    // MDG_DIAG_SKIP=smooth,mse: throughput diagnostics only (tools/stream_diag.py);
-    // the skipped stage's outputs are stale, so results are wrong
+#ifdef MDG_DIAG
+    // diagnostic builds only (make diag; tools/stream_diag.py): MDG_DIAG_SKIP=smooth,mse
+    // skips those stages (their outputs are stale, results wrong); MDG_DIAG_DUP=prep,
+    // smooth,detect,select,retain,mse launches those stages twice (each is idempotent;
+    // smooth adds a k_flags), for their marginal cost in stream mode
     const char* skip = std::getenv("MDG_DIAG_SKIP");
     const bool skip_smooth = skip && std::strstr(skip, "smooth"), skip_mse = skip && std::strstr(skip, "mse");
-    // MDG_DIAG_DUP=prep,smooth,detect,scores,select,fitinit,retain,mse: launch those
-    // stages twice (each is idempotent; smooth adds a k_prep), for their marginal
-    // cost in stream mode
     const char* dup_env = std::getenv("MDG_DIAG_DUP");
     auto reps = [&](const char* stage) { return dup_env && std::strstr(dup_env, stage) ? 2 : 1; };
+#else
+    constexpr bool skip_smooth = false, skip_mse = false;
+    auto reps = [](const char*) { return 1; };
+#endif
     const int sm_it = (int)s->smooth_iterations, sm_ws = (int)s->smooth_window;
     const bool panic_shape = ma && (int64_t)(s->smooth_window / 2) > a.N;
     // the chain smoother does k_prep's work itself (MDG_PREP=separate: not)
@@ -465,8 +475,10 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
         for (int r = reps("prep"); r > 0; --r) launch_prep(a, w, st);
         kn[ST_PREP] = "k_prep";
     }
+#ifdef MDG_DIAG
     if (const char* e = std::getenv("MDG_DIAG_PAD"))
         for (int k = std::atoi(e); k > 0; --k) launch_diag_nop(a, w, st);
+#endif
     if (ma) {
         if (panic_shape) {
             // moving_average.rs:63 `values_len - self.right` underflows: reference panics
@@ -491,17 +503,7 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     }
     {
         StageTimer t(c, ST_SELECT);
-        if (!det_only && (!peaks_score() || reps("scores") == 2)) launch_scores(a, w, st);
         for (int r = reps("select"); r > 0; --r) kn[ST_SELECT] = launch_select(a, w, det_only, s->threshold, st);
-    }
-    if (reps("fitinit") == 2) {  // the selection kernels already initialised the fit
-        StageTimer t(c, ST_FIT_INIT);
-        launch_fit_init(a, w, gupd, st);
-        kn[ST_FIT_INIT] = "k_fit_init";
-    }
-    if (fit_sup_dyn(a)) {
-        StageTimer t(c, ST_FIT_INIT);
-        launch_fit_plan(a, w, st);
     }
     for (uint32_t it = 0; it < s->fit_iterations; ++it) {
         {
@@ -514,18 +516,24 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
             kn[ST_FIT_UPDATE] = "k_fit_update";
         }
     }
-    if (!mse_fuses_retain() || skip_mse || reps("retain") == 2) {
+    // k_mse_local compacts the retained Lorentzians itself; k_retain only when the MSE
+    // is skipped or the retain duplicated (diagnostic builds)
+    if (skip_mse || reps("retain") == 2) {
         StageTimer t(c, ST_RETAIN);
         launch_retain(a, w, st);
         kn[ST_RETAIN] = "k_retain<1024>";
     }
     if (!skip_mse) {
-        {
-            StageTimer t(c, ST_MSE);
-            for (int r = reps("mse"); r > 0; --r) kn[ST_MSE] = launch_mse(a, w, nparts, st);
-        }
+        StageTimer t(c, ST_MSE);
+        for (int r = reps("mse"); r > 0; --r) kn[ST_MSE] = launch_mse(a, w, nparts, st);
+    }
+    if (!skip_mse && (s->options & MDG_OPTION_EXACT_MSE)) {
+        // the reference's summation order (deconvoluter.rs:828-862), over the retained
+        // Lorentzians k_mse_local compacted; replaces its MSE
+        if ((rc = ensure_exact(c, a.B, a.N))) return rc;
         StageTimer t(c, ST_MSE_REDUCE);
-        launch_mse_final(a, w, nparts, st);
+        launch_mse_exact_batch(a, w, (double*)c->exact.p, a.N, st);
+        kn[ST_MSE_REDUCE] = "k_mse_exact_res+k_mse_exact_fold";
     }
     HIPCHK(hipGetLastError());
     return MDG_OK;
@@ -654,7 +662,7 @@ int mdg_settings_validate(const mdg_settings* s) {
         return MDG_INVALID_SELECTION;
     }
     if (s->fitter != MDG_FIT_ANALYTICAL || s->fit_iterations == 0) return MDG_INVALID_FITTING;  // fitter.rs:80-90
-    if (s->reserved != 0) return MDG_INVALID_ARGUMENT;
+    if (s->options & ~(int32_t)MDG_OPTION_EXACT_MSE) return MDG_INVALID_ARGUMENT;
     return MDG_OK;
 }
 
@@ -781,7 +789,7 @@ int mdg_ctx_destroy(mdg_ctx* c) {
         drop_graphs(c);
         for (Buffer& b : c->opt)
             if (b.p) (void)hipFree(b.p);
-        for (Buffer* b : {&c->arena, &c->chain, &c->chain_flags, &c->ign, &c->st_x, &c->st_y, &c->st_sb, &c->st_out, &c->st_cnt,
+        for (Buffer* b : {&c->arena, &c->chain, &c->chain_flags, &c->ign, &c->exact, &c->st_x, &c->st_y, &c->st_sb, &c->st_out, &c->st_cnt,
                           &c->st_mse, &c->st_status, &c->st_L, &c->st_sup, &c->st_flag, &c->st_raw,
                           &c->st_desc})
             if (b->p) (void)hipFree(b->p);
@@ -963,6 +971,7 @@ int run_pipeline_graphed(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     if (ma && chain_supported(a.B, a.N, (int)s->smooth_iterations, (int)s->smooth_window) &&
         !(std::getenv("MDG_SMOOTH") && std::string(std::getenv("MDG_SMOOTH")) != "chain"))
         (void)ensure_chain(c, chain_bytes(a.B, a.N, (int)s->smooth_window, (int)s->smooth_iterations));
+    if ((s->options & MDG_OPTION_EXACT_MSE) && (rc = ensure_exact(c, a.B, a.N))) return rc;
     if (c->graphs_gen != c->ws_gen) {  // buffers moved since these graphs were captured
         drop_graphs(c);
         c->graphs_gen = c->ws_gen;
@@ -972,9 +981,8 @@ int run_pipeline_graphed(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     // the kernel-choice overrides (tests, diagnostics) select other kernels, so
     // they are part of the key too
     std::string envs;
-    for (const char* e : {"MDG_SMOOTH", "MDG_CHAIN_EXCL", "MDG_FITSUP", "MDG_GFIT", "MDG_TW_G", "MDG_DYN_WPC", "MDG_DYN_PIECES", "MDG_MSE", "MDG_MSE_QNPT", "MDG_MSE_NPT",
-                          "MDG_MSE_NEARCAP", "MDG_PEAKS_2PASS", "MDG_PEAKS_NOSCORE", "MDG_DIAG_SKIP", "MDG_DIAG_DUP", "MDG_DIAG_PAD",
-                          "MDG_DIAG_PAD_SMALL", "MDG_PREP"}) {
+    for (const char* e : {"MDG_SMOOTH", "MDG_CHAIN_EXCL", "MDG_FITSUP", "MDG_GFIT", "MDG_TW_G", "MDG_MSE_NEARCAP",
+                          "MDG_DIAG_SKIP", "MDG_DIAG_DUP", "MDG_DIAG_PAD", "MDG_DIAG_PAD_SMALL", "MDG_PREP"}) {
         const char* v = std::getenv(e);
         envs += v ? v : "\x01";
         envs += '\0';
@@ -992,6 +1000,7 @@ int run_pipeline_graphed(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     std::memcpy(k, &c->chain.p, sizeof(void*));
     k += sizeof(void*);
     std::memcpy(k, &c->chain.bytes, sizeof(size_t));
+    // (the exact-MSE rows' address: a move bumps ws_gen, which drops every graph)
     mdg_ctx::CachedGraph* hit = nullptr;
     for (auto& ge : c->graphs)
         if (ge.key == key) hit = &ge;
@@ -1182,17 +1191,27 @@ static int batch_host(mdg_ctx* c, size_t b, size_t n, bool shared_x, Upload uplo
     int32_t* h_cnt = (int32_t*)(h_mse + b);
     int32_t* h_st = h_cnt + b;
     c->hsmall_busy = true;
-    if ((rc = upload(dx, dy, st))) return rc;
+    // From here on DMAs may read the caller's page-locked rows (upload_rows sends
+    // mdg_host_alloc rows without copying them): a failure must not return while they
+    // are in flight, or the caller could release and reuse the rows under the copy.
+    auto fail = [&](int code) {
+        (void)hipStreamSynchronize(st);
+        c->hsmall_busy = false;
+        return code;
+    };
+    if ((rc = upload(dx, dy, st))) return fail(rc);
     std::memcpy(h_sb, sb, b * 16);
-    HIPCHK(hipMemcpyAsync(c->st_sb.p, h_sb, b * 16, hipMemcpyHostToDevice, st));
+    hipError_t he = hipMemcpyAsync(c->st_sb.p, h_sb, b * 16, hipMemcpyHostToDevice, st);
+    if (he != hipSuccess) return fail(hip_fail(he));
     BatchArgs a;
     if ((rc = fill_args(c, a, b, n, dx, shared_x ? 0 : n, dy, n, (const double*)c->st_sb.p, ignore,
                         n_ignore, (double*)c->st_out.p, cap, d_cnt, d_mse, d_st)))
-        return rc;
-    rc = run_pipeline(c, a, s);
-    if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(h_mse, d_mse, b * 16, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+        return fail(rc);
+    if ((rc = run_pipeline(c, a, s))) return fail(rc);
+    he = hipMemcpyAsync(h_mse, d_mse, b * 16, hipMemcpyDeviceToHost, st);
+    if (he != hipSuccess) return fail(hip_fail(he));
+    he = hipStreamSynchronize(st);
+    if (he != hipSuccess) return fail(hip_fail(he));
     c->hsmall_busy = false;
     std::memcpy(mse, h_mse, b * 8);
     const int32_t* cnt = h_cnt;
@@ -1615,12 +1634,18 @@ struct mdg_queue {
     std::condition_variable cv;
     std::thread watcher;
     uint64_t deadline_flushes = 0;
+    int fail_next = 0;  // mdg_queue_fail_next_launch: status of the next launch (tests)
 };
 
 namespace {
 
 int queue_launch(mdg_queue* q) {
     if (q->open.empty()) return MDG_OK;
+    if (q->fail_next) {  // mdg_queue_fail_next_launch (tests): this launch fails
+        const int rc = q->fail_next;
+        q->fail_next = 0;
+        return rc;
+    }
     mdg_queue::Lane& L = q->lanes[q->next];
     q->next = (q->next + 1) % (int)q->lanes.size();
     const int B = (int)q->open.size();
@@ -1748,7 +1773,10 @@ int mdg_queue_set_flush_us(mdg_queue* q, int64_t us) {
         q->watcher = std::thread([q] {
             std::unique_lock<std::mutex> lk(q->mu);
             while (!q->stop) {
-                if (q->flush_us <= 0 || q->open.empty()) {
+                // nothing to launch: no deadline, an empty batch, or a queue whose
+                // earlier launch failed (sticky error: the open batch never launches,
+                // every call returns the error) -- wait, releasing q->mu
+                if (q->flush_us <= 0 || q->open.empty() || q->error) {
                     q->cv.wait(lk);
                     continue;
                 }
@@ -1757,15 +1785,20 @@ int mdg_queue_set_flush_us(mdg_queue* q, int64_t us) {
                     q->cv.wait_until(lk, due);
                     continue;
                 }
-                if (!q->error) {
-                    const int rc = queue_launch(q);  // under q->mu, like a submit's launch
-                    if (rc) q->error = rc;
-                    ++q->deadline_flushes;
-                }
+                const int rc = queue_launch(q);  // under q->mu, like a submit's launch
+                if (rc) q->error = rc;
+                ++q->deadline_flushes;
             }
         });
     }
     q->cv.notify_one();
+    return MDG_OK;
+}
+
+int mdg_queue_fail_next_launch(mdg_queue* q, int status) {
+    if (!q || status == MDG_OK) return MDG_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> g(q->mu);
+    q->fail_next = status;
     return MDG_OK;
 }
 

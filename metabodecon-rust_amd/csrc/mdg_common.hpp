@@ -23,7 +23,6 @@ constexpr double kCheckPrecision = 1.0e+3 * 2.220446049250313080847e-16;
 constexpr double kEpsilon = 2.220446049250313080847e-16;  // f64::EPSILON
 constexpr int kIgnoreRow = 64;  // ignore-region pairs per spectrum row, grown in steps of this
 constexpr int kMseMaxParts = 2048;  // MSE partial sums per spectrum (workspace rows)
-constexpr int kFitDynCtl = 576;  // k_fit_sup_dyn control words before its chunk counters
 
 // ---- counter-based splitmix64 (synthetic workload only) ----------------------
 MDG_HD inline uint64_t mix64(uint64_t z) {

@@ -162,62 +162,6 @@ __device__ __forceinline__ double superpose_t(double x, const double* __restrict
     return acc;
 }
 
-// NPT points per thread against the same Lorentzian groups: each point's sum is the
-// same left fold as superpose_t (bit-identical), the parameter loads are shared and
-// the NPT evaluations of a term are independent (ILP with one wave per SIMD)
-template <bool FAST, int NPT>
-__device__ __forceinline__ void sup_group_n(const double (&x)[NPT], double (&acc)[NPT],
-                                            const double (&c)[3 * kSupGP], double (&n)[3 * kSupGP],
-                                            const_f64_ptr next, bool load_next) {
-    double e[NPT][kSupGP];
-#pragma unroll
-    for (int i = 0; i < NPT; ++i) e[i][0] = lorentz_mse<FAST>(x[i], c[0], c[1], c[2]);
-    __builtin_amdgcn_sched_barrier(0);
-    if (load_next) {
-#pragma unroll
-        for (int k = 0; k < 3 * kSupGP; ++k) n[k] = next[k];
-    }
-#pragma unroll
-    for (int k = 1; k < kSupGP; ++k)
-#pragma unroll
-        for (int i = 0; i < NPT; ++i) e[i][k] = lorentz_mse<FAST>(x[i], c[3 * k], c[3 * k + 1], c[3 * k + 2]);
-#pragma unroll
-    for (int i = 0; i < NPT; ++i)
-#pragma unroll
-        for (int k = 0; k < kSupGP; ++k) acc[i] += e[i][k];
-}
-
-template <bool FAST, int NPT>
-__device__ __forceinline__ void superpose_n(const double (&x)[NPT], const double* __restrict__ params_g,
-                                            int P, double (&acc)[NPT]) {
-    constexpr int GW = 3 * kSupGP;
-    const const_f64_ptr params = (const_f64_ptr)(params_g);
-    const int G = P / kSupGP;
-#pragma unroll
-    for (int i = 0; i < NPT; ++i) acc[i] = -0.0;
-    int g = 0;
-    if (G > 0) {
-        double A[GW], B[GW];
-#pragma unroll
-        for (int k = 0; k < GW; ++k) A[k] = params[k];
-        for (; g + 2 < G; g += 2) {
-            sup_group_n<FAST, NPT>(x, acc, A, B, params + GW * (g + 1), true);
-            sup_group_n<FAST, NPT>(x, acc, B, A, params + GW * (g + 2), true);
-        }
-        if (g + 1 < G) {
-            sup_group_n<FAST, NPT>(x, acc, A, B, params + GW * (g + 1), true);
-            sup_group_n<FAST, NPT>(x, acc, B, A, params, false);
-        } else {
-            sup_group_n<FAST, NPT>(x, acc, A, B, params, false);
-        }
-    }
-    for (int j = kSupGP * G; j < P; ++j) {
-        const_f64_ptr L = params + 3 * j;
-#pragma unroll
-        for (int i = 0; i < NPT; ++i) acc[i] += lorentz_mse<FAST>(x[i], L[0], L[1], L[2]);
-    }
-}
-
 __device__ __forceinline__ double superpose(double x, const double* __restrict__ params, int P,
                                             bool fast) {
     return fast ? superpose_t<true>(x, params, P) : superpose_t<false>(x, params, P);
@@ -245,7 +189,7 @@ __device__ int g_chain_mode = 0;  // chain_diag: 1 = feeder publishes everything
     do {                                                                    \
         if ((threadIdx.x & 63) == 0 && g_diag)                              \
             for (int _i = 0; _i < 8; ++_i)                                  \
-                g_diag[(blockIdx.x * 16 + (threadIdx.x >> 6)) * 8 + _i] = (long long)_d_acc[_i]; \
+                g_diag[((blockIdx.y * gridDim.x + blockIdx.x) * 16 + (threadIdx.x >> 6)) * 8 + _i] = (long long)_d_acc[_i]; \
     } while (0)
 #else
 #define KSTAMP(slot)
@@ -654,140 +598,6 @@ __global__ __launch_bounds__(64) void k_smooth_pipe(BatchArgs a, Workspace w, in
     }
     generic(tB, T);
 }
-
-// ----------------------------------------------------------------------------------
-// K1c  wave-per-pass moving average (small batches; measured: one wave issues one
-// f64 add per ~4.7 cycles whether dependent or not, so the recurrence is
-// issue-bound and the passes must run on separate SIMDs).
-//
-// Workgroup = one spectrum, wave p = pass p, and only lane 0 of each wave runs
-// the recurrence (tick: ds_read in, add, sub, mul, ds_write emit). Pass p emits
-// o_p[i] at tick i+R into LDS ring p (4 blocks of U ticks); pass p+1 runs two
-// blocks behind and reads it back, so one barrier per block of U ticks orders
-// every hand-off. Wave 0's 64 lanes prefetch raw input blocks into LDS one block
-// ahead; the last wave's 64 lanes copy its ring block to HBM coalesced.
-// ----------------------------------------------------------------------------------
-template <int WS>
-__global__ __launch_bounds__(512) void k_smooth_waves(BatchArgs a, Workspace w, int P) {
-    constexpr int R = WS / 2;
-    constexpr int U = WS * ((32 + WS - 1) / WS);  // ticks per block (multiple of WS)
-    constexpr int RING = 4 * U;                   // 4 blocks per emit ring
-    constexpr int LAG = 2;                        // blocks between consecutive passes
-    constexpr int PIECES = (U * 8 + 255) / 256;   // 256-byte DMA pieces per raw block
-    constexpr int RAWSLOT = PIECES * 32;          // raw slot stride in doubles (padded)
-    static_assert(R < U, "block shorter than the window");
-    extern __shared__ __attribute__((aligned(16))) double lds[];
-    double* raw = lds;                   // 4 slots of one raw block each (wave 0's input)
-    double* rings = lds + 4 * RAWSLOT;   // ring p: emits of pass p at their tick slot
-    const int s = blockIdx.x;
-    if (w.status[s]) return;  // uniform per workgroup
-    // waves >= P are idle and only join the barriers: the workgroup is padded to a
-    // multiple of 4 waves because 3-wave workgroups measured ~2x slower per op
-    // (tools/ubench: 9-12 vs 5 cycles per dependent f64 add)
-    const int p = threadIdx.x >> 6;
-    const bool active = p < P;
-    const int lane = threadIdx.x & 63;
-    const int N = a.N;
-    const double* yrow = a.y + (size_t)s * a.y_stride;
-    double* orow = w.smooth + (size_t)s * N;
-    const int nkb = (N + R + U - 1) / U;  // blocks of ticks per pass
-    const int total = nkb + LAG * (P - 1);
-    double* my_ring = rings + (active ? p : 0) * RING;
-    const double* in_ring = rings + (p > 0 ? p - 1 : 0) * RING;
-    MAState<WS> st;
-    st.sum = 0.0;
-    st.div = 1.0;
-#pragma unroll
-    for (int k = 0; k < WS; ++k) st.fifo[k] = 0.0;
-
-    // Raw input of wave 0 arrives by LDS-DMA (global_load_lds, 4 bytes per lane,
-    // PIECES instructions per block) three blocks ahead, into slot j&3. No VGPR
-    // holds an in-flight load, so nothing makes the compiler drain the queue;
-    // the one wait is the counted vmcnt below. Past-the-end dwords are clamped to
-    // the row's last dword (never consumed: ticks >= N take no input).
-    const int last_dw = 2 * N - 1;
-    auto dma_block = [&](int j) {
-        const unsigned* src = (const unsigned*)yrow;
-        double* slot = raw + (j & 3) * RAWSLOT;
-#pragma unroll
-        for (int pc = 0; pc < PIECES; ++pc) {
-            const int dw = min(j * U * 2 + pc * 64 + lane, last_dw);
-            __builtin_amdgcn_global_load_lds((const void*)(src + dw),
-                                             (__attribute__((address_space(3))) void*)(slot + pc * 32),
-                                             4, 0, 0);
-        }
-    };
-    if (p == 0) {
-        dma_block(0);
-        dma_block(1);
-        dma_block(2);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    lds_barrier();
-    DIAG_DECL
-    for (int gb = 0; gb < total; ++gb) {
-        const int kb = gb - LAG * p;
-        if (p == 0) dma_block(kb + 3);  // j beyond nkb: harmless clamped copy
-        DIAG_STAMP(0);
-        // All 64 lanes run the recurrence redundantly (identical values): with one
-        // active lane, waves of a workgroup running concurrently on other SIMDs
-        // slowed every f64 op to 10-15 cycles; with full EXEC each sustains 4.6
-        // (tools/ubench, wave_chain). Only the ring write-back is lane 0's.
-        if (active && kb >= 0 && kb < nkb) {
-            const int q0 = kb * U;
-            double* out = my_ring + (kb & 3) * U;  // slot of tick q0 + k
-            // gather the whole block's inputs first (broadcast LDS reads): every read
-            // is issued before any write (reads cannot be reordered past ring writes)
-            double v[U];
-            if (p == 0) {
-                const double* src = raw + (kb & 3) * RAWSLOT;
-#pragma unroll
-                for (int k = 0; k < U; ++k) v[k] = src[k];
-            } else {
-                const double* in0 = in_ring + (kb & 3) * U + R;  // o_{p-1}[q] sits at tick q+R
-                const double* in1 = in_ring + ((kb + 1) & 3) * U + R - U;
-#pragma unroll
-                for (int k = 0; k < U; ++k) v[k] = k + R < U ? in0[k] : in1[k];
-            }
-            DIAG_STAMP(1);
-            if (q0 >= WS && q0 + U <= N) {
-#pragma unroll
-                for (int k = 0; k < U; ++k) v[k] = ma_tick_steady<WS>(st, k % WS, v[k]);
-            } else {
-#pragma unroll
-                for (int k = 0; k < U; ++k) {
-                    const int q = q0 + k;
-                    v[k] = ma_tick_generic<WS>(st, k % WS, q, N, q < N ? v[k] : 0.0);
-                }
-            }
-            if (lane == 0) {
-#pragma unroll
-                for (int k = 0; k < U; ++k) out[k] = v[k];
-            }
-        }
-        DIAG_STAMP(2);
-        if (p == 0) {
-            // block kb+1's DMA must have landed; only blocks kb+2, kb+3 may be in flight
-            // (wave 0 issues no other vector-memory op unless it is also the last pass)
-            if (P == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PIECES) : "memory");
-        }
-        DIAG_STAMP(3);
-        lds_barrier();
-        DIAG_STAMP(4);
-        // last pass: slot k of block kb holds o[kb*U + k - R]
-        if (p == P - 1 && kb >= 0 && kb < nkb) {
-            const double* blk = my_ring + (kb & 3) * U;
-            for (int k = lane; k < U; k += 64) {
-                const int i = kb * U + k - R;
-                if (i >= 0 && i < N) orow[i] = blk[k];
-            }
-        }
-        DIAG_STAMP(5);
-    }
-    DIAG_FLUSH();
-}
-
 
 // ----------------------------------------------------------------------------------
 // K1d  chain moving average: one workgroup per (spectrum, pass), passes on
@@ -1498,29 +1308,9 @@ __device__ __forceinline__ double score_peak(const double* __restrict__ sm, int 
     return fmin(left, right);
 }
 
-// K3a per chunk of kPkWords mask words (one word per thread): kept and bordered
-// peak counts. K3b re-scans its chunk, places it after the kept peaks of the chunks
-// before it and compacts in centre order; chunk 0 publishes det_count, or
-// NoPeaksDetected when no peak has both borders (detector.rs:99-164). Many
-// workgroups per spectrum: the single-workgroup version took 46-53 us at N = 131072.
+// K3 per chunk of kPkWords mask words (one word per thread, many workgroups per
+// spectrum: a single-workgroup version took 46-53 us at N = 131072).
 constexpr int kPkWords = 256;
-__global__ __launch_bounds__(kPkWords) void k_peaks_count(BatchArgs a, Workspace w, int detector_only) {
-    const int s = blockIdx.y, chunk = blockIdx.x;
-    __shared__ long long lds_l[kPkWords / 64 + 1];
-    if (w.status[s]) return;
-    const int wd = chunk * kPkWords + threadIdx.x;
-    int bordered = 0, kept = 0;
-    if (wd < w.W) kept = word_peaks<false>(a, w, s, wd, detector_only, &bordered, 0);
-    const long long k_tot = block_sum_ll<kPkWords>(kept, lds_l);
-    const long long b_tot = block_sum_ll<kPkWords>(bordered, lds_l);
-    if (threadIdx.x == 0) {
-        const int nch = (w.W + kPkWords - 1) / kPkWords;
-        int32_t* cnt = w.peak_cnt + (size_t)s * 2 * nch;
-        cnt[2 * chunk] = (int32_t)k_tot;
-        cnt[2 * chunk + 1] = (int32_t)b_tot;
-    }
-}
-
 // K3 in one pass (decoupled look-back): every chunk counts its peaks, publishes
 // {bordered, kept} in its slot of w.peak_cnt (cleared by k_flags), then reads the
 // slots of all chunks of its spectrum -- they publish before they wait, so one
@@ -1588,54 +1378,9 @@ __global__ __launch_bounds__(kPkThreads) void k_peaks(BatchArgs a, Workspace w, 
         w.scores[b0 + p] = score_peak(sm, a.N, w.det_l[b0 + p], w.det_c[b0 + p], w.det_r[b0 + p]);
 }
 
-__global__ __launch_bounds__(kPkWords) void k_peaks_write(BatchArgs a, Workspace w, int detector_only) {
-    const int s = blockIdx.y, chunk = blockIdx.x;
-    __shared__ int lds_i[kPkWords / 64 + 1];
-    __shared__ long long lds_l[kPkWords / 64 + 1];
-    if (w.status[s]) return;
-    const int nch = (w.W + kPkWords - 1) / kPkWords;
-    const int32_t* cnt = w.peak_cnt + (size_t)s * 2 * nch;
-    long long before = 0, k_all = 0, b_all = 0;
-    for (int k = threadIdx.x; k < nch; k += kPkWords) {
-        before += k < chunk ? cnt[2 * k] : 0;
-        k_all += cnt[2 * k];
-        b_all += cnt[2 * k + 1];
-    }
-    before = block_sum_ll<kPkWords>(before, lds_l);
-    k_all = block_sum_ll<kPkWords>(k_all, lds_l);
-    b_all = block_sum_ll<kPkWords>(b_all, lds_l);
-    if (b_all == 0) {
-        if (chunk == 0 && threadIdx.x == 0) w.status[s] = MDG_NO_PEAKS_DETECTED;
-        return;
-    }
-    if (chunk == 0 && threadIdx.x == 0) w.det_count[s] = (int32_t)k_all;
-    const int wd = chunk * kPkWords + threadIdx.x;
-    int bordered = 0, kept = 0;
-    if (wd < w.W) kept = word_peaks<false>(a, w, s, wd, detector_only, &bordered, 0);
-    int total;
-    const int o = block_exclusive_scan<kPkWords>(kept, lds_i, &total);
-    if (kept) word_peaks<true>(a, w, s, wd, detector_only, &bordered, (size_t)s * w.capD + before + o);
-}
-
 // ----------------------------------------------------------------------------------
 // K4  noise-score selection (noise_score_filter.rs:91-138, scorer.rs:65-75, common.rs:26-40)
 // ----------------------------------------------------------------------------------
-
-// ScorerMinimumSum::score_peak (scorer.rs:65-75) for every detected peak, one
-// thread per peak over many workgroups: min(sum |D[l..=c]|, sum |D[c..=r]|) with
-// D[k] = (y[k-1] - 2 y[k]) + y[k+1], both sums left folds in k order. The
-// smoothed values of a chunk of 8 ticks are loaded together (clamped addresses),
-// so a peak costs one memory latency per 8 ticks instead of one per tick.
-__global__ void k_scores(BatchArgs a, Workspace w) {
-    const int s = blockIdx.y;
-    if (w.status[s]) return;
-    const int P = w.det_count[s];
-    const size_t base = (size_t)s * w.capD;
-    const double* __restrict__ sm = w.smooth_ptr + (size_t)s * w.smooth_stride;
-    const int N = a.N;
-    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x)
-        w.scores[base + p] = score_peak(sm, N, w.det_l[base + p], w.det_c[base + p], w.det_r[base + p]);
-}
 
 // Left fold over the signal-free-region scores peaks[..left] ++ peaks[right..P]
 // in the reference's order (noise_score_filter.rs:129-138), by ONE wave. Terms
@@ -2424,18 +2169,6 @@ __device__ __forceinline__ void fit_init_pair(const BatchArgs& a, const Workspac
     }
 }
 
-// The selection kernels initialise the fit of the peaks they select
-// (fit_init_peak / fit_init_pair), so the pipeline has no separate launch for it;
-// k_fit_init is the stand-alone form (MDG_DIAG_DUP=fitinit re-runs it).
-__global__ void k_fit_init(BatchArgs a, Workspace w) {
-    const int s = blockIdx.y;
-    if (w.status[s]) return;
-    const int P = w.sel_count[s];
-    const size_t base = (size_t)s * w.capD;
-    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x)
-        fit_init_peak(a, w, s, base, p, w.sel_l[base + p], w.sel_c[base + p], w.sel_r[base + p]);
-}
-
 // K6  fit superposition at the 3P reduced points + ratio (fitter_analytical.rs:40-47)
 // Ping-pong range flags: iteration `it` reads unsafe[it&1] (written by the
 // producer of its parameters) and clears unsafe[(it+1)&1] for k_fit_update(it).
@@ -2443,272 +2176,6 @@ __global__ void k_fit_init(BatchArgs a, Workspace w) {
 // count is reached skips the remaining superposition/update launches
 __device__ __forceinline__ bool fit_done(const Workspace& w, int s, int it) {
     return w.fit_iters_s && it >= w.fit_iters_s[s];
-}
-
-__device__ __forceinline__ bool fit_fast(const Workspace& w, int s, int it) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) w.unsafe[4 * s + ((it + 1) & 1)] = 0;
-    return w.x_ok[s] && w.unsafe[4 * s + (it & 1)] == 0;
-}
-
-// fold the first r < 16 terms of a row-replicated group (see fold16)
-__device__ __forceinline__ void fold_partial(double& acc, double t, double one, int r) {
-    switch (r) {
-        case 1:
-            asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) : "+v"(acc) : "v"(t), "v"(one));
-            break;
-        case 2:
-            asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) MDG_FMAC_BCAST(1) : "+v"(acc) : "v"(t), "v"(one));
-            break;
-        case 3:
-            asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) MDG_FMAC_BCAST(1) MDG_FMAC_BCAST(2) : "+v"(acc) : "v"(t), "v"(one));
-            break;
-        case 4:
-            asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) MDG_FMAC_BCAST(1) MDG_FMAC_BCAST(2) MDG_FMAC_BCAST(3) : "+v"(acc) : "v"(t), "v"(one));
-            break;
-        case 5:
-            asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) MDG_FMAC_BCAST(1) MDG_FMAC_BCAST(2) MDG_FMAC_BCAST(3) MDG_FMAC_BCAST(4) : "+v"(acc) : "v"(t), "v"(one));
-            break;
-        case 6:
-            asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) MDG_FMAC_BCAST(1) MDG_FMAC_BCAST(2) MDG_FMAC_BCAST(3) MDG_FMAC_BCAST(4) MDG_FMAC_BCAST(5) : "+v"(acc) : "v"(t), "v"(one));
-            break;
-        case 7:
-            asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) MDG_FMAC_BCAST(1) MDG_FMAC_BCAST(2) MDG_FMAC_BCAST(3) MDG_FMAC_BCAST(4) MDG_FMAC_BCAST(5) MDG_FMAC_BCAST(6) : "+v"(acc) : "v"(t), "v"(one));
-            break;
-        case 8:
-            asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) MDG_FMAC_BCAST(1) MDG_FMAC_BCAST(2) MDG_FMAC_BCAST(3) MDG_FMAC_BCAST(4) MDG_FMAC_BCAST(5) MDG_FMAC_BCAST(6) MDG_FMAC_BCAST(7) : "+v"(acc) : "v"(t), "v"(one));
-            break;
-        case 9:
-            asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) MDG_FMAC_BCAST(1) MDG_FMAC_BCAST(2) MDG_FMAC_BCAST(3) MDG_FMAC_BCAST(4) MDG_FMAC_BCAST(5) MDG_FMAC_BCAST(6) MDG_FMAC_BCAST(7) MDG_FMAC_BCAST(8) : "+v"(acc) : "v"(t), "v"(one));
-            break;
-        case 10:
-            asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) MDG_FMAC_BCAST(1) MDG_FMAC_BCAST(2) MDG_FMAC_BCAST(3) MDG_FMAC_BCAST(4) MDG_FMAC_BCAST(5) MDG_FMAC_BCAST(6) MDG_FMAC_BCAST(7) MDG_FMAC_BCAST(8) MDG_FMAC_BCAST(9) : "+v"(acc) : "v"(t), "v"(one));
-            break;
-        case 11:
-            asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) MDG_FMAC_BCAST(1) MDG_FMAC_BCAST(2) MDG_FMAC_BCAST(3) MDG_FMAC_BCAST(4) MDG_FMAC_BCAST(5) MDG_FMAC_BCAST(6) MDG_FMAC_BCAST(7) MDG_FMAC_BCAST(8) MDG_FMAC_BCAST(9) MDG_FMAC_BCAST(10) : "+v"(acc) : "v"(t), "v"(one));
-            break;
-        case 12:
-            asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) MDG_FMAC_BCAST(1) MDG_FMAC_BCAST(2) MDG_FMAC_BCAST(3) MDG_FMAC_BCAST(4) MDG_FMAC_BCAST(5) MDG_FMAC_BCAST(6) MDG_FMAC_BCAST(7) MDG_FMAC_BCAST(8) MDG_FMAC_BCAST(9) MDG_FMAC_BCAST(10) MDG_FMAC_BCAST(11) : "+v"(acc) : "v"(t), "v"(one));
-            break;
-        case 13:
-            asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) MDG_FMAC_BCAST(1) MDG_FMAC_BCAST(2) MDG_FMAC_BCAST(3) MDG_FMAC_BCAST(4) MDG_FMAC_BCAST(5) MDG_FMAC_BCAST(6) MDG_FMAC_BCAST(7) MDG_FMAC_BCAST(8) MDG_FMAC_BCAST(9) MDG_FMAC_BCAST(10) MDG_FMAC_BCAST(11) MDG_FMAC_BCAST(12) : "+v"(acc) : "v"(t), "v"(one));
-            break;
-        case 14:
-            asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) MDG_FMAC_BCAST(1) MDG_FMAC_BCAST(2) MDG_FMAC_BCAST(3) MDG_FMAC_BCAST(4) MDG_FMAC_BCAST(5) MDG_FMAC_BCAST(6) MDG_FMAC_BCAST(7) MDG_FMAC_BCAST(8) MDG_FMAC_BCAST(9) MDG_FMAC_BCAST(10) MDG_FMAC_BCAST(11) MDG_FMAC_BCAST(12) MDG_FMAC_BCAST(13) : "+v"(acc) : "v"(t), "v"(one));
-            break;
-        case 15:
-            asm volatile("s_nop 1\n" MDG_FMAC_BCAST(0) MDG_FMAC_BCAST(1) MDG_FMAC_BCAST(2) MDG_FMAC_BCAST(3) MDG_FMAC_BCAST(4) MDG_FMAC_BCAST(5) MDG_FMAC_BCAST(6) MDG_FMAC_BCAST(7) MDG_FMAC_BCAST(8) MDG_FMAC_BCAST(9) MDG_FMAC_BCAST(10) MDG_FMAC_BCAST(11) MDG_FMAC_BCAST(12) MDG_FMAC_BCAST(13) MDG_FMAC_BCAST(14) : "+v"(acc) : "v"(t), "v"(one));
-            break;
-        default:
-            break;
-    }
-}
-
-// fold16 of ei into acc, interleaved with the FAST evaluation (lorentz_t<true>:
-// (x - mp)^2 + hw, then div_rn_fast's sequence, one Newton step) of the next group, returned:
-// two independent dependency chains share the issue slots
-__device__ __forceinline__ double fold16_eval_fast(double& acc, double ei, double one, double x,
-                                                   double sf, double hw, double mp) {
-    double eo, d, den, r, t, q;
-    asm volatile(
-        "s_nop 1\n"
-        "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:0 row_mask:0xf bank_mask:0xf\n"
-        "v_add_f64 %[d], %[x], -%[mp]\n"
-        "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:1 row_mask:0xf bank_mask:0xf\n"
-        "v_mul_f64 %[d], %[d], %[d]\n"
-        "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:2 row_mask:0xf bank_mask:0xf\n"
-        "v_add_f64 %[den], %[hw], %[d]\n"
-        "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:3 row_mask:0xf bank_mask:0xf\n"
-        "v_rcp_f64 %[r], %[den]\n"
-        "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:4 row_mask:0xf bank_mask:0xf\n"
-        "v_fma_f64 %[t], -%[den], %[r], 1.0\n"
-        "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:5 row_mask:0xf bank_mask:0xf\n"
-        "v_fma_f64 %[r], %[r], %[t], %[r]\n"
-        "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:6 row_mask:0xf bank_mask:0xf\n"
-        "v_fma_f64 %[t], -%[den], %[r], 1.0\n"
-        "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:7 row_mask:0xf bank_mask:0xf\n"
-        "v_fma_f64 %[r], %[r], %[t], %[r]\n"
-        "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
-        "v_mul_f64 %[q], %[sf], %[r]\n"
-        "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:9 row_mask:0xf bank_mask:0xf\n"
-        "v_fma_f64 %[t], -%[den], %[q], %[sf]\n"
-        "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:10 row_mask:0xf bank_mask:0xf\n"
-        "v_fma_f64 %[eo], %[t], %[r], %[q]\n"
-        "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:11 row_mask:0xf bank_mask:0xf\n"
-        "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:12 row_mask:0xf bank_mask:0xf\n"
-        "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:13 row_mask:0xf bank_mask:0xf\n"
-        "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:14 row_mask:0xf bank_mask:0xf\n"
-        "v_fmac_f64_dpp %[acc], %[ei], %[one] row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
-        : [acc] "+v"(acc), [eo] "=&v"(eo), [d] "=&v"(d), [den] "=&v"(den), [r] "=&v"(r),
-          [t] "=&v"(t), [q] "=&v"(q)
-        : [ei] "v"(ei), [one] "v"(one), [x] "v"(x), [sf] "v"(sf), [hw] "v"(hw), [mp] "v"(mp));
-    return eo;
-}
-
-// Two independent 4-point sets (A, B) per wave: fold16 of both into their sums,
-// interleaved with the FAST evaluation of the next group for both (same peaks,
-// different x) -- four dependency chains share the issue slots.
-__device__ __forceinline__ void fold2_eval_fast(double& accA, double& accB, double& eA, double& eB,
-                                                double one, double xA, double xB, double sf,
-                                                double hw, double mp) {
-    double eoA, dA, denA, rA, tA, qA; double eoB, dB, denB, rB, tB, qB;
-    asm volatile(
-        "s_nop 1\n"
-        "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:0 row_mask:0xf bank_mask:0xf\n"
-        "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:0 row_mask:0xf bank_mask:0xf\n"
-        "v_add_f64 %[dA], %[xA], -%[mp]\n"
-        "v_add_f64 %[dB], %[xB], -%[mp]\n"
-        "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:1 row_mask:0xf bank_mask:0xf\n"
-        "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:1 row_mask:0xf bank_mask:0xf\n"
-        "v_mul_f64 %[dA], %[dA], %[dA]\n"
-        "v_mul_f64 %[dB], %[dB], %[dB]\n"
-        "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:2 row_mask:0xf bank_mask:0xf\n"
-        "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:2 row_mask:0xf bank_mask:0xf\n"
-        "v_add_f64 %[denA], %[hw], %[dA]\n"
-        "v_add_f64 %[denB], %[hw], %[dB]\n"
-        "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:3 row_mask:0xf bank_mask:0xf\n"
-        "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:3 row_mask:0xf bank_mask:0xf\n"
-        "v_rcp_f64 %[rA], %[denA]\n"
-        "v_rcp_f64 %[rB], %[denB]\n"
-        "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:4 row_mask:0xf bank_mask:0xf\n"
-        "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:4 row_mask:0xf bank_mask:0xf\n"
-        "v_fma_f64 %[tA], -%[denA], %[rA], 1.0\n"
-        "v_fma_f64 %[tB], -%[denB], %[rB], 1.0\n"
-        "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:5 row_mask:0xf bank_mask:0xf\n"
-        "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:5 row_mask:0xf bank_mask:0xf\n"
-        "v_fma_f64 %[rA], %[rA], %[tA], %[rA]\n"
-        "v_fma_f64 %[rB], %[rB], %[tB], %[rB]\n"
-        "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:6 row_mask:0xf bank_mask:0xf\n"
-        "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:6 row_mask:0xf bank_mask:0xf\n"
-        "v_fma_f64 %[tA], -%[denA], %[rA], 1.0\n"
-        "v_fma_f64 %[tB], -%[denB], %[rB], 1.0\n"
-        "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:7 row_mask:0xf bank_mask:0xf\n"
-        "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:7 row_mask:0xf bank_mask:0xf\n"
-        "v_fma_f64 %[rA], %[rA], %[tA], %[rA]\n"
-        "v_fma_f64 %[rB], %[rB], %[tB], %[rB]\n"
-        "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
-        "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
-        "v_mul_f64 %[qA], %[sf], %[rA]\n"
-        "v_mul_f64 %[qB], %[sf], %[rB]\n"
-        "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:9 row_mask:0xf bank_mask:0xf\n"
-        "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:9 row_mask:0xf bank_mask:0xf\n"
-        "v_fma_f64 %[tA], -%[denA], %[qA], %[sf]\n"
-        "v_fma_f64 %[tB], -%[denB], %[qB], %[sf]\n"
-        "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:10 row_mask:0xf bank_mask:0xf\n"
-        "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:10 row_mask:0xf bank_mask:0xf\n"
-        "v_fma_f64 %[eoA], %[tA], %[rA], %[qA]\n"
-        "v_fma_f64 %[eoB], %[tB], %[rB], %[qB]\n"
-        "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:11 row_mask:0xf bank_mask:0xf\n"
-        "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:11 row_mask:0xf bank_mask:0xf\n"
-        "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:12 row_mask:0xf bank_mask:0xf\n"
-        "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:12 row_mask:0xf bank_mask:0xf\n"
-        "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:13 row_mask:0xf bank_mask:0xf\n"
-        "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:13 row_mask:0xf bank_mask:0xf\n"
-        "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:14 row_mask:0xf bank_mask:0xf\n"
-        "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:14 row_mask:0xf bank_mask:0xf\n"
-        "v_fmac_f64_dpp %[accA], %[eiA], %[one] row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
-        "v_fmac_f64_dpp %[accB], %[eiB], %[one] row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
-        : [accA] "+v"(accA), [accB] "+v"(accB), [eoA] "=&v"(eoA), [dA] "=&v"(dA), [denA] "=&v"(denA), [rA] "=&v"(rA), [tA] "=&v"(tA), [qA] "=&v"(qA), [eoB] "=&v"(eoB), [dB] "=&v"(dB), [denB] "=&v"(denB), [rB] "=&v"(rB), [tB] "=&v"(tB), [qB] "=&v"(qB)
-        : [eiA] "v"(eA), [eiB] "v"(eB), [one] "v"(one), [xA] "v"(xA), [xB] "v"(xB), [sf] "v"(sf),
-          [hw] "v"(hw), [mp] "v"(mp));
-    eA = eoA;
-    eB = eoB;
-}
-
-// K6c  fit superposition for the smallest batches (B <= 4): a wave evaluates 4
-// reduced points x 16 Lorentzians per instruction (16-lane row = one point) and
-// folds each 16-peak group into its row's running sum with row_newbcast DPP adds
-// (fold16), in peak order -- the reference's summation (lorentzian.rs:606-611),
-// bit-identical to K6. 3P/4 waves instead of 3P/64, so a single spectrum spreads
-// over the whole chip; peak parameters are staged in LDS in chunks of kFitChunk.
-constexpr int kFitChunk = 2048;
-template <bool FAST>
-__device__ __forceinline__ void fit_dpp_body(const BatchArgs& a, const Workspace& w, int s, int P,
-                                             double* lds_p) {
-    const size_t base = (size_t)s * w.capD;
-    const double* __restrict__ params = w.params + 3 * base;
-    const int lane = threadIdx.x & 63, sub = lane & 15;
-    const int n_pts = 3 * P;
-    const int tiles = (n_pts + 31) / 32;  // 32 points per 256-thread workgroup, 8 per wave
-    const double one = 1.0;
-    KSTAMP(20);
-    for (int tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
-        const int iA = tile * 32 + (threadIdx.x >> 6) * 8 + (lane >> 4), iB = iA + 4;
-        const double xA = w.rx[3 * base + min(iA, n_pts - 1)];
-        const double xB = w.rx[3 * base + min(iB, n_pts - 1)];
-        double accA = -0.0, accB = -0.0;
-        for (int c0 = 0; c0 < P; c0 += kFitChunk) {
-            const int cn = min(kFitChunk, P - c0);
-            __syncthreads();
-            {
-                // coalesced copy of the chunk's {sfhw, hw2, maxp} triples, all loads in
-                // flight (fixed trip count, clamped addresses, predicated LDS writes)
-                constexpr int PER = 3 * kFitChunk / 256;
-                const double* src = params + 3 * (size_t)c0;
-                const int nd = 3 * cn;
-                double v[PER];
-#pragma unroll
-                for (int u = 0; u < PER; ++u) v[u] = src[min(u * 256 + (int)threadIdx.x, nd - 1)];
-#pragma unroll
-                for (int u = 0; u < PER; ++u)
-                    if (u * 256 + (int)threadIdx.x < nd) lds_p[u * 256 + threadIdx.x] = v[u];
-            }
-            __syncthreads();
-            KSTAMP(21);
-            const int G = cn / 16;
-            if constexpr (FAST) {
-                // software-pipelined: fold group k-1 while evaluating group k, the
-                // parameters of group k+1 read from LDS one step ahead (sets P / Q)
-                if (G > 0) {
-                    auto ld = [&](int grp, double& f, double& h, double& m) {
-                        const int j = 16 * min(grp, G - 1) + sub;  // clamped: never divergent
-                        f = lds_p[3 * j];
-                        h = lds_p[3 * j + 1];
-                        m = lds_p[3 * j + 2];
-                    };
-                    const double f0 = lds_p[3 * sub], h0 = lds_p[3 * sub + 1], m0 = lds_p[3 * sub + 2];
-                    double eA = lorentz_t<true>(xA, f0, h0, m0), eB = lorentz_t<true>(xB, f0, h0, m0);
-                    double fP, hP, mP, fQ, hQ, mQ;
-                    ld(1, fP, hP, mP);
-                    int k = 1;  // next group to evaluate
-                    for (; k + 2 <= G; k += 2) {
-                        ld(k + 1, fQ, hQ, mQ);
-                        fold2_eval_fast(accA, accB, eA, eB, one, xA, xB, fP, hP, mP);
-                        ld(k + 2, fP, hP, mP);
-                        fold2_eval_fast(accA, accB, eA, eB, one, xA, xB, fQ, hQ, mQ);
-                    }
-                    if (k < G) fold2_eval_fast(accA, accB, eA, eB, one, xA, xB, fP, hP, mP);
-                    fold16(accA, eA, one);
-                    fold16(accB, eB, one);
-                }
-            } else {
-                for (int g = 0; g < G; ++g) {
-                    const int j = 16 * g + sub;
-                    const double f = lds_p[3 * j], h = lds_p[3 * j + 1], m = lds_p[3 * j + 2];
-                    fold16(accA, lorentz_t<false>(xA, f, h, m), one);
-                    fold16(accB, lorentz_t<false>(xB, f, h, m), one);
-                }
-            }
-            if (16 * G < cn) {
-                const int jj = min(16 * G + sub, cn - 1);
-                const double f = lds_p[3 * jj], h = lds_p[3 * jj + 1], m = lds_p[3 * jj + 2];
-                fold_partial(accA, lorentz_t<FAST>(xA, f, h, m), one, cn - 16 * G);
-                fold_partial(accB, lorentz_t<FAST>(xB, f, h, m), one, cn - 16 * G);
-            }
-        }
-        KSTAMP(22);
-        if (sub == 0 && iA < n_pts) w.ratio[3 * base + iA] = w.ry[3 * base + iA] / accA;
-        if (sub == 0 && iB < n_pts) w.ratio[3 * base + iB] = w.ry[3 * base + iB] / accB;
-    }
-    KSTAMP(23);
-}
-
-__global__ __launch_bounds__(256) void k_fit_sup_dpp(BatchArgs a, Workspace w, int it) {
-    __shared__ double lds_p[3 * kFitChunk];  // {sfhw, hw2, maxp} of one chunk of peaks
-    const int s = blockIdx.y;
-    if (w.status[s] || fit_done(w, s, it)) return;
-    const int P = w.sel_count[s];
-    if (fit_fast(w, s, it)) fit_dpp_body<true>(a, w, s, P, lds_p);
-    else fit_dpp_body<false>(a, w, s, P, lds_p);
 }
 
 // K6e  fit superposition + stencil update, term-fold form (small batches). A
@@ -2860,7 +2327,6 @@ struct TwShape {
     static constexpr int LDS = 2 * Q * RS;
     static_assert(Q % 3 == 0 && Q / 3 <= 64 && Q <= 64 && Q % PS == 0, "tile shape");
 };
-using TwDefault = TwShape<63, 2, 3>;
 
 
 template <bool FAST, class SH>
@@ -2875,6 +2341,13 @@ __device__ __forceinline__ void fit_tw_body(const Workspace& w, int s, int P, in
     const double* __restrict__ params = params_version(w, base, it);
     const bool folder = wv == EW;
     if (folder) __builtin_amdgcn_s_setprio(3);
+    // diagnostic builds (tools/ubench/fit_diag.hip): per-wave cycle sums -- evaluator
+    // 0 eval, 1 barrier, 5 prologue loads; fold wave 2 fold, 3 barrier, 6 first wait,
+    // 4 stencil update; slot 7 = the wave's start time
+    DIAG_DECL
+#ifdef MDG_DIAG
+    _d_acc[7] = _d_t;
+#endif
     for (int tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
         const int p0 = tile * QQ;
         if (!folder) {
@@ -2888,6 +2361,10 @@ __device__ __forceinline__ void fit_tw_body(const Workspace& w, int s, int P, in
             const int jl = pb * 64 + lane;
             int j = min(jl, P - 1);
             double f = params[3 * j], h = params[3 * j + 1], m = params[3 * j + 2];
+#ifdef MDG_DIAG
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::"v"(f), "v"(h), "v"(m), "s"(xq[0]));
+            DIAG_STAMP(5);
+#endif
             for (int c = 0; c <= nch; ++c) {
                 if (c < nch) {
                     double* Tb = T + (c & 1) * QQ * RS + ps * QS * RS + jl;
@@ -2903,7 +2380,9 @@ __device__ __forceinline__ void fit_tw_body(const Workspace& w, int s, int P, in
 #pragma unroll
                     for (int q = 0; q < QS; ++q) Tb[q * RS] = lorentz_t<FAST>(xq[q], cf, ch, cm);
                 }
+                DIAG_STAMP(0);
                 lds_barrier();
+                DIAG_STAMP(1);
             }
         } else {
             double acc = -0.0;
@@ -2911,6 +2390,7 @@ __device__ __forceinline__ void fit_tw_body(const Workspace& w, int s, int P, in
             double one = 1.0;
             asm volatile("" : "+v"(one));
             lds_barrier();  // chunk 0 written
+            DIAG_STAMP(6);
             for (int c = 0; c < nch; ++c) {
                 const double2* row = (const double2*)(T + (c & 1) * QQ * RS + q * RS);
                 const int cn = min(J, P - c * J);
@@ -2925,7 +2405,9 @@ __device__ __forceinline__ void fit_tw_body(const Workspace& w, int s, int P, in
                     const double* r1 = (const double*)row;
                     for (int k = 0; k < cn; ++k) acc = __builtin_fma(r1[k], one, acc);
                 }
+                DIAG_STAMP(2);
                 lds_barrier();
+                DIAG_STAMP(3);
             }
             // stencil update of the tile's peaks: lane k gathers the ratios y/sup of
             // its peak's three points from lanes 3k..3k+2
@@ -2947,8 +2429,10 @@ __device__ __forceinline__ void fit_tw_body(const Workspace& w, int s, int P, in
                 solve(sq, L);
                 if (!peak_fast_ok(L[0], L[1], L[2])) atomicAdd(&w.unsafe[4 * s + (it + 1) % 3], 1);
             }
+            DIAG_STAMP(4);
         }
     }
+    DIAG_FLUSH();
 }
 
 template <class SH>
@@ -2976,327 +2460,6 @@ __global__ void k_fit_sup(BatchArgs a, Workspace w, int it) {
     for (int i = part * blockDim.x + threadIdx.x; i < 3 * P; i += parts * blockDim.x) {
         const double sup = superpose(w.rx[3 * base + i], params, P, fast);
         w.ratio[3 * base + i] = w.ry[3 * base + i] / sup;
-    }
-}
-
-// K6f  fit superposition with the stencil update fused (batches, B > 8): one point
-// per lane and each lane's left fold over the P Lorentzians as in k_fit_sup, but a
-// 256-thread workgroup owns 255 consecutive points = 85 whole peaks, so after the
-// superposition the ratios meet in LDS and 85 threads do k_fit_update's work for
-// their peak (scale the stencil by the ratios, mirror_shoulder, solve). Version it+1
-// of the parameters goes into the other buffer (params / params_alt, as the
-// term-fold kernels do), because other workgroups still read version it: one launch
-// per fit iteration instead of two. Range flags rotate over three slots as in
-// k_fit_sup_tf: iteration it reads slot it % 3, its updates count into (it+1) % 3,
-// and it clears (it+2) % 3 (last read by iteration it-1).
-constexpr int kFuPts = 255;  // points per workgroup: 85 peaks
-
-__global__ __launch_bounds__(256) void k_fit_sup_fu(BatchArgs a, Workspace w, int it) {
-    const int s = blockIdx.x % a.B, part = blockIdx.x / a.B, parts = gridDim.x / a.B;
-    __shared__ double rat[256];
-    if (w.status[s] || fit_done(w, s, it)) return;
-    const int P = w.sel_count[s];
-    const int npts = 3 * P;
-    const size_t base = (size_t)s * w.capD;
-    if (part == 0 && threadIdx.x == 0) w.unsafe[4 * s + (it + 2) % 3] = 0;
-    const bool fast = w.x_ok[s] && w.unsafe[4 * s + it % 3] == 0;
-    const double* __restrict__ prm = params_version(w, base, it);
-    double* __restrict__ next = (double*)params_version(w, base, it + 1);
-    const int tid = threadIdx.x;
-    for (int t = part; t * kFuPts < npts; t += parts) {  // uniform over the workgroup
-        const int i = t * kFuPts + tid;
-        double ratio = 0.0;
-        if (tid < kFuPts && i < npts) {
-            const double sup = superpose(w.rx[3 * base + i], prm, P, fast);
-            ratio = w.ry[3 * base + i] / sup;  // fitter_analytical.rs:42-47
-        }
-        rat[tid] = ratio;
-        __syncthreads();
-        const int pk = t * (kFuPts / 3) + tid;
-        if (tid < kFuPts / 3 && pk < P) {  // fitter_analytical.rs:48-65
-            double* st = w.stencil + 6 * base + 6 * (size_t)pk;
-            Stencil q{st[0], st[1], st[2], st[3], st[4], st[5]};
-            q.y1 = q.y1 * rat[3 * tid];
-            q.y2 = q.y2 * rat[3 * tid + 1];
-            q.y3 = q.y3 * rat[3 * tid + 2];
-            mirror_shoulder(q);
-            st[0] = q.x1; st[1] = q.x2; st[2] = q.x3; st[3] = q.y1; st[4] = q.y2; st[5] = q.y3;
-            double* L = next + 3 * (size_t)pk;
-            solve(q, L);
-            if (!peak_fast_ok(L[0], L[1], L[2])) atomicAdd(&w.unsafe[4 * s + (it + 1) % 3], 1);
-        }
-        __syncthreads();
-    }
-}
-
-// K6q  work-queue fit superposition (batches): the same per-point left folds as
-// k_fit_sup, but a point's fold over the P Lorentzians is cut into kDynPieces
-// consecutive ranges, and persistent workgroups pull (64-point chunk, piece) items
-// from eight queue heads (one per XCD group of blocks, blockIdx % 8; a workgroup
-// whose queue is empty takes from the others). Items are ordered piece-major, so a
-// launch's tail is a fraction of a piece instead of a whole 2048-term fold: with one
-// 64-point chunk per wave and every fold as long as the others, the static grid of
-// k_fit_sup leaves SIMDs idle for up to a whole fold at its end (at B = 256 about a
-// tenth of the launch). A piece k > 0 continues the fold from the
-// partial sum piece k-1 left: it waits for the chunk's counter to reach it*K + k
-// (the item was taken earlier, by a running wave, so the wait always ends), then
-// loads the 64 partial sums. Hand-off per MI355X_MICROARCH.md (valid forms): the
-// producer stores its sums write-through (agent-scope relaxed atomic stores, sc1),
-// drains them with s_waitcnt vmcnt(0), and one lane stores the counter (agent
-// scope); the consumer polls it with sc1 loads and loads the sums with sc1 loads.
-// Each point's operations are the reference's, in its order: bit-identical.
-// ctl layout (int32): [0] chunks per spectrum; [64 + 32 * (slot * 8 + q)] queue
-// head q of iteration slot (it & 1), each on its own 128-B line; [kFitDynCtl + chunk]
-// the chunk's progress (it * K + pieces done; monotone, zeroed per pipeline).
-constexpr int kDynPiecesDefault = 4;  // MDG_DYN_PIECES overrides (tuning)
-#ifdef MDG_DYN_DEBUG
-constexpr unsigned kDynSpins = 1u << 16;
-#else
-constexpr unsigned kDynSpins = 1u << 22;
-#endif
-
-__global__ __launch_bounds__(1024) void k_fit_plan(BatchArgs a, Workspace w) {
-    __shared__ int pmax;
-    if (threadIdx.x == 0) pmax = 0;
-    __syncthreads();
-    int m = 0;
-    for (int s = threadIdx.x; s < a.B; s += blockDim.x)
-        if (w.status[s] == 0) m = max(m, w.sel_count[s]);
-    atomicMax(&pmax, m);
-    __syncthreads();
-    const int CH = max(1, (3 * pmax + 63) / 64);
-    int32_t* ctl = w.fit_dyn;
-    if (threadIdx.x == 0) ctl[0] = CH;
-    if (threadIdx.x < 16) ctl[64 + 32 * threadIdx.x] = 0;
-    for (int q = threadIdx.x; q < a.B * CH; q += blockDim.x) ctl[kFitDynCtl + q] = 0;
-}
-
-__global__ __launch_bounds__(256) void k_fit_sup_dyn(BatchArgs a, Workspace w, int it, int kDynPieces) {
-    int32_t* ctl = w.fit_dyn;
-    const int CH = ctl[0];
-    const int nq = a.B * CH;
-    const int lane = threadIdx.x & 63;
-    const int slot = it & 1;
-    if (blockIdx.x == 0) {
-        // the next iteration's heads, and the range flags its k_fit_update counts into
-        if (threadIdx.x < 8) ctl[64 + 32 * ((slot ^ 1) * 8 + threadIdx.x)] = 0;
-        for (int s = threadIdx.x; s < a.B; s += blockDim.x)
-            if (!fit_done(w, s, it)) w.unsafe[4 * s + ((it + 1) & 1)] = 0;
-    }
-    const int home = blockIdx.x & 7;
-    for (int qi = 0; qi < 8; ++qi) {
-        const int x = (home + qi) & 7;
-        const int nx = (nq - x + 7) / 8;  // chunks x, x + 8, ... of the batch
-        const int items = nx * kDynPieces;
-        int32_t* head = ctl + 64 + 32 * (slot * 8 + x);
-        for (;;) {
-            int j = 0;
-            if (lane == 0) j = __hip_atomic_fetch_add(head, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            j = __builtin_amdgcn_readfirstlane(j);
-            if (j >= items) break;
-            const int k = j / nx;
-            const int ch = x + 8 * (j - k * nx);
-            const int s = ch / CH, c = ch - s * CH;
-            if (w.status[s] || fit_done(w, s, it)) continue;
-            const int P = w.sel_count[s];
-            const int npts = 3 * P;
-            if (c * 64 >= npts) continue;
-            const size_t base = (size_t)s * w.capD;
-            const bool fast = w.x_ok[s] && w.unsafe[4 * s + (it & 1)] == 0;
-            const int T = (P + kDynPieces - 1) / kDynPieces;
-            const int lo = min(P, k * T), hi = min(P, lo + T);
-            const int i = c * 64 + lane;
-            const double xv = w.rx[3 * base + min(i, npts - 1)];
-            double* part = w.fit_part + (size_t)ch * 64 + lane;
-            int32_t* done = ctl + kFitDynCtl + ch;
-            double acc = -0.0;
-            if (k > 0) {
-                // every value the wave branches on is read into an SGPR (readfirstlane):
-                // the waits and the stores below stay wave-uniform control flow
-                const int need = it * kDynPieces + k;
-                unsigned spins = 0;
-                int have = __builtin_amdgcn_readfirstlane(
-                    __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                while (have < need && spins < kDynSpins) {
-                    __builtin_amdgcn_s_sleep(1);
-                    ++spins;
-                    have = __builtin_amdgcn_readfirstlane(
-                        __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                }
-                if (have < need) {  // never expected: bounds a protocol bug
-#ifdef MDG_DYN_DEBUG
-                    if (lane == 0)
-                        printf("dyn spin fail: it %d item j %d (queue %d, nx %d) k %d ch %d s %d c %d P %d need %d "
-                               "have %d CH %d block %d\n", it, j, x, nx, k, ch, s, c, P, need, have, CH,
-                               (int)blockIdx.x);
-#endif
-                    w.status[s] = MDG_ERR_HIP;
-                    continue;
-                }
-                acc = __hip_atomic_load(part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            const double* prm = w.params + 3 * base + 3 * (size_t)lo;
-            acc = fast ? superpose_t<true>(xv, prm, hi - lo, acc) : superpose_t<false>(xv, prm, hi - lo, acc);
-            if (k < kDynPieces - 1) {
-                __hip_atomic_store(part, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                // every lane stores the same counter value: no lane-dependent branch
-                __hip_atomic_store(done, it * kDynPieces + k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } else if (i < npts) {
-                w.ratio[3 * base + i] = w.ry[3 * base + i] / acc;  // fitter_analytical.rs:42-47
-            }
-        }
-    }
-}
-
-// EXPERIMENT (configs[2] "superposition recast as MFMA outer product", SURVEY
-// 8d): the fit superposition with every denominator hw2 + (x - maxp)^2 taken
-// from v_mfma_f64_16x16x4_f64 as the product [x'^2, x', 1, 0] . [1, -2m', m'^2 +
-// hw2, 0] with x' = x - c, m' = maxp - c centred on the tile's first point (to
-// keep the cancellation near a peak small). A wave owns 16 points (A rows) and
-// walks the peaks 16 at a time (B columns); lane l then holds the denominators
-// of peak 16t + (l & 15) at points (l >> 4) + 4r, r = 0..3, divides sfhw by them
-// (div_rn under the fast flags) and accumulates per lane; the 16 lanes of a DPP
-// row then add their partial sums. NOT bit-identical (the denominators round
-// differently and the sum is reordered): selected only by MDG_FITSUP=mfma, and
-// measured against the oracle in tools/mfma_experiment.py.
-template <bool FAST>
-__device__ __forceinline__ void fit_mfma_tile(const Workspace& w, size_t base, int P, int p0, int npts,
-                                              const double* __restrict__ params) {
-    typedef double v4d __attribute__((ext_vector_type(4)));
-    const int lane = threadIdx.x & 63;
-    const int col = lane & 15, kk = lane >> 4;
-    const double* rx = w.rx + 3 * base;
-    const double c = rx[min(p0, npts - 1)];
-    const double xa = rx[min(p0 + col, npts - 1)] - c;  // A: row = point p0 + col
-    const double a = kk == 0 ? xa * xa : kk == 1 ? xa : kk == 2 ? 1.0 : 0.0;
-    double acc[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int j0 = 0; j0 < P; j0 += 16) {
-        const int j = min(j0 + col, P - 1);
-        const double f = params[3 * j], h = params[3 * j + 1], m = params[3 * j + 2] - c;
-        const double b = kk == 0 ? 1.0 : kk == 1 ? -2.0 * m : kk == 2 ? m * m + h : 0.0;
-        v4d d = {0.0, 0.0, 0.0, 0.0};
-        d = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, d, 0, 0, 0);
-        if (j0 + col < P) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) acc[r] += FAST ? div_rn(f, d[r]) : f / d[r];
-        }
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) acc[r] += __shfl_xor(acc[r], o, 16);
-    }
-    if (col == 0) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int i = p0 + kk + 4 * r;
-            if (i < npts) w.ratio[3 * base + i] = w.ry[3 * base + i] / acc[r];
-        }
-    }
-}
-
-__global__ __launch_bounds__(256) void k_fit_sup_mfma(BatchArgs a, Workspace w, int it) {
-    const int s = blockIdx.x % a.B, part = blockIdx.x / a.B, parts = gridDim.x / a.B;
-    if (w.status[s] || fit_done(w, s, it)) return;
-    const int P = w.sel_count[s];
-    const size_t base = (size_t)s * w.capD;
-    const double* __restrict__ params = w.params + 3 * base;
-    if (part == 0 && threadIdx.x == 0) w.unsafe[4 * s + ((it + 1) & 1)] = 0;
-    const bool fast = w.x_ok[s] && w.unsafe[4 * s + (it & 1)] == 0;
-    const int npts = 3 * P, wv = threadIdx.x >> 6;
-    for (int p0 = (part * 4 + wv) * 16; p0 < npts; p0 += parts * 64) {
-        if (fast) fit_mfma_tile<true>(w, base, P, p0, npts, params);
-        else fit_mfma_tile<false>(w, base, P, p0, npts, params);
-    }
-}
-
-// K6b  fit superposition for small batches (B*3P too small to fill 256 CUs with
-// one thread per point). A 1024-thread workgroup owns Q reduced points; the
-// evaluations of a chunk of J peaks are spread over (point, peak) lane pairs and
-// parked in LDS, then one wave folds them into each point's running sum in peak
-// order -- the reference's exact summation order (lorentzian.rs:606-611), so the
-// result is bit-identical to K6 while every CU does divisions. Chunks are
-// triple-buffered: the evals of chunk c overlap the fold of chunk c-1, a buffer is
-// rewritten only two barriers after its fold, and the folding wave rotates.
-// The next chunk's parameters are prefetched into registers across the barrier.
-template <int Q, int J, int BS>
-__global__ __launch_bounds__(BS) void k_fit_sup_split(BatchArgs a, Workspace w, int it) {
-    constexpr int SUBS = BS / Q;      // peak lanes per point
-    constexpr int EPT = J / SUBS;     // evals per thread per chunk
-    constexpr int NW = BS / 64;
-    static_assert(Q <= 64 && J % SUBS == 0, "shape");
-    const int s = blockIdx.y;
-    __shared__ double ev[3][J][Q];
-    __shared__ double accs[Q];
-    if (w.status[s] || fit_done(w, s, it)) return;
-    const int P = w.sel_count[s];
-    const size_t base = (size_t)s * w.capD;
-    const double* __restrict__ params = w.params + 3 * base;
-    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-    const int pt = tid % Q;
-    const int sub = tid / Q;
-    const int npts = 3 * P;
-    const int nch = (P + J - 1) / J;
-    const bool fast = fit_fast(w, s, it);
-    for (int g0 = blockIdx.x * Q; g0 < npts; g0 += gridDim.x * Q) {
-        const int i = g0 + pt;
-        const double xi = i < npts ? w.rx[3 * base + i] : 0.0;
-        double pf[EPT][3];
-#pragma unroll
-        for (int r = 0; r < EPT; ++r) {
-            const int j = sub + SUBS * r;
-            const bool ok = j < P;
-            pf[r][0] = ok ? params[3 * j] : 0.0;
-            pf[r][1] = ok ? params[3 * j + 1] : 1.0;
-            pf[r][2] = ok ? params[3 * j + 2] : 0.0;
-        }
-        for (int c = 0; c <= nch; ++c) {
-            if (c < nch) {
-                double (*e)[Q] = ev[c % 3];
-                double v[EPT];
-                if (fast) {
-#pragma unroll
-                    for (int r = 0; r < EPT; ++r) v[r] = lorentz_t<true>(xi, pf[r][0], pf[r][1], pf[r][2]);
-                } else {
-#pragma unroll
-                    for (int r = 0; r < EPT; ++r) v[r] = lorentz_t<false>(xi, pf[r][0], pf[r][1], pf[r][2]);
-                }
-#pragma unroll
-                for (int r = 0; r < EPT; ++r) e[sub + SUBS * r][pt] = v[r];
-                // prefetch chunk c+1 (out-of-range peaks evaluate to 0 and are never folded)
-#pragma unroll
-                for (int r = 0; r < EPT; ++r) {
-                    const int j = (c + 1) * J + sub + SUBS * r;
-                    const bool ok = j < P;
-                    pf[r][0] = ok ? params[3 * j] : 0.0;
-                    pf[r][1] = ok ? params[3 * j + 1] : 1.0;
-                    pf[r][2] = ok ? params[3 * j + 2] : 0.0;
-                }
-            }
-            lds_barrier();
-            if (c > 0) {
-                const int cc = c - 1;
-                if (wv == cc % NW && lane < Q) {
-                    const double (*e)[Q] = ev[cc % 3];
-                    const int jn = min(J, P - cc * J);
-                    double acc = cc == 0 ? -0.0 : accs[lane];
-                    if (jn == J) {
-#pragma unroll 16
-                        for (int jl = 0; jl < J; ++jl) acc += e[jl][lane];
-                    } else {
-                        for (int jl = 0; jl < jn; ++jl) acc += e[jl][lane];
-                    }
-                    accs[lane] = acc;
-                }
-            }
-        }
-        __syncthreads();
-        if (tid < Q && g0 + tid < npts) {
-            const double sup = nch > 0 ? accs[tid] : -0.0;
-            w.ratio[3 * base + g0 + tid] = w.ry[3 * base + g0 + tid] / sup;
-        }
-        __syncthreads();
     }
 }
 
@@ -3475,130 +2638,9 @@ __device__ __forceinline__ int64_t mse_len(const Workspace& w, int s) {
 }
 
 template <int BS>
-__global__ __launch_bounds__(BS) void k_mse_partial(BatchArgs a, Workspace w, int nparts) {
-    // 1-D grid, spectrum = block % B: round-robin dispatch puts blocks w and w+256 on
-    // the same CU, so the workgroups resident on a CU share one spectrum's
-    // Lorentzians in the scalar cache (B dividing 256) instead of streaming several
-    const int s = blockIdx.x % a.B, part = blockIdx.x / a.B;
-    __shared__ double red[BS / 64];
-    if (w.status[s] || w.mse_panic[s]) return;
-    const int P = w.kept_count[s];
-    const double* __restrict__ kept = w.kept + 3 * (size_t)s * w.capD;
-    const double* x = a.x + (size_t)s * a.x_stride;
-    const double* y = a.y + (size_t)s * a.y_stride;
-    const int nig = w.n_ig[s];
-    const int64_t total = mse_len(w, s);
-    const bool fast = w.x_ok[s] && w.unsafe_kept[s] == 0;
-    double acc = 0.0;
-    for (int64_t v = (int64_t)part * BS + threadIdx.x; v < total; v += (int64_t)nparts * BS) {
-        const int64_t idx = mse_index(w, s, nig, v);
-        const double sup = superpose(x[idx], kept, P, fast);
-        const double d = sup - y[idx];
-        acc += d * d;
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double t = 0.0;
-        for (int k = 0; k < BS / 64; ++k) t += red[k];
-        w.mse_part[(size_t)s * nparts + part] = t;
-    }
-}
-
-// NPT points per thread: with 91.8k signal-region points, one point
-// per lane needs 1434 waves on 1024 SIMDs, so 410 SIMDs run two waves back to back;
-// two points per lane fit every thread block on its own SIMDs (718 waves) with two
-// independent evaluations per term. Same per-point folds, same residual order
-// within a thread (point i before i + 1), then the same shuffle / LDS tree.
-template <int BS>
 __device__ __forceinline__ void mse_publish_fold(const BatchArgs& a, const Workspace& w, int s, int part,
                                                  int nparts, double acc, int kept_n, double* parts);
 __device__ __forceinline__ void mse_panic_out(const BatchArgs& a, int s);
-
-// The last workgroup of a spectrum to finish (arrival counter, acq_rel at agent
-// scope: the partials of the others are visible to it) folds the partials itself
-// (k_mse_final's work, one launch fewer) and resets the counter.
-template <int BS, int NPT>
-__global__ __launch_bounds__(BS) void k_mse_partial_n(BatchArgs a, Workspace w, int nparts) {
-    const int s = blockIdx.x % a.B, part = blockIdx.x / a.B;
-    __shared__ double red[BS / 64];
-    __shared__ int last;
-    if (w.status[s]) return;  // already reported by k_retain
-    if (w.mse_panic[s]) {
-        if (part == 0) mse_panic_out(a, s);
-        return;
-    }
-    const int P = w.kept_count[s];
-    const double* __restrict__ kept = w.kept + 3 * (size_t)s * w.capD;
-    const double* x = a.x + (size_t)s * a.x_stride;
-    const double* y = a.y + (size_t)s * a.y_stride;
-    const int nig = w.n_ig[s];
-    const int64_t total = mse_len(w, s);
-    const bool fast = w.x_ok[s] && w.unsafe_kept[s] == 0;
-    double acc = 0.0;
-    for (int64_t v0 = (int64_t)part * BS * NPT + threadIdx.x; v0 < total;
-         v0 += (int64_t)nparts * BS * NPT) {
-        double xv[NPT], yv[NPT];
-        bool ok[NPT];
-#pragma unroll
-        for (int i = 0; i < NPT; ++i) {
-            const int64_t v = v0 + (int64_t)i * BS;
-            ok[i] = v < total;
-            const int64_t idx = mse_index(w, s, nig, ok[i] ? v : 0);
-            xv[i] = x[idx];
-            yv[i] = y[idx];
-        }
-        double sup[NPT];
-        if (fast) superpose_n<true, NPT>(xv, kept, P, sup);
-        else superpose_n<false, NPT>(xv, kept, P, sup);
-#pragma unroll
-        for (int i = 0; i < NPT; ++i) {
-            const double d = sup[i] - yv[i];
-            if (ok[i]) acc += d * d;
-        }
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double t = 0.0;
-        for (int k = 0; k < BS / 64; ++k) t += red[k];
-        // sc1 store, its completion, then the arrival (the smoother's hand-off; an
-        // acq_rel RMW here writes back L2 in every workgroup: +10 us at B = 1)
-        __hip_atomic_store(w.mse_part + (size_t)s * nparts + part, t, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int done = __hip_atomic_fetch_add(w.mse_done + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = done == nparts - 1;
-        if (last) __hip_atomic_store(w.mse_done + s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    if (!last) return;
-    __shared__ double parts[1024];
-    for (int k = threadIdx.x; k < nparts; k += BS) parts[k] = ld_sc1(w.mse_part + (size_t)s * nparts + k);
-    __syncthreads();
-    if (threadIdx.x < 64) {
-        // dpp_fold's order (groups of 16 by row broadcast, then the remainder) on the
-        // LDS copy; dpp_fold itself streams with global loads, which LDS cannot serve
-        const int sub = threadIdx.x & 15;
-        const double one = 1.0;
-        double t = 0.0;
-        const int G = nparts / 16;
-        for (int g = 0; g < G; ++g) fold16(t, parts[16 * g + sub], one);
-        const int r = nparts - 16 * G;
-        if (r > 0) {
-            const double v = parts[min(16 * G + sub, nparts - 1)];
-            for (int k = 0; k < r; ++k) t += readlane_f64(v, k);
-        }
-        if (threadIdx.x == 0) {
-            a.out_mse[s] = t / (double)mse_len(w, s);
-            a.out_status[s] = (w.kept_count[s] > a.cap) ? MDG_CAPACITY : MDG_OK;
-        }
-    }
-}
 
 // ----------------------------------------------------------------------------------
 // MSE superposition with one division per four Lorentzians (k_mse_quad).
@@ -3634,112 +2676,6 @@ __device__ __forceinline__ double quad_term(double x, const double (&c)[12]) {
     const double r1 = __builtin_fma(r0, __builtin_fma(-D, r0, 1.0), r0);
     const double q0 = N * r1;
     return __builtin_fma(__builtin_fma(-D, q0, N), r1, q0);
-}
-
-// acc[i] += sum over Lorentzians [j0, j1) of point x[i]; FAST: quads (j1 - j0 any)
-template <bool FAST, int NPT>
-__device__ __forceinline__ void sup_range_quad(const double (&x)[NPT], const_f64_ptr params, int j0,
-                                               int j1, double (&acc)[NPT]) {
-    int j = j0;
-    if (FAST && j1 - j0 >= 4) {
-        const int nq = (j1 - j0) / 4;
-        double A[12], B[12];
-#pragma unroll
-        for (int k = 0; k < 12; ++k) A[k] = params[3 * j + k];
-        int q = 0;
-        for (; q + 2 <= nq; q += 2) {
-            const const_f64_ptr nb = params + 3 * (j + 4);
-#pragma unroll
-            for (int k = 0; k < 12; ++k) B[k] = nb[k];
-            double t[NPT];
-#pragma unroll
-            for (int i = 0; i < NPT; ++i) t[i] = quad_term(x[i], A);
-#pragma unroll
-            for (int i = 0; i < NPT; ++i) acc[i] += t[i];
-            const int jn = (q + 2 < nq) ? j + 8 : j + 4;  // next A (re-read of B's at the end)
-            const const_f64_ptr na = params + 3 * jn;
-#pragma unroll
-            for (int k = 0; k < 12; ++k) A[k] = na[k];
-#pragma unroll
-            for (int i = 0; i < NPT; ++i) t[i] = quad_term(x[i], B);
-#pragma unroll
-            for (int i = 0; i < NPT; ++i) acc[i] += t[i];
-            j += 8;
-        }
-        if (q < nq) {
-#pragma unroll
-            for (int i = 0; i < NPT; ++i) acc[i] += quad_term(x[i], A);
-            j += 4;
-        }
-    }
-    for (; j < j1; ++j) {
-        const const_f64_ptr L = params + 3 * j;
-#pragma unroll
-        for (int i = 0; i < NPT; ++i) acc[i] += lorentz_mse<FAST>(x[i], L[0], L[1], L[2]);
-    }
-}
-
-template <int NPT>
-__global__ __launch_bounds__(256) void k_mse_quad(BatchArgs a, Workspace w, int nparts) {
-    constexpr int BS = 256, NW = 4, PTS = 64 * NPT;
-    const int s = blockIdx.x % a.B, part = blockIdx.x / a.B;
-    __shared__ double psum[NW - 1][PTS];
-    if (w.status[s]) return;  // already reported by k_retain
-    if (w.mse_panic[s]) {
-        if (part == 0) mse_panic_out(a, s);
-        return;
-    }
-    const int P = w.kept_count[s];
-    const const_f64_ptr kept = (const_f64_ptr)(w.kept + 3 * (size_t)s * w.capD);
-    const double* x = a.x + (size_t)s * a.x_stride;
-    const double* y = a.y + (size_t)s * a.y_stride;
-    const int nig = w.n_ig[s];
-    const int64_t total = mse_len(w, s);
-    const bool fast = w.x_ok[s] && w.unsafe_kept[s] == 0;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    // wave wv's Lorentzians: [j0, j1), quad-aligned split
-    const int per = ((P + 4 * NW - 1) / (4 * NW)) * 4;
-    const int j0 = min(P, wv * per), j1 = min(P, j0 + per);
-    double acc = 0.0;
-    for (int64_t v0 = (int64_t)part * PTS; v0 < total; v0 += (int64_t)nparts * PTS) {
-        double xv[NPT], yv[NPT];
-        bool ok[NPT];
-#pragma unroll
-        for (int i = 0; i < NPT; ++i) {
-            const int64_t v = v0 + lane + 64 * i;
-            ok[i] = v < total;
-            const int64_t idx = mse_index(w, s, nig, ok[i] ? v : 0);
-            xv[i] = x[idx];
-            yv[i] = wv == 0 ? y[idx] : 0.0;
-        }
-        double sup[NPT];
-#pragma unroll
-        for (int i = 0; i < NPT; ++i) sup[i] = 0.0;
-        if (fast) sup_range_quad<true, NPT>(xv, kept, j0, j1, sup);
-        else sup_range_quad<false, NPT>(xv, kept, j0, j1, sup);
-        if (wv > 0) {
-#pragma unroll
-            for (int i = 0; i < NPT; ++i) psum[wv - 1][lane + 64 * i] = sup[i];
-        }
-        __syncthreads();
-        if (wv == 0) {
-#pragma unroll
-            for (int i = 0; i < NPT; ++i) {
-                double t = sup[i];
-#pragma unroll
-                for (int k = 0; k < NW - 1; ++k) t += psum[k][lane + 64 * i];
-                const double d = t - yv[i];
-                if (ok[i]) acc += d * d;
-            }
-        }
-        __syncthreads();
-    }
-    if (wv == 0) {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-    }
-    __shared__ double parts[kMseMaxParts];
-    mse_publish_fold<BS>(a, w, s, part, nparts, acc, w.kept_count[s], parts);
 }
 
 // Thread 0's acc is this workgroup's partial of spectrum s: publish it, count the
@@ -4059,35 +2995,11 @@ __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int
     mse_publish_fold<BS>(a, w, s, part, nparts, tot, kept_n, red);
 }
 
-// total length of the MSE regions of spectrum s (the divisor of compute_mse)
-
-// One wave per spectrum: the nparts partial sums are folded left to right from +0.0
-// (the order k_mse_partial's tree fixes) with the ordered DPP fold, instead of a
-// single thread whose dependent global loads cost ~200 cycles each (42 us at B=1).
-// the nparts partials of spectrum s, folded by one wave (threads 0..63)
-__device__ __forceinline__ void mse_finish(const BatchArgs& a, const Workspace& w, int s,
-                                           const double* part, int nparts) {
-    const double t = dpp_fold(0.0, part, nparts);
-    if (threadIdx.x != 0) return;
-    a.out_mse[s] = t / (double)mse_len(w, s);
-    a.out_status[s] = (w.kept_count[s] > a.cap) ? MDG_CAPACITY : MDG_OK;
-}
-
 __device__ __forceinline__ void mse_panic_out(const BatchArgs& a, int s) {
     if (threadIdx.x == 0) {
         a.out_status[s] = MDG_REFERENCE_PANIC;
         a.out_mse[s] = 0.0;
     }
-}
-
-__global__ __launch_bounds__(64) void k_mse_final(BatchArgs a, Workspace w, int nparts) {
-    const int s = blockIdx.x;
-    if (w.status[s]) return;  // already reported by k_retain
-    if (w.mse_panic[s]) {
-        mse_panic_out(a, s);
-        return;
-    }
-    mse_finish(a, w, s, w.mse_part + (size_t)s * nparts, nparts);
 }
 
 // ----------------------------------------------------------------------------------
@@ -4120,6 +3032,50 @@ __global__ __launch_bounds__(64) void k_exact_fold(const double* __restrict__ t,
         len += hi - lo;
     }
     if (threadIdx.x == 0) out[0] = total / (double)len;
+}
+
+// Exact-order MSE of a whole batch (mdg_settings.options & MDG_OPTION_EXACT_MSE),
+// after k_mse_local has compacted the retained Lorentzians: compute_mse
+// (deconvoluter.rs:828-862) in the reference's operation order.
+// k_mse_exact_res: the squared residual of every MSE-region point, in the regions'
+// virtual concatenation order (row s of res, res_row doubles apart): the point's
+// superposition is superposition_vec's in-order left fold over the retained
+// Lorentzians (lorentzian.rs:606-611; superpose, bit-identical to the oracle --
+// the fit's exact division), then (sup - y)^2 (`.powi(2)` is one multiply).
+// 1-D grid, spectrum = block % B (k_fit_sup's layout: workgroups resident on a CU at
+// once share one spectrum's Lorentzians in the scalar cache).
+__global__ void k_mse_exact_res(BatchArgs a, Workspace w, double* res, int64_t res_row) {
+    const int s = blockIdx.x % a.B, part = blockIdx.x / a.B, parts = gridDim.x / a.B;
+    if (w.status[s] || w.mse_panic[s]) return;
+    const int P = w.kept_count[s];
+    const double* __restrict__ kept = w.kept + 3 * (size_t)s * w.capD;
+    const double* x = a.x + (size_t)s * a.x_stride;
+    const double* y = a.y + (size_t)s * a.y_stride;
+    const int nig = w.n_ig[s];
+    const int64_t total = mse_len(w, s);
+    const bool fast = w.x_ok[s] && w.unsafe_kept[s] == 0;
+    double* r = res + (size_t)s * res_row;
+    for (int64_t v = (int64_t)part * blockDim.x + threadIdx.x; v < total; v += (int64_t)parts * blockDim.x) {
+        const int64_t idx = mse_index(w, s, nig, v);
+        const double d = superpose(x[idx], kept, P, fast) - y[idx];
+        r[v] = d * d;
+    }
+}
+
+// k_mse_exact_fold: one wave per spectrum folds each region's squared residuals left
+// to right from -0.0 (`.sum::<f64>()`), adds the region sums in region order (the
+// outer `.sum::<f64>()`) and divides by the regions' total length; it overwrites the
+// MSE k_mse_local wrote (its status stays).
+__global__ __launch_bounds__(64) void k_mse_exact_fold(BatchArgs a, Workspace w, const double* res,
+                                                       int64_t res_row) {
+    const int s = blockIdx.x;
+    if (w.status[s] || w.mse_panic[s]) return;
+    const int nig = w.n_ig[s];
+    const int64_t* cum = w.ig_cum + (size_t)s * (w.ig_cap + 2);
+    const double* r = res + (size_t)s * res_row;
+    double total = -0.0;
+    for (int k = 0; k <= nig; ++k) total += dpp_fold(-0.0, r + cum[k], (int)(cum[k + 1] - cum[k]));
+    if (threadIdx.x == 0) a.out_mse[s] = total / (double)cum[nig + 1];
 }
 
 __global__ void k_range_check(const double* __restrict__ x, int64_t n,
@@ -4184,8 +3140,9 @@ void launch_prep(const BatchArgs& a, const Workspace& w, hipStream_t st) {
     launch_k(k_prep, dim3(cdiv(a.B, 64)), dim3(64), 0, st, a, w);
 }
 
-// throughput diagnostic (MDG_DIAG_PAD, mdg_capi.hip): a launch that does nothing,
-// with the pipeline's kernel arguments
+#ifdef MDG_DIAG
+// throughput diagnostic (MDG_DIAG_PAD, mdg_capi.hip; diagnostic builds only): a
+// launch that does nothing, with the pipeline's kernel arguments
 __global__ void k_diag_nop(BatchArgs a, Workspace w) {
     if (a.B < 0) w.status[0] = 0;
 }
@@ -4200,19 +3157,7 @@ void launch_diag_nop(const BatchArgs& a, const Workspace& w, hipStream_t st) {
         launch_k(k_diag_nop, dim3(g ? std::max(1, std::atoi(g)) : 1), dim3(g ? 256 : 64), 0, st, a, w);
     }
 }
-template <int WS>
-static const char* launch_waves(const BatchArgs& a, const Workspace& w, int iters, hipStream_t st) {
-    constexpr int U = WS * ((32 + WS - 1) / WS);
-    constexpr int RAWSLOT = ((U * 8 + 255) / 256) * 32;
-    const size_t lds = sizeof(double) * (4 * RAWSLOT + (size_t)iters * 4 * U);
-    const int waves = (iters + 3) / 4 * 4;
-    launch_k(k_smooth_waves<WS>, dim3(a.B), dim3(64 * waves), lds, st, a, w, iters);
-    static const char* names[] = {"", "", "k_smooth_waves<2>", "k_smooth_waves<3>", "k_smooth_waves<4>",
-                                  "k_smooth_waves<5>", "k_smooth_waves<6>", "k_smooth_waves<7>",
-                                  "k_smooth_waves<8>", "k_smooth_waves<9>", "", "k_smooth_waves<11>"};
-    return names[WS];
-}
-
+#endif
 template <int WS>
 static const char* launch_pipe(const BatchArgs& a, const Workspace& w, int iters, hipStream_t st) {
     const int spw = 64 / iters;
@@ -4255,8 +3200,8 @@ bool smooth_uses_chain(const BatchArgs& a, const Workspace& w, int iters, int ws
 const char* launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int ws, hipStream_t st,
                           int fused_prep) {
     // the chain kernel; then lane-pipelined (window fits the register FIFO); the
-    // one-lane-per-spectrum kernel otherwise (wave-per-pass only when forced).
-    // MDG_SMOOTH = chain | waves | pipe | generic forces one (tests); an
+    // one-lane-per-spectrum kernel otherwise.
+    // MDG_SMOOTH = chain | pipe | generic forces one (tests); an
     // unsupported shape falls through. fused_prep (chain only): the chain kernel
     // runs k_prep's work itself.
     const char* force = std::getenv("MDG_SMOOTH");
@@ -4272,25 +3217,10 @@ const char* launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int
             default: break;
         }
     }
-    // beyond the chain's batch limit the lane-pipelined kernel beats one wave per
-    // pass (tools/smooth_sweep.sh: 131072 points, B = 1024: 4.8 against 9.9 ms;
-    // configs[3], 4096 x 65536: 2.7 against 17.0 ms), so the wave kernel is only
-    // taken when forced
-    const bool waves = force && std::string(force) == "waves";
-    if (waves && iters >= 1 && iters <= 8 && a.N > ws + 1) {
-        switch (ws) {
-            case 2: return launch_waves<2>(a, w, iters, st);
-            case 3: return launch_waves<3>(a, w, iters, st);
-            case 4: return launch_waves<4>(a, w, iters, st);
-            case 5: return launch_waves<5>(a, w, iters, st);
-            case 6: return launch_waves<6>(a, w, iters, st);
-            case 7: return launch_waves<7>(a, w, iters, st);
-            case 8: return launch_waves<8>(a, w, iters, st);
-            case 9: return launch_waves<9>(a, w, iters, st);
-            case 11: return launch_waves<11>(a, w, iters, st);
-            default: break;
-        }
-    }
+    // beyond the chain's batch limit the lane-pipelined kernel (tools/smooth_sweep.sh:
+    // 131072 points, B = 1024: 4.8 ms; configs[3], 4096 x 65536: 2.7 ms; round 2's
+    // wave-per-pass kernel took 9.9 and 17.0); windows outside its
+    // register FIFO the one-lane-per-spectrum kernel
     const bool pipe = !force || std::string(force) == "pipe";
     if (pipe && iters >= 1 && iters <= 32 && a.N > ws + 1) {
         switch (ws) {
@@ -4312,22 +3242,12 @@ const char* launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int
 void launch_flags(const BatchArgs& a, const Workspace& w, hipStream_t st) {
     launch_k(k_flags, dim3(cdiv(a.N, 256), a.B), dim3(256), 0, st, a, w);
 }
-bool peaks_score() { return !std::getenv("MDG_PEAKS_NOSCORE") && !std::getenv("MDG_PEAKS_2PASS"); }
 const char* launch_peaks(const BatchArgs& a, const Workspace& w, int detector_only, hipStream_t st) {
     const int nch = cdiv(w.W, kPkWords);
     static_assert(kPkWords == 256, "k_flags clears ceil(W / 256) slots");
-    if (std::getenv("MDG_PEAKS_2PASS")) {  // the two-kernel form, for comparison
-        launch_k(k_peaks_count, dim3(nch, a.B), dim3(kPkWords), 0, st, a, w, detector_only);
-        launch_k(k_peaks_write, dim3(nch, a.B), dim3(kPkWords), 0, st, a, w, detector_only);
-        return "k_flags+k_peaks_count+k_peaks_write";
-    }
-    // k_peaks scores the peaks it writes (no k_scores launch) unless MDG_PEAKS_NOSCORE
-    launch_k(k_peaks, dim3(nch, a.B), dim3(kPkThreads), 0, st, a, w, detector_only, peaks_score() ? 1 : 0);
+    // k_peaks scores the peaks it writes (scorer.rs:65-75) for the selector
+    launch_k(k_peaks, dim3(nch, a.B), dim3(kPkThreads), 0, st, a, w, detector_only, 1);
     return "k_flags+k_peaks";
-}
-void launch_scores(const BatchArgs& a, const Workspace& w, hipStream_t st) {
-    const int gx = std::max(1, std::min(64, 4096 / std::max(1, a.B)));
-    launch_k(k_scores, dim3(gx, a.B), dim3(256), 0, st, a, w);
 }
 const char* launch_select(const BatchArgs& a, const Workspace& w, int detector_only,
                           double threshold, hipStream_t st) {
@@ -4336,128 +3256,46 @@ const char* launch_select(const BatchArgs& a, const Workspace& w, int detector_o
         return "k_select_detector_only";
     }
     launch_k(k_select<1024>, dim3(a.B), dim3(1024), 0, st, a, w, threshold);
-    return "k_scores+k_select<1024>";
+    return "k_select<1024>";
 }
-void launch_fit_init(const BatchArgs& a, const Workspace& w, int gx, hipStream_t st) {
-    launch_k(k_fit_init, dim3(gx, a.B), dim3(256), 0, st, a, w);
-}
-// Fit kernel choice by measurement (tools/fit_sweep.sh, P = 2048, ms per 10 launches):
-//   B=1 tf 0.215 / dpp 0.277 / plain 0.81;  B=2 tf 0.369 / dpp 0.428;
-//   B=4 dpp 0.589 / tf 0.668;  B=8 dpp 1.37 / plain 1.44 / tf 1.46;
-//   B=12 plain 1.57 / dpp 1.96;  B=256 plain 12.0 / tf 25.4 / dpp 30.6.
-// B=1 uses the wide-tile term fold tw<63, 1, 7> (98 workgroups instead of 256):
-// bench spectra/s alone 1021 vs 1007 (tf), 16 concurrent contexts 5715-5742 vs
-// 4555-5139; at B = 2..8 it is slower alone (1607 vs 1648 at B=2, 2249 vs 2624 at
-// B=4) though faster with 16 contexts, so those keep tf / dpp.
-// MDG_FITSUP = tf | tw | tw3 | tw4 | tw7 | tw9 | tw14 | dpp | split | plain forces one.
+// Fit kernel choice by batch size, fit time per spectrum alone: B <= 2
+// the 24-point term fold over one workgroup per tile ("tf": 212 / 149 us at B = 1 /
+// 2, latency 0.88 ms at B = 1 against 0.95 for "tw7"); B <= 24 the 63-point term
+// fold over one workgroup per tile ("tw7": 120 / 113 / 93 us at B = 4 / 8 / 16);
+// beyond, one point per lane with the update separate ("plain": 79 / 57 us at B =
+// 32 / 256). When other engine contexts on the device have run pipelines, B = 1
+// keeps "tw7": "tf"'s lead alone is gone as soon as a second context has been used
+// (latency 0.95 ms either way), and 18 concurrent B = 1 pipelines run 6.6k
+// spectra/s with "tf" against 7.8-8.1k with "tw7". The kernels measured and
+// rejected in rounds 2-3 are not in the library. MDG_FITSUP = tf |
+// tw7 | plain forces one of the three (all bit-identical; tests, measurements);
+// any other value is ignored.
 static std::string fit_choice(const BatchArgs& a) {
-    const char* force = std::getenv("MDG_FITSUP");
-    if (force && *force) return force;
-    // By batch size, fit time per spectrum alone: B <= 2 the 24-point
-    // term fold over one workgroup per tile ("tf": 212 / 149 us at B = 1 / 2, latency
-    // 0.88 ms at B = 1 against 0.95 for "tw7"); B <= 24 the 63-point term fold over
-    // one workgroup per tile ("tw7": 120 / 113 / 93 us at B = 4 / 8 / 16 against 167 /
-    // 187 / 118 for "dpp" / "dpp" / "plain"); beyond, one point per lane with the
-    // update separate ("plain": 79 / 57 us at B = 32 / 256). The fused k_fit_sup_fu
-    // ("fu") is as fast as "plain" alone but slower in the queue.
-    // When other engine contexts on the device have run pipelines, B = 1 keeps "tw7":
-    // "tf"'s lead alone is gone as soon as a second context has been used (latency
-    // 0.95 ms either way, the spectrum still alone on the GPU), and 18 concurrent
-    // B = 1 pipelines run 6.6k spectra/s with "tf" against 7.8-8.1k with "tw7".
+    if (const char* force = std::getenv("MDG_FITSUP")) {
+        const std::string f(force);
+        if (f == "tf" || f == "tw7" || f == "plain") return f;
+    }
     if (a.B == 1 && a.contexts > 1) return "tw7";
     return a.B <= 2 ? "tf" : a.B <= 24 ? "tw7" : "plain";
 }
-bool fit_sup_dyn(const BatchArgs& a) { return fit_choice(a) == "dyn"; }
-static int dyn_pieces() {
-    const char* e = std::getenv("MDG_DYN_PIECES");
-    return e ? std::max(1, std::min(64, std::atoi(e))) : kDynPiecesDefault;
-}
-void launch_fit_plan(const BatchArgs& a, const Workspace& w, hipStream_t st) {
-    launch_k(k_fit_plan, dim3(1), dim3(1024), 0, st, a, w);
-}
-bool fit_sup_fused(const BatchArgs& a) {
-    const std::string f = fit_choice(a);
-    return f == "tf" || f == "fu" || f.rfind("tw", 0) == 0;
-}
+bool fit_sup_fused(const BatchArgs& a) { return fit_choice(a) != "plain"; }
 const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st) {
     const std::string f = fit_choice(a);
-    if (f.rfind("tw", 0) == 0) {
-        // 63 points per workgroup: 98 workgroups at P = 2048, grid-stride beyond
-        // MDG_TW_G (tuning): workgroups per spectrum (tiles beyond them grid-stride)
-        // one workgroup per 63-point tile of a 2048-peak spectrum (98; more tiles
-        // grid-stride): every spectrum of a small batch spreads over the CUs.
-        // (Round 2 used max(2, 128 / B) for 18 concurrent B = 1 streams.)
-        const char* tg = std::getenv("MDG_TW_G");
+    // MDG_TW_G (tuning): workgroups per spectrum; tiles beyond them grid-stride
+    const char* tg = std::getenv("MDG_TW_G");
+    if (f == "tw7") {
+        // 7 evaluator waves: 1 peak block x 7 point subsets, 63 points per workgroup:
+        // one workgroup per tile of a 2048-peak spectrum (98)
+        using SH = TwShape<63, 1, 7>;
         const int g = tg ? std::max(1, std::atoi(tg)) : (3 * 2048 + 62) / 63;
-        if (f == "tw4") {  // 4 evaluator waves: 2 peak blocks x 2 point subsets (Q = 60)
-            using SH = TwShape<60, 2, 2>;
-            launch_k(k_fit_sup_tw<SH>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
-            return "k_fit_sup_tw<60, 2, 2>";
-        }
-        if (f == "tw7") {  // 7 evaluator waves: 1 peak block x 7 point subsets (Q = 63)
-            using SH = TwShape<63, 1, 7>;
-            launch_k(k_fit_sup_tw<SH>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
-            return "k_fit_sup_tw<63, 1, 7>";
-        }
-        if (f == "tw3") {
-            using SH = TwShape<63, 1, 3>;
-            launch_k(k_fit_sup_tw<SH>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
-            return "k_fit_sup_tw<63, 1, 3>";
-        }
-        if (f == "tw9") {
-            using SH = TwShape<63, 1, 9>;
-            launch_k(k_fit_sup_tw<SH>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
-            return "k_fit_sup_tw<63, 1, 9>";
-        }
-        if (f == "tw14") {  // 2 peak blocks x 7 point subsets
-            using SH = TwShape<63, 2, 7>;
-            launch_k(k_fit_sup_tw<SH>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
-            return "k_fit_sup_tw<63, 2, 7>";
-        }
-        using SH = TwDefault;
         launch_k(k_fit_sup_tw<SH>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
-        return "k_fit_sup_tw<63, 2, 3>";
+        return "k_fit_sup_tw<63, 1, 7>";
     }
     if (f == "tf") {
-        // 24 points per workgroup: 256 workgroups at P = 2048, grid-stride beyond
-        // one workgroup per 24-point tile of a 2048-peak spectrum (256)
-        const char* tg = std::getenv("MDG_TW_G");
+        // 24 points per workgroup: one workgroup per tile of a 2048-peak spectrum (256)
         const int g = tg ? std::max(1, std::atoi(tg)) : (3 * 2048 + 23) / 24;
         launch_k(k_fit_sup_tf, dim3(g, a.B), dim3(64 * (kTfEW + 1)), 0, st, a, w, it);
         return "k_fit_sup_tf";
-    } else if (f == "dpp") {
-        // 32 points per workgroup: 192 workgroups at P = 2048, grid-stride beyond
-        const int g = std::max(64, std::min(512, 1024 / a.B));
-        launch_k(k_fit_sup_dpp, dim3(g, a.B), dim3(256), 0, st, a, w, it);
-        return "k_fit_sup_dpp";
-    } else if (f == "mfma") {
-        // experiment only (not bit-exact): 64 points per workgroup
-        const int g = std::max(1, std::min(2048, (3 * (a.N / 2 + 2) + 63) / 64));
-        const int parts = std::max(1, std::min(g, 8192 / a.B));
-        launch_k(k_fit_sup_mfma, dim3(parts * a.B), dim3(256), 0, st, a, w, it);
-        return "k_fit_sup_mfma";
-    } else if (f == "split") {
-        // 16 points per 1024-thread workgroup: 3P/16 workgroups per spectrum (384 at
-        // P = 2048) keep every CU busy; grid-stride beyond that
-        const int g = std::max(64, std::min(1024, 2048 / a.B));
-        launch_k((k_fit_sup_split<16, 128, 1024>), dim3(g, a.B), dim3(1024), 0, st, a, w, it);
-        return "k_fit_sup_split<16, 128, 1024>";
-    }
-    if (f == "dyn") {
-        // persistent: 7 workgroups per CU (the SGPR-limited occupancy of the fold);
-        // MDG_DYN_WPC / MDG_DYN_PIECES override the workgroups per CU and the pieces
-        // per fold (tuning; the pieces must not change within a pipeline run)
-        const char* e = std::getenv("MDG_DYN_WPC");
-        const int wpc = e ? std::max(1, std::min(16, std::atoi(e))) : 7;
-        launch_k(k_fit_sup_dyn, dim3(256 * wpc), dim3(256), 0, st, a, w, it, dyn_pieces());
-        return "k_fit_sup_dyn";
-    }
-    if (f == "fu") {
-        // 255 points per workgroup: 25 workgroups per spectrum at P = 2048
-        // (6144 points), grid-stride beyond
-        const int parts = std::max(1, (3 * 2048 + kFuPts - 1) / kFuPts);
-        launch_k(k_fit_sup_fu, dim3(parts * a.B), dim3(256), 0, st, a, w, it);
-        return "k_fit_sup_fu";
     }
     // gx 256-thread workgroups per spectrum (24: one point per thread at P = 2048)
     launch_k(k_fit_sup, dim3(gx * a.B), dim3(256), 0, st, a, w, it);
@@ -4469,79 +3307,37 @@ void launch_fit_update(const BatchArgs& a, const Workspace& w, int gx, int it, h
 void launch_retain(const BatchArgs& a, const Workspace& w, hipStream_t st) {
     launch_k(k_retain<1024>, dim3(a.B), dim3(1024), 0, st, a, w);
 }
-// MSE kernel: local (k_mse_local, default: local expansions of the far Lorentzians)
-// | quad (k_mse_quad<NPT>: every term, one division per four) | n
-// (k_mse_partial_n<256, 2>, one division per term) | plain (k_mse_partial +
-// k_mse_final); MDG_MSE overrides
-static std::string mse_kind() {
-    const char* e = std::getenv("MDG_MSE");
-    return (e && *e) ? std::string(e) : std::string("local");
-}
-static int mse_quad_npt(const BatchArgs& a) {
-    if (const char* e = std::getenv("MDG_MSE_QNPT")) return std::atoi(e) == 2 ? 2 : 1;
-    return 2;
-}
-// k_mse_local compacts the retained Lorentzians itself (no k_retain launch)
-bool mse_fuses_retain() { return mse_kind() == "local"; }
-// k_mse_local points per thread: tiles of 512 (2, default) or 256 (1) points
-// (MDG_MSE_NPT). Measured in the queue (256 x 2): MSE 3.83-3.86 against 5.05-5.14 us
-// per spectrum, 15.27-15.39k against 15.03-15.07k spectra/s; the far-field pass is
-// shared by twice the points while the near list grows (tools/gpu_s9.sh)
-static int mse_local_npt() {
-    const char* e = std::getenv("MDG_MSE_NPT");
-    return (e && std::atoi(e) == 1) ? 1 : 2;
-}
+// The MSE kernel is k_mse_local<2> (local expansions of the far Lorentzians, tiles of
+// 512 points; it compacts the retained Lorentzians itself, so no k_retain launch).
+// Round 3 measured it against the 256-point tiles (k_mse_local<1>) and the earlier
+// k_mse_quad / k_mse_partial_n / k_mse_partial; those are not in the
+// library any more.
+constexpr int kLocNPT = 2;
 int mse_nparts(const BatchArgs& a) {
-    const std::string k = mse_kind();
-    if (k == "local") {
-        const int tp = kLocTP * mse_local_npt();
-        return std::max(1, std::min({kMseMaxParts, (a.N + tp - 1) / tp, std::max(1, 8192 / a.B)}));
-    }
-    if (k == "quad") {
-        // one workgroup per 64 * NPT points (its four waves split the Lorentzians)
-        const int pts = 64 * mse_quad_npt(a);
-        return std::max(1, std::min({kMseMaxParts, (a.N + pts - 1) / pts, std::max(1, 8192 / a.B)}));
-    }
-    const int base = std::max(1, std::min({1024, (a.N + 255) / 256, std::max(1, 4096 / a.B)}));
-    return k == "plain" ? base : std::max(1, (base + 1) / 2);  // n: two points per thread
+    const int tp = kLocTP * kLocNPT;
+    return std::max(1, std::min({kMseMaxParts, (a.N + tp - 1) / tp, std::max(1, 8192 / a.B)}));
 }
 const char* launch_mse(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st) {
-    if (mse_kind() == "local") {
-        // MDG_MSE_NEARCAP (tests): a smaller near-list capacity, to exercise the
-        // direct fallback of crowded tiles
-        int cap = kLocNear;
-        if (const char* e = std::getenv("MDG_MSE_NEARCAP")) cap = std::max(0, std::min(kLocNear, std::atoi(e)));
-        // nparts tile workgroups per spectrum plus its retain workgroup
-        if (mse_local_npt() == 2) {
-            launch_k(k_mse_local<2>, dim3((nparts + 1) * a.B), dim3(256), 0, st, a, w, nparts, cap);
-            return "k_mse_local<2>";
-        }
-        launch_k(k_mse_local<1>, dim3((nparts + 1) * a.B), dim3(256), 0, st, a, w, nparts, cap);
-        return "k_mse_local<1>";
-    }
-    if (mse_kind() == "quad") {
-        if (mse_quad_npt(a) == 2) {
-            launch_k(k_mse_quad<2>, dim3(nparts * a.B), dim3(256), 0, st, a, w, nparts);
-            return "k_mse_quad<2>";
-        }
-        launch_k(k_mse_quad<1>, dim3(nparts * a.B), dim3(256), 0, st, a, w, nparts);
-        return "k_mse_quad<1>";
-    }
-    if (mse_kind() == "n") {
-        launch_k((k_mse_partial_n<256, 2>), dim3(nparts * a.B), dim3(256), 0, st, a, w, nparts);
-        return "k_mse_partial_n<256, 2>";
-    }
-    launch_k(k_mse_partial<256>, dim3(nparts * a.B), dim3(256), 0, st, a, w, nparts);
-    return "k_mse_partial<256>+k_mse_final";
-}
-void launch_mse_final(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st) {
-    if (mse_kind() != "plain") return;  // k_mse_quad / k_mse_partial_n fold the partials
-    launch_k(k_mse_final, dim3(a.B), dim3(64), 0, st, a, w, nparts);
+    // MDG_MSE_NEARCAP (tests): a smaller near-list capacity, to exercise the kernel's
+    // own direct fallback for crowded tiles
+    int cap = kLocNear;
+    if (const char* e = std::getenv("MDG_MSE_NEARCAP")) cap = std::max(0, std::min(kLocNear, std::atoi(e)));
+    // nparts tile workgroups per spectrum plus its retain workgroup
+    launch_k(k_mse_local<kLocNPT>, dim3((nparts + 1) * a.B), dim3(256), 0, st, a, w, nparts, cap);
+    return "k_mse_local<2>";
 }
 void launch_mse_exact(const double* sup, const double* y, int64_t n, const Workspace& w,
                       double* scratch, double* out, hipStream_t st) {
     hipLaunchKernelGGL(k_sq_residuals, dim3(cdiv(n, 256)), dim3(256), 0, st, sup, y, n, scratch);
     hipLaunchKernelGGL(k_exact_fold, dim3(1), dim3(64), 0, st, scratch, w, out);
+}
+void launch_mse_exact_batch(const BatchArgs& a, const Workspace& w, double* res, int64_t res_row,
+                            hipStream_t st) {
+    // enough 256-thread workgroups for 4 points per thread at 131072 points, fewer per
+    // spectrum for larger batches (the grid-stride loop covers the rest)
+    const int parts = std::max(1, std::min<int>(cdiv(res_row, 1024), std::max(1, 16384 / a.B)));
+    launch_k(k_mse_exact_res, dim3(parts * a.B), dim3(256), 0, st, a, w, res, res_row);
+    launch_k(k_mse_exact_fold, dim3(a.B), dim3(64), 0, st, a, w, (const double*)res, res_row);
 }
 void launch_superposition_vec(const double* x, int64_t n, const double* params, int P,
                               double* out, int* flag, hipStream_t st) {

@@ -81,12 +81,7 @@ struct Workspace {
     int32_t* unsafe;          // B x 4: count of fit params outside it, per params version
                               // (k_fit_update path: version & 1; fused k_fit_sup_tf: version % 3)
     int32_t* unsafe_kept;     // B: same for the retained Lorentzians
-    int32_t* mse_done;        // B: k_mse_partial_n workgroups finished (the last one folds, resets)
-    // k_fit_sup_dyn (work-queue fit): control words (chunks per spectrum, per-XCD
-    // queue heads of two iteration slots, one progress counter per 64-point chunk)
-    // and the chunks' partial sums between the pieces of a fold
-    int32_t* fit_dyn;
-    double* fit_part;
+    int32_t* mse_done;        // B: k_mse_local workgroups finished (the last one folds, resets)
     int32_t* peak_cnt;        // B x ceil(W/256) u64: k_peaks slots {valid, bordered, kept} per mask chunk
     // k_smooth_chain (allocated on first use; null otherwise)
     double* chain_raw;        // P x B x chain_stride: raw running sums of every pass
@@ -133,31 +128,30 @@ inline void launch_k(void (*k)(BatchArgs, Workspace, P...), dim3 g, dim3 b, size
 }
 
 void launch_prep(const BatchArgs& a, const Workspace& w, hipStream_t st);
+#ifdef MDG_DIAG
 void launch_diag_nop(const BatchArgs& a, const Workspace& w, hipStream_t st);
+#endif
 bool smooth_uses_chain(const BatchArgs& a, const Workspace& w, int iters, int ws);
 const char* launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int ws, hipStream_t st,
                           int fused_prep = 0);
 void launch_flags(const BatchArgs& a, const Workspace& w, hipStream_t st);
 const char* launch_peaks(const BatchArgs& a, const Workspace& w, int detector_only, hipStream_t st);
-void launch_scores(const BatchArgs& a, const Workspace& w, hipStream_t st);
 const char* launch_select(const BatchArgs& a, const Workspace& w, int detector_only,
                           double threshold, hipStream_t st);
-bool mse_fuses_retain();
-bool peaks_score();
-void launch_fit_init(const BatchArgs& a, const Workspace& w, int gx, hipStream_t st);
 // returns true when the launched kernel also did the stencil update (no k_fit_update)
 bool fit_sup_fused(const BatchArgs& a);
 const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st);
-// the work-queue fit (k_fit_sup_dyn) needs its plan (chunks per spectrum, zeroed
-// queue heads and chunk counters) once per pipeline, before iteration 0
-bool fit_sup_dyn(const BatchArgs& a);
-void launch_fit_plan(const BatchArgs& a, const Workspace& w, hipStream_t st);
 void launch_fit_update(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st);
 void launch_retain(const BatchArgs& a, const Workspace& w, hipStream_t st);
-// MSE partial sums per spectrum for launch_mse / launch_mse_final (<= 1024)
+// MSE tiles per spectrum for launch_mse (<= kMseMaxParts)
 int mse_nparts(const BatchArgs& a);
+// k_mse_local: the MSE and the retained Lorentzians (out rows, counts, statuses)
 const char* launch_mse(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st);
-void launch_mse_final(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st);
+// exact-order MSE of every spectrum of the batch (MDG_OPTION_EXACT_MSE), after
+// launch_mse: squared residuals into res (B rows of res_row >= N doubles), then the
+// reference's left folds; overwrites out_mse
+void launch_mse_exact_batch(const BatchArgs& a, const Workspace& w, double* res, int64_t res_row,
+                            hipStream_t st);
 // windowed left fold of n <= kWinMax non-negative terms (test support)
 void launch_ordered_sum(const double* t, int n, double acc0, double* out, hipStream_t st);
 // fast-range division variants against IEEE '/' (test support): variant 0 div_rn,

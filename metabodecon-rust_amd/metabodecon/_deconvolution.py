@@ -357,6 +357,22 @@ class Deconvoluter:
     def settings(self) -> nat.Settings:
         return self._s.copy()
 
+    @property
+    def exact_mse(self) -> bool:
+        """Engine option (not a reference setting): compute each Deconvolution's MSE in
+        the reference's summation order (compute_mse, deconvoluter.rs:828-862), so
+        ``Deconvolution.mse`` and the serialized files' ``mse`` equal the reference's
+        bit for bit. Off (the default) the engine's MSE is within 1e-12 relative of it
+        and cheaper; Lorentzians are bit-identical either way (mdgpu.h
+        MDG_OPTION_EXACT_MSE)."""
+        return bool(self._s.options & nat.OPTION_EXACT_MSE)
+
+    @exact_mse.setter
+    def exact_mse(self, on: bool) -> None:
+        s = self._s.copy()
+        s.options = (s.options | nat.OPTION_EXACT_MSE) if on else (s.options & ~nat.OPTION_EXACT_MSE)
+        self._apply(s)
+
     def add_ignore_region(self, boundaries) -> None:
         a, b = float(boundaries[0]), float(boundaries[1])
         cur = self._ignore or []

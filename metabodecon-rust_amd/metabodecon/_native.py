@@ -30,10 +30,11 @@ REFERENCE_PANIC = 30
 ERR_HIP = 100
 ERR_NO_DEVICE = 101
 ERR_OUT_OF_MEMORY = 102
+OPTION_EXACT_MSE = 1  # mdg_settings.options (mdgpu.h MDG_OPTION_EXACT_MSE)
 
 N_STAGES = 12
 STAGE_NAMES = ["prep", "smooth", "detect", "select", "fit_init", "fit_superposition",
-               "fit_update", "retain", "mse_superposition", "mse_reduce", "superposition_vec",
+               "fit_update", "retain", "mse_superposition", "mse_exact", "superposition_vec",
                "synth"]
 
 # every symbol include/mdgpu.h declares (checked by tests/test_capi_exports.py)
@@ -52,7 +53,7 @@ EXPORTS = [
     "mdg_synth_lorentzians_hw", "mdg_synth_batch_device_hw",
     "mdg_queue_create", "mdg_queue_submit", "mdg_queue_flush", "mdg_queue_set_flush_us",
     "mdg_queue_synchronize",
-    "mdg_queue_lane", "mdg_queue_stats", "mdg_queue_destroy",
+    "mdg_queue_lane", "mdg_queue_stats", "mdg_queue_destroy", "mdg_queue_fail_next_launch",
 ]
 
 
@@ -73,7 +74,7 @@ class Settings(ctypes.Structure):
         ("scoring", ctypes.c_int32),
         ("fit_iterations", ctypes.c_uint32),
         ("fitter", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("options", ctypes.c_int32),  # MDG_OPTION_* bits
         ("threshold", ctypes.c_double),
     ]
 
@@ -270,6 +271,7 @@ def _declare(L):
     L.mdg_queue_lane.argtypes = [_vp, ctypes.c_int, ctypes.POINTER(_vp)]
     L.mdg_queue_stats.argtypes = [_vp, _u64p, _u64p, _szp]
     L.mdg_queue_destroy.argtypes = [_vp]
+    L.mdg_queue_fail_next_launch.argtypes = [_vp, ctypes.c_int]
     L.mdg_synth_batch_device_hw.argtypes = [_vp, _sz, _sz, ctypes.c_double, ctypes.c_double,
                                             ctypes.c_uint64, _sz, ctypes.c_double, ctypes.c_double,
                                             ctypes.c_double, ctypes.c_double, _vp, _vp]
@@ -523,6 +525,12 @@ class SpectrumQueue:
         st = lib().mdg_queue_synchronize(self.handle)
         if st:
             raise RuntimeError(f"mdg_queue_synchronize: {strerror(st)}")
+
+    def fail_next_launch(self, status: int) -> None:
+        """Test support: the next batch launch fails with `status` (sticky afterwards)."""
+        st = lib().mdg_queue_fail_next_launch(self.handle, int(status))
+        if st:
+            raise RuntimeError(strerror(st))
 
     def lane(self, k: int) -> Context:
         h = _vp()

@@ -278,7 +278,7 @@ class Spectrum:
         def one(p):
             try:
                 return read_bruker_arrays(p, experiment, processing)
-            except MetadataError as e:
+            except Exception as e:  # noqa: BLE001 -- raised below, in directory order
                 return e
         if len(paths) > 1:
             from concurrent.futures import ThreadPoolExecutor
@@ -286,9 +286,17 @@ class Spectrum:
                 arrays = list(pool.map(one, paths))
         else:
             arrays = [one(p) for p in paths]
-        for a in arrays:
-            if isinstance(a, MetadataError):
-                raise getattr(exc, a.kind, exc.SpectrumError)(str(a)) from None
+        # The reference reads and validates one spectrum at a time (read_spectrum, then
+        # Spectrum::new, then the next directory: bruker.rs:360-373), so the first
+        # failure in directory order wins, whether a read error or a validation error:
+        # the spectra before the first failed read are validated first.
+        bad = next((i for i, a in enumerate(arrays) if isinstance(a, BaseException)), None)
+        if bad is not None:
+            _set_of_rows(arrays[:bad], signal_boundaries)  # raises an earlier validation error
+            e = arrays[bad]
+            if isinstance(e, MetadataError):
+                raise getattr(exc, e.kind, exc.SpectrumError)(str(e)) from None
+            raise e
         return _set_of_rows(arrays, signal_boundaries)
 
 

@@ -48,7 +48,7 @@ class Settings(ctypes.Structure):
         ("scoring", ctypes.c_int32),
         ("fit_iterations", ctypes.c_uint32),
         ("fitter", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("options", ctypes.c_int32),  # mdgpu.h layout (the oracle always sums in the reference order)
         ("threshold", ctypes.c_double),
     ]
 

@@ -43,7 +43,7 @@ typedef struct mdo_settings {
     int32_t scoring;             /* 0 minimum sum */
     uint32_t fit_iterations;
     int32_t fitter;              /* 0 analytical */
-    int32_t reserved;
+    int32_t options;  /* mdgpu.h layout; the oracle always sums in the reference order */
     double threshold;
 } mdo_settings;
 

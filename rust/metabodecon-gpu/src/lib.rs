@@ -26,6 +26,7 @@
 use std::ffi::CStr;
 use std::os::raw::{c_int, c_void};
 use std::ptr::{self, NonNull};
+use std::sync::atomic::{AtomicI32, Ordering};
 
 use metabodecon::deconvolution::error::{Error as DeconvolutionError, Kind};
 use metabodecon::deconvolution::{
@@ -52,7 +53,7 @@ pub mod ffi {
         pub scoring: i32,
         pub fit_iterations: u32,
         pub fitter: i32,
-        pub reserved: i32,
+        pub options: i32,
         pub threshold: f64,
     }
 
@@ -95,6 +96,7 @@ pub mod ffi {
     pub const MDG_SELECT_NOISE_SCORE: i32 = 1;
     pub const MDG_SCORE_MINIMUM_SUM: i32 = 0;
     pub const MDG_FIT_ANALYTICAL: i32 = 0;
+    pub const MDG_OPTION_EXACT_MSE: i32 = 1;
 
     #[link(name = "mdgpu")]
     extern "C" {
@@ -270,6 +272,9 @@ pub mod ffi {
 /// like the reference's `Send + Sync` Deconvoluter (deconvoluter.rs:913-917).
 pub struct GpuContext {
     ctx: NonNull<ffi::MdgCtx>,
+    /// `mdg_settings.options` for the calls made through this context
+    /// (`MDG_OPTION_EXACT_MSE`, set by `set_exact_mse`).
+    options: AtomicI32,
 }
 
 unsafe impl Send for GpuContext {}
@@ -281,7 +286,7 @@ impl GpuContext {
         let mut raw: *mut ffi::MdgCtx = ptr::null_mut();
         let st = unsafe { ffi::mdg_ctx_create(device as c_int, &mut raw) };
         match NonNull::new(raw) {
-            Some(ctx) if st == ffi::MDG_OK => Ok(Self { ctx }),
+            Some(ctx) if st == ffi::MDG_OK => Ok(Self { ctx, options: AtomicI32::new(0) }),
             _ => Err(engine_error(st)),
         }
     }
@@ -303,6 +308,23 @@ impl GpuContext {
 
     pub fn synchronize(&self) -> Result<()> {
         check(unsafe { ffi::mdg_ctx_synchronize(self.raw()) })
+    }
+
+    /// Engine option (not a reference setting): compute each `Deconvolution`'s MSE in
+    /// the reference's summation order (`compute_mse`, deconvoluter.rs:828-862), bit
+    /// for bit; off (the default) it is within 1e-12 relative and cheaper. The
+    /// Lorentzians are bit-identical either way (mdgpu.h `MDG_OPTION_EXACT_MSE`).
+    pub fn set_exact_mse(&self, on: bool) {
+        let v = if on { ffi::MDG_OPTION_EXACT_MSE } else { 0 };
+        self.options.store(v, Ordering::Relaxed);
+    }
+
+    pub fn exact_mse(&self) -> bool {
+        self.options.load(Ordering::Relaxed) & ffi::MDG_OPTION_EXACT_MSE != 0
+    }
+
+    fn options(&self) -> i32 {
+        self.options.load(Ordering::Relaxed)
     }
 
     pub fn raw(&self) -> *mut ffi::MdgCtx {
@@ -338,7 +360,20 @@ impl GpuSpectrumQueue {
         max_batch: usize,
         lanes: i32,
     ) -> Result<Self> {
-        let s = Settings::of(deconvoluter).to_ffi()?;
+        Self::with_exact_mse(deconvoluter, device, n, max_batch, lanes, false)
+    }
+
+    /// `new`, with the exact-order MSE option (`GpuContext::set_exact_mse`).
+    pub fn with_exact_mse(
+        deconvoluter: &Deconvoluter,
+        device: i32,
+        n: usize,
+        max_batch: usize,
+        lanes: i32,
+        exact_mse: bool,
+    ) -> Result<Self> {
+        let options = if exact_mse { ffi::MDG_OPTION_EXACT_MSE } else { 0 };
+        let s = Settings::of(deconvoluter).to_ffi(options)?;
         let ig = ignore_pairs(deconvoluter);
         let mut raw: *mut ffi::MdgQueue = ptr::null_mut();
         let st = unsafe {
@@ -482,9 +517,10 @@ impl Settings {
     /// Enum settings -> `mdg_settings` (smoother.rs:27-65, selector.rs:21-66,
     /// fitter.rs:26-63). Variants the engine does not know are rejected as the
     /// matching invalid-settings error.
-    fn to_ffi(&self) -> Result<ffi::MdgSettings> {
+    fn to_ffi(&self, options: i32) -> Result<ffi::MdgSettings> {
         let mut s = ffi::MdgSettings::default();
         unsafe { ffi::mdg_settings_default(&mut s) };
+        s.options = options;
         let too_big = |v: usize| u32::try_from(v).is_err();
         match self.smoothing {
             SmoothingSettings::Identity => s.smoother = ffi::MDG_SMOOTH_IDENTITY,
@@ -566,7 +602,7 @@ pub trait GpuDeconvoluter {
 impl GpuDeconvoluter for Deconvoluter {
     fn gpu_deconvolute_spectrum(&self, ctx: &GpuContext, spectrum: &Spectrum) -> Result<Deconvolution> {
         let settings = Settings::of(self);
-        let s = settings.to_ffi()?;
+        let s = settings.to_ffi(ctx.options())?;
         let ig = ignore_pairs(self);
         let (sb0, sb1) = spectrum.signal_boundaries(); // ordered as stored (spectrum.rs:854-863)
         let (x, y) = (spectrum.chemical_shifts(), spectrum.intensities());
@@ -605,7 +641,7 @@ impl GpuDeconvoluter for Deconvoluter {
         spectra: &[S],
     ) -> Result<Vec<Deconvolution>> {
         let settings = Settings::of(self);
-        let s = settings.to_ffi()?;
+        let s = settings.to_ffi(ctx.options())?;
         let ig = ignore_pairs(self);
         let mut results: Vec<Option<(c_int, Vec<ffi::MdgLorentzian>, f64)>> =
             (0..spectra.len()).map(|_| None).collect();

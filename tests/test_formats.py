@@ -556,3 +556,31 @@ def test_all_reference_jcampdx_files(affn):
                                                 ("v5", "ntuples_difdup.dx")} else 0), (v, p)
     blood = md.Spectrum.read_jcampdx_set(os.path.join(REF_JDX, "blood"), (-2.2, 11.8))
     assert len(blood) == 16 and all(len(s) == 131072 for s in blood)
+
+
+def test_bruker_set_first_failure_in_directory_order(tmp_path):
+    """read_bruker_set reads the set with threads but raises the first
+    failure in directory order, like the reference's sequential read-and-validate
+    (bruker.rs:360-373). a_first: readable, but its axis (OFFSET 3.0) does not hold
+    the signal boundaries -- a validation error; b_second: its 1r file is missing -- a
+    read error (OSError). The validation error of the earlier spectrum wins; without
+    a_first the read error is raised."""
+    import shutil
+    import metabodecon as md
+    from metabodecon import exceptions as mexc
+    src = os.path.join(GOLDEN, "bruker", "blood")
+    a = tmp_path / "a_first"
+    b = tmp_path / "b_second"
+    shutil.copytree(os.path.join(src, "blood_01"), a)
+    shutil.copytree(os.path.join(src, "blood_02"), b)
+    procs = a / "10" / "pdata" / "10" / "procs"
+    procs.write_text(procs.read_text().replace("##$OFFSET= 14.81146", "##$OFFSET= 3.0"))
+    os.remove(b / "10" / "pdata" / "10" / "1r")
+    with pytest.raises(mexc.SpectrumError) as ei:
+        md.Spectrum.read_bruker_set(str(tmp_path), 10, 10, (-2.2, 11.8))
+    assert not isinstance(ei.value, OSError)
+    with pytest.raises(mexc.SpectrumError):  # the same error reading a_first alone
+        md.Spectrum.read_bruker(str(a), 10, 10, (-2.2, 11.8))
+    shutil.rmtree(a)
+    with pytest.raises(OSError):
+        md.Spectrum.read_bruker_set(str(tmp_path), 10, 10, (-2.2, 11.8))

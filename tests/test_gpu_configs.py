@@ -135,16 +135,14 @@ def test_optimize_settings_blood_01_full_size():
     assert got == mse
 
 
-@pytest.mark.parametrize("npt", ["1", "2"])
 @pytest.mark.parametrize("hw_scale,sigma", [(0.5, 1.0), (0.3, 1.0e-3), (0.5, 0.0)])
-def test_mse_narrow_peaks_close_fit(hw_scale, sigma, npt, monkeypatch):
+def test_mse_narrow_peaks_close_fit(hw_scale, sigma):
     """k_mse_local sums the far Lorentzians of a tile as a 20-term series of
     Im[a/(x - z)], whose terms exceed the Lorentzian by ~distance/half-width, so its
     roundoff is amplified most by narrow peaks; and a close fit (near-zero noise)
     makes the residual, hence the MSE, small against the superposition. Narrow
     half-widths (x0.3, x0.5) with sigma 1, 1e-3 and 0: every MSE within MSE_RTOL of
     the oracle's left fold (and the parameters bit-identical, as everywhere)."""
-    monkeypatch.setenv("MDG_MSE_NPT", npt)  # 256- and 512-point tiles
     cap = 4096
     res = _device_batch(4, 131072, 2048, hw_scale, cap, seed0=40, sigma=sigma)
     assert res["kernels"].get("mse_superposition", "").startswith("k_mse_local")

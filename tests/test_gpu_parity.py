@@ -158,13 +158,13 @@ def test_single_spectrum_entry(ctx):
         assert rc == nat.CAPACITY and cnt.value == g["params"].shape[0]
 
 
-@pytest.mark.parametrize("path", ["fused", "MDG_PEAKS_NOSCORE", "MDG_PEAKS_2PASS"])
+@pytest.mark.parametrize("path", ["chain", "pipe", "generic"])
 def test_detected_peaks_match_oracle(ctx, path, monkeypatch):
     """Detected triples equal the oracle's; the selection (which reads the noise
-    scores) equals the golden on every detection path: scores computed by k_peaks
-    itself (default), by a separate k_scores, and the two-kernel peak list."""
-    if path != "fused":
-        monkeypatch.setenv(path, "1")
+    scores k_peaks computes for the peaks it writes) equals the golden, behind every
+    smoother kernel (the chain smoother runs the set-up itself, the others after
+    k_prep)."""
+    monkeypatch.setenv("MDG_SMOOTH", path)
     x, y, sb, st, ign = load_case("blood_01")
     gpu_batch(ctx, x, y[None, :], [sb], st)
     det = ctx.last_peaks(0, "detected").astype(np.int64)
@@ -261,7 +261,7 @@ def test_fused_prep_after_failures_and_other_smoothers(monkeypatch):
     """The chain smoother runs k_prep's work itself and never reads the status the
     previous run left; k_flags returns its progress counters to zero. On one
     context: a failing spectrum (NoPeaksDetected), then a good one, the same on
-    the wave smoother, with k_prep launched separately, and the chain again --
+    the lane-pipelined smoother, with k_prep launched separately, and the chain again --
     every result equal to the oracle."""
     c = nat.Context(0)
     st = oracle.default_settings()
@@ -270,7 +270,7 @@ def test_fused_prep_after_failures_and_other_smoothers(monkeypatch):
     flat = np.full(n, 7.0)
     x, y, sb, cst, _ = load_case("blood_07")
     o = oracle.deconvolute(x, y, sb, cst)
-    for smooth, prep in [("chain", None), ("waves", None), ("chain", "separate"), ("chain", None)]:
+    for smooth, prep in [("chain", None), ("pipe", None), ("chain", "separate"), ("chain", None)]:
         monkeypatch.setenv("MDG_SMOOTH", smooth)
         if prep:
             monkeypatch.setenv("MDG_PREP", prep)
@@ -348,11 +348,11 @@ def test_small_and_odd_shapes(ctx):
             assert abs(mse[0] - o.mse) <= MSE_RTOL * abs(o.mse)
 
 
-@pytest.mark.parametrize("path", ["chain", "waves", "pipe"])
+@pytest.mark.parametrize("path", ["chain", "pipe", "generic"])
 @pytest.mark.parametrize("it,ws", [(1, 2), (2, 4), (3, 3), (5, 7), (8, 5), (10, 3), (3, 31),
                                    (4, 9), (2, 11)])
 def test_smoother_settings_sweep(ctx, it, ws, path, monkeypatch):
-    """Both exact smoother kernels (wave-per-pass and lane-pipelined, chosen by
+    """Every smoother kernel (chain, lane-pipelined, one lane per spectrum, forced by
     MDG_SMOOTH) against the oracle; (3, 31) and iterations > 8 exercise fallbacks."""
     monkeypatch.setenv("MDG_SMOOTH", path)
     x, y, sb, _, _ = load_case("blood_05")
@@ -427,7 +427,7 @@ def _smooth_rows(ctx, ys, it, ws):
     return [ctx.last_smoothed(s, ys.shape[1]) for s in range(ys.shape[0])]
 
 
-@pytest.mark.parametrize("path", ["chain", "pipe", "waves", "generic"])
+@pytest.mark.parametrize("path", ["chain", "pipe", "generic"])
 def test_smoothed_rows_bit_exact(ctx, path, monkeypatch):
     """Smoothed intensities of every kernel equal the oracle's moving average bit for
     bit (moving_average.rs:53-83), on real spectra and a synthetic 128k one."""
@@ -464,11 +464,14 @@ def test_chain_smoother_repeated_launches(ctx, monkeypatch):
             assert np.array_equal(row, oracle.moving_average(ys[s], 3, 3)), (rep, s)
 
 
-@pytest.mark.parametrize("path", ["dpp", "split", "plain", "fu", "dyn", "tf", "tw", "tw3", "tw4", "tw7", "tw9", "tw14"])
+FIT_KERNELS = ["tf", "tw7", "plain"]  # the library's fit kernels (fit_choice, mdg_kernels.hip)
+
+
+@pytest.mark.parametrize("path", FIT_KERNELS)
 def test_fit_superposition_kernels(ctx, path, monkeypatch):
-    """Every fit-superposition kernel (row-broadcast DPP fold, LDS split fold, one
-    thread per point, term fold; chosen by MDG_FITSUP) gives the oracle's Lorentzians bit for
-    bit, including peak counts that are not multiples of the 16-peak groups."""
+    """Every fit-superposition kernel the library ships (24- and 63-point term folds,
+    one thread per point; forced by MDG_FITSUP) gives the oracle's Lorentzians bit for
+    bit, including peak counts that are not multiples of the tiles and chunks."""
     monkeypatch.setenv("MDG_FITSUP", path)
     names = ["sim_03", "blood_03", "synth_128k_2k_s1"]
     for name in names:
@@ -480,8 +483,7 @@ def test_fit_superposition_kernels(ctx, path, monkeypatch):
         assert abs(mse[0] - o.mse) <= MSE_RTOL * abs(o.mse), name
 
 
-
-@pytest.mark.parametrize("path", ["dpp", "split", "plain", "fu", "dyn", "tf", "tw", "tw3", "tw4", "tw7", "tw9", "tw14"])
+@pytest.mark.parametrize("path", FIT_KERNELS)
 def test_fit_superposition_kernels_batch(ctx, path, monkeypatch):
     """The fit kernels on a batch whose spectra have different peak counts (tail
     tiles, grid-stride loops, per-spectrum range flags) against the oracle."""
@@ -499,18 +501,12 @@ def test_fit_superposition_kernels_batch(ctx, path, monkeypatch):
         assert abs(mse[s] - o.mse) <= MSE_RTOL * abs(o.mse), s
 
 
-@pytest.mark.parametrize("kernel,near_cap", [("local", None), ("local", "8"), ("local", "0"),
-                                             ("local1", None), ("local1", "8"),
-                                             ("quad", None), ("n", None), ("plain", None)])
-def test_mse_cases(ctx, kernel, near_cap, monkeypatch):
-    """The MSE against the oracle: ignore regions (two in one spectrum), a short
-    signal region (sim) and a batch whose spectra differ in peak count -- on every
-    MSE kernel; for k_mse_local also with a tiny near-list capacity (crowded tiles
-    take the direct sum) and none at all (every tile direct)."""
-    if kernel == "local1":  # k_mse_local with 256-point tiles (one point per thread)
-        monkeypatch.setenv("MDG_MSE_NPT", "1")
-        kernel = "local"
-    monkeypatch.setenv("MDG_MSE", kernel)
+@pytest.mark.parametrize("near_cap", [None, "8", "0"])
+def test_mse_cases(ctx, near_cap, monkeypatch):
+    """The MSE (k_mse_local) against the oracle: ignore regions (two in one spectrum),
+    a short signal region (sim) and a batch whose spectra differ in peak count; also
+    with a tiny near-list capacity (crowded tiles take the kernel's direct sum) and
+    none at all (every tile direct)."""
     if near_cap is not None:
         monkeypatch.setenv("MDG_MSE_NEARCAP", near_cap)
     for name in ["blood_01_water", "blood_02_two_regions_increasing", "sim_05", "synth_128k_2k_s0"]:
@@ -652,7 +648,7 @@ def test_device_graph_replay(ctx, monkeypatch):
 
 def test_graph_key_follows_kernel_overrides(monkeypatch):
     """A cached pipeline graph is keyed by the kernel-choice overrides too: the
-    same device buffers with MDG_MSE / MDG_FITSUP switched between calls launch
+    same device buffers with MDG_SMOOTH / MDG_FITSUP switched between calls launch
     the newly chosen kernels (reported by the engine), each call equal to the
     oracle."""
     torch = pytest.importorskip("torch")
@@ -671,8 +667,8 @@ def test_graph_key_follows_kernel_overrides(monkeypatch):
     s = nat.default_settings()
     o = oracle.deconvolute(cx, cy, csb, cst)
     seen = []
-    for mse_k, fit_k in [("local", "tw7"), ("quad", "tw7"), ("local", "dpp"), ("local", "tw7")]:
-        monkeypatch.setenv("MDG_MSE", mse_k)
+    for sm_k, fit_k in [("chain", "tw7"), ("pipe", "tw7"), ("chain", "plain"), ("chain", "tw7")]:
+        monkeypatch.setenv("MDG_SMOOTH", sm_k)
         monkeypatch.setenv("MDG_FITSUP", fit_k)
         rc = nat.lib().mdg_deconvolute_batch_device(
             c.handle, 1, n, x.data_ptr(), 0, y.data_ptr(), n, sb.data_ptr(), ctypes.byref(s), None,
@@ -680,13 +676,13 @@ def test_graph_key_follows_kernel_overrides(monkeypatch):
         assert rc == 0
         c.synchronize()
         k = c.stage_kernels()
-        seen.append((k["mse_superposition"], k["fit_superposition"]))
+        seen.append((k["smooth"], k["fit_superposition"]))
         assert int(status[0]) == 0
         assert np.array_equal(out[0, : int(cnt[0])].cpu().numpy(), o.params)
         assert abs(float(mse[0]) - o.mse) <= MSE_RTOL * abs(o.mse)
     c.close()
-    assert seen[0][0].startswith("k_mse_local") and seen[1][0].startswith("k_mse_quad")
-    assert seen[2][1] == "k_fit_sup_dpp" and seen[3] == seen[0]
+    assert seen[0][0].startswith("k_smooth_chain") and seen[1][0].startswith("k_smooth_pipe")
+    assert seen[2][1] == "k_fit_sup" and seen[3] == seen[0]
 
 
 @pytest.mark.parametrize("name", ["sim_01", "sim_07"])

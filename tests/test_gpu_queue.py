@@ -5,7 +5,6 @@ Each submission is one spectrum with its own device arrays; the queue batches th
 into pipelines. Every result must equal the oracle (and the goldens): parameters and
 counts bit-identical, statuses equal, MSE within 1e-12 relative.
 """
-import argparse
 import ctypes
 import os
 
@@ -214,19 +213,71 @@ def test_queue_ignore_regions_and_settings():
 
 
 def test_bench_headline_configuration_bit_exact():
-    """the exact mode bench.py times -- headline_queue with its
-    default queue (128-spectrum batches on 2 lanes), device-generated distinct
-    configs[1] spectra submitted one at a time -- with EVERY timed result row checked
-    against the oracle (bench's own checker, verify = every submission)."""
+    """The exact configuration bench.py times: headline_queue with the queue shape of
+    bench.parse([]) -- the defaults the driver's run uses (256-spectrum batches on 2
+    lanes, a step of 512 single-spectrum submissions) -- on device-generated distinct
+    configs[1] spectra, with EVERY timed result row (one step: 512) checked against
+    the oracle (bench's own checker, verify = every submission of every batch)."""
     torch = pytest.importorskip("torch")
     import bench
-    args = argparse.Namespace(
-        n=131072, peaks=2048, cap=4096, steps=2, warmup=1, max_batch=128, lanes=2,
-        step_spectra=0, verify=128, fit_iterations=0, hw_scale=1.0, force_dist=False,
-        no_profile=True, cpu_threads=0)
+    args = bench.parse([])
+    assert (args.max_batch, args.lanes, args.step_spectra) == (256, 2, 0)
+    args.steps, args.warmup, args.verify, args.no_profile = 1, 1, args.max_batch, True
     import torch.distributed as dist
     dev = torch.device("cuda", 0)
     h = bench.headline_queue(args, nat, torch, dist, dev, 0, 1)
     v = h["verified"]
-    assert v["checked"] == 2 * 256 and v["ok"] == v["checked"], v
-    assert h["batches"] == 4
+    step = args.max_batch * args.lanes
+    assert h["step_spectra"] == step and h["batches"] == args.lanes
+    assert v["checked"] == step and v["ok"] == v["checked"], v
+
+
+def test_queue_failed_launch_is_sticky_and_never_hangs():
+    """a failed batch launch with a flush deadline running. The watcher
+    thread's launch fails (injected: mdg_queue_fail_next_launch, as an allocation
+    failure would), the open batch stays unlaunched, and the watcher must wait instead
+    of spinning with the queue's lock held: submit, flush, synchronize and stats
+    return (the first three with the sticky error) and close() completes."""
+    import threading
+    import time
+    torch = pytest.importorskip("torch")
+    x, y, sb, _, _ = load_case("blood_04")
+    n = y.size
+    xd = torch.from_numpy(x).cuda()
+    yd = torch.from_numpy(y).cuda()
+    cap = n // 2 + 2
+    out, cnt, mse, st = _outputs(torch, 2, cap)
+    torch.cuda.synchronize()
+    q = nat.SpectrumQueue(0, n, 8, 2, nat.default_settings())
+    done = threading.Event()
+    errors = {}
+
+    def body():
+        q.fail_next_launch(nat.ERR_OUT_OF_MEMORY)
+        q.set_flush_us(1000)
+        q.submit(xd.data_ptr(), yd.data_ptr(), sb, out[0].data_ptr(), cap, cnt[0:].data_ptr(),
+                 mse[0:].data_ptr(), st[0:].data_ptr())
+        t0 = time.time()
+        while time.time() - t0 < 5:  # the watcher's launch attempt (1 ms deadline)
+            time.sleep(0.01)
+            try:
+                q.submit(xd.data_ptr(), yd.data_ptr(), sb, out[1].data_ptr(), cap,
+                         cnt[1:].data_ptr(), mse[1:].data_ptr(), st[1:].data_ptr())
+            except RuntimeError as e:
+                errors["submit"] = str(e)
+                break
+        for name, fn in (("flush", q.flush), ("synchronize", q.synchronize)):
+            try:
+                fn()
+            except RuntimeError as e:
+                errors[name] = str(e)
+        errors["stats"] = q.stats()
+        q.close()
+        done.set()
+
+    th = threading.Thread(target=body, daemon=True)
+    th.start()
+    assert done.wait(30), "queue calls blocked after a failed launch"
+    msg = nat.strerror(nat.ERR_OUT_OF_MEMORY)
+    assert msg in errors.get("submit", "") and msg in errors["flush"] and msg in errors["synchronize"]
+    assert errors["stats"]["batches"] == 0 and errors["stats"]["open"] >= 1

@@ -33,6 +33,31 @@ def test_validate_matches_oracle(kw):
     assert nat.validate(s) == oracle.lib().mdo_validate_settings(o)
 
 
+def test_engine_options_validation():
+    """mdg_settings.options: MDG_OPTION_EXACT_MSE is the one defined bit (0 and 1 are
+    valid), every other bit is MDG_INVALID_ARGUMENT; Deconvoluter.exact_mse sets and
+    clears it without touching the reference settings."""
+    s = nat.default_settings()
+    assert s.options == 0 and nat.validate(s) == 0
+    s.options = nat.OPTION_EXACT_MSE
+    assert nat.validate(s) == 0
+    for bad in (2, 3, 1 << 30, -1):
+        s.options = bad
+        assert nat.validate(s) == nat.INVALID_ARGUMENT, bad
+    d = Deconvoluter()
+    before = d.settings
+    d.exact_mse = True
+    assert d.exact_mse and d.settings.options == nat.OPTION_EXACT_MSE
+    d.set_noise_score_selector(6.0)
+    assert d.exact_mse  # other setters keep the option
+    d.exact_mse = False
+    after = d.settings
+    assert after.options == 0 and after.threshold == 6.0
+    for f, _ in nat.Settings._fields_:
+        if f != "threshold":
+            assert getattr(after, f) == getattr(before, f), f
+
+
 def test_deconvoluter_setters_raise_reference_exceptions():
     d = Deconvoluter()
     with pytest.raises(exceptions.InvalidSmoothingSettings):

@@ -177,6 +177,6 @@ def test_mutated_signature_fails_to_compile(shim, tmp_path, mutation):
 def test_mutated_struct_layout_fails_to_compile(shim, tmp_path):
     externs, structs, consts = shim
     bad = dict(structs)
-    bad["MdgSettings"] = [(f, "f64" if f == "reserved" else t) for f, t in structs["MdgSettings"]]
+    bad["MdgSettings"] = [(f, "f64" if f == "options" else t) for f, t in structs["MdgSettings"]]
     res, _ = _compile(tmp_path, c_program(externs, bad, consts), link=False)
     assert res.returncode != 0

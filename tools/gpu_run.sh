@@ -13,6 +13,8 @@
 #   forcedist    bench.py under torch.distributed.run at world 1 (RCCL gather, configs_dist)
 #   prof         the round's profile set (tools/prof_all.sh)
 #   c4           configs[4] by lanes and hardware queues (bench.py --c4-only)
+#   fitdiag      small-batch fit: PMC passes of tools/blood_trace.py 16 and the stamped
+#                tools/ubench/fit_diag (tools/pmc_fit.sh; build fit_diag first)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/run
 log=gpurun_out/run/session.log
@@ -44,6 +46,11 @@ for step in "$@"; do
         [ $l -ge $q ] || cfgs+=("q${q}_l$l GPU_MAX_HW_QUEUES=$q MDGPU_LANES=$l --c4-only")
       done; done
       run c4 1200 bash tools/ab.sh c4 "${cfgs[@]}" ;;
+    fitdiag)
+      run pmc_fit 600 bash tools/pmc_fit.sh 16 16 992 tw7,tf,plain
+      for g in 16 32 48 64; do run "fit_diag_g$g" 60 env MDG_TW_G=$g tools/ubench/fit_diag 16 992 tw7; done
+      run fit_diag_b8 60 tools/ubench/fit_diag 8 992 tw7,tf
+      run fit_diag_b1 60 tools/ubench/fit_diag 1 992 tw7,tf ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -1,7 +1,11 @@
 // Phase breakdown and timing of the fit-superposition kernels on synthetic peak
 // tables (P peaks, 3P reduced points per spectrum): builds the library kernel source
-// with -DMDG_DIAG. usage: fit_diag [B] [P]
+// with -DMDG_DIAG. usage: fit_diag [B] [P] [kinds, comma-separated; MDG_FITSUP names,
+// '/noeval' suffix = tf without evaluation]
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -DMDG_DIAG \
+//       tools/ubench/fit_diag.hip -o tools/ubench/fit_diag
 #include "../../metabodecon-rust_amd/csrc/mdg_kernels.hip"
+#include <algorithm>
 #include <cstdio>
 #include <vector>
 using namespace mdg;
@@ -42,10 +46,20 @@ int main(int argc, char** argv) {
     Workspace w{}; w.capD = capD; w.status = status; w.sel_count = sel; w.params = d_par;
     w.rx = d_rx; w.ry = d_ry; w.ratio = d_ratio; w.x_ok = xok; w.unsafe = unsafe;
     w.stencil = d_st; w.fit_iters = 10;
-    const char* kinds[] = {"dpp", "plain", "tf", "tf/noeval"};
+    std::vector<std::string> kinds;
+    {
+        std::string all = argc > 3 ? argv[3] : "dpp,plain,tf,tf/noeval";
+        size_t p0 = 0;
+        while (p0 <= all.size()) {
+            const size_t p1 = all.find(',', p0);
+            kinds.push_back(all.substr(p0, p1 == std::string::npos ? std::string::npos : p1 - p0));
+            if (p1 == std::string::npos) break;
+            p0 = p1 + 1;
+        }
+    }
     std::vector<double> ref;
-    for (const char* k : kinds) {
-        const std::string ks(k);
+    for (const std::string& ks : kinds) {
+        const char* k = ks.c_str();
         const int mode = ks.find("/nostore") != std::string::npos ? 1 : ks.find("/noeval") != std::string::npos ? 2 : 0;
         (void)hipMemcpyToSymbol(HIP_SYMBOL(g_tf_mode), &mode, sizeof(mode));
         setenv("MDG_FITSUP", ks.substr(0, ks.find('/')).c_str(), 1);
@@ -68,7 +82,45 @@ int main(int argc, char** argv) {
         const double evals = 3.0 * P * P * B;
         printf("%-6s B=%d P=%d  %.2f us/launch  %.3f T evals/s  same_as_dpp=%d\n", k, B, P, best * 1e3,
                evals / (best * 1e-3) / 1e12, (int)same);
-        if (k[0] == 't') {
+        if (ks.rfind("tw", 0) == 0) {
+            // tw: waves 0..EW-1 evaluators, wave EW the fold wave; grid (g, B); a block
+            // with blockIdx.x >= tiles has no work. Slots: see fit_tw_body.
+            std::vector<long long> d(nd);
+            (void)hipMemcpy(d.data(), diag, nd * 8, hipMemcpyDeviceToHost);
+            const int EW = ks == "tw7" ? 7 : ks == "tw3" ? 3 : ks == "tw9" ? 9 : ks == "tw4" ? 4 : ks == "tw14" ? 14 : 6;
+            const int QQ = ks == "tw4" ? 60 : 63;
+            const char* tg = std::getenv("MDG_TW_G");
+            const int g = tg ? std::max(1, std::atoi(tg)) : (3 * 2048 + 62) / 63;
+            const int tiles = (3 * P + QQ - 1) / QQ, active = std::min(g, tiles);
+            double ev[8] = {0}, fo[8] = {0};
+            long long t0 = -1, t1 = 0;
+            std::vector<long long> ends, starts;
+            for (int s = 0; s < B; ++s)
+                for (int b = 0; b < active; ++b) {
+                    const long long* blk = &d[((size_t)(s * g + b) * 16) * 8];
+                    long long life = 0;
+                    for (int wv = 0; wv <= EW; ++wv) {
+                        const long long* r = blk + wv * 8;
+                        long long l = 0;
+                        for (int i = 0; i < 7; ++i) { (wv < EW ? ev : fo)[i] += r[i]; l += r[i]; }
+                        life = std::max(life, l);
+                    }
+                    const long long st = blk[7];
+                    starts.push_back(st);
+                    ends.push_back(st + life);
+                    t0 = t0 < 0 ? st : std::min(t0, st);
+                    t1 = std::max(t1, st + life);
+                }
+            const double nb = (double)B * active;
+            printf("   %d blocks (%d per spectrum, %d tiles), span %.0f cycles\n", (int)nb, active, tiles, (double)(t1 - t0));
+            printf("   evaluator wave avg: prologue %.0f  eval %.0f  barrier %.0f\n", ev[5] / nb / EW, ev[0] / nb / EW, ev[1] / nb / EW);
+            printf("   fold wave avg: first-wait %.0f  fold %.0f  barrier %.0f  update %.0f\n", fo[6] / nb, fo[2] / nb, fo[3] / nb, fo[4] / nb);
+            std::sort(starts.begin(), starts.end());
+            std::sort(ends.begin(), ends.end());
+            auto q = [&](std::vector<long long>& v, double f) { return (double)(v[(size_t)(f * (v.size() - 1))] - t0); };
+            printf("   block start q0/25/50/75/100: %.0f %.0f %.0f %.0f %.0f\n", q(starts, 0), q(starts, .25), q(starts, .5), q(starts, .75), q(starts, 1));
+            printf("   block end   q0/25/50/75/100: %.0f %.0f %.0f %.0f %.0f\n", q(ends, 0), q(ends, .25), q(ends, .5), q(ends, .75), q(ends, 1));
+        } else if (k[0] == 't') {
             std::vector<long long> d(nd);
             (void)hipMemcpy(d.data(), diag, nd * 8, hipMemcpyDeviceToHost);
             const char* nm[5] = {"eval", "ev-barrier", "fold", "fold-barrier", "fold-other"};
