@@ -1116,8 +1116,12 @@ __global__ __launch_bounds__(64 * (2 + kChainScalers)) void k_smooth_chain(Batch
                 __builtin_amdgcn_s_sleep(1);
             }
             if (!ok) break;
-            if (lane == 0)
-                __hip_atomic_fetch_max(my_flag, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // the publication is issued by the whole wave with a wave-uniform value (no
+            // lane-guarded branch around it; the compiler's atomic optimizer sends one
+            // atomic): the round-3 lost-counter bug was a lane-guarded store in a
+            // region with spilled SGPRs (publication audit)
+            __hip_atomic_fetch_max(my_flag, __builtin_amdgcn_readfirstlane(hi), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
             CTL_ST(pub, b + 1);
             if (sw == 0) {
                 DIAGC_ADD(18, 1);
@@ -1130,11 +1134,9 @@ __global__ __launch_bounds__(64 * (2 + kChainScalers)) void k_smooth_chain(Batch
         if (sw == 0) DIAGC(17, __builtin_amdgcn_s_memtime());
         if (!ok) {
             CTL_ST(abort, 1);
-            if (lane == 0) {
-                w.status[s] = MDG_ERR_HIP;
-                // release every downstream pass so all waves drain
-                __hip_atomic_fetch_max(my_flag, 1 << 30, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
+            w.status[s] = MDG_ERR_HIP;  // every lane, the same value
+            // release every downstream pass so all waves drain (whole wave, as above)
+            __hip_atomic_fetch_max(my_flag, 1 << 30, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 #undef CTL_LD
@@ -1335,9 +1337,13 @@ __global__ __launch_bounds__(kPkThreads) void k_peaks(BatchArgs a, Workspace w, 
     int total;
     const int o = block_exclusive_scan<BS>(kept, lds_i, &total);
     const long long b_tot = block_sum_ll<BS>(bordered, lds_l);
-    if (threadIdx.x == 0)
-        __hip_atomic_store(slot + chunk, kPkValid | ((unsigned long long)b_tot << 31) | (unsigned)total,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // published by the whole of wave 0 (a wave-uniform branch; the block sums are
+    // uniform, read through readfirstlane), not by one lane (publication audit)
+    if (threadIdx.x < 64) {
+        const unsigned long long v = kPkValid | ((unsigned long long)__builtin_amdgcn_readfirstlane((int)b_tot) << 31) |
+                                     (unsigned)__builtin_amdgcn_readfirstlane(total);
+        __hip_atomic_store(slot + chunk, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     long long before = 0, k_all = 0, b_all = 0;
     bool ok = true;
     for (int k = threadIdx.x; k < nch; k += BS) {
