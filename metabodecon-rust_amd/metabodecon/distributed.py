@@ -2,11 +2,13 @@
 
 Spectra are independent units (deconvoluter.rs:700-710 maps them one by one),
 so a batch is sharded into contiguous blocks, one per rank, with no data-path
-collective. The only exchange is the gather of the results: the per-spectrum
-(status, count, mse) records and the Lorentzian tables, padded to the largest
-count, via ``all_gather_into_tensor`` (RCCL over xGMI with the ``nccl``
-backend, ``gloo`` on CPU for tests). Two collectives per batch, a few hundred
-KB per rank -- negligible next to the compute.
+collective. The only exchange is the gather of the results: per spectrum its
+(status, count, mse) record and its Lorentzian table, padded to the largest count,
+packed into one buffer per rank and sent in ONE gather to the collecting rank
+(``gather_packed``; an all-gather only when every rank asks for the results),
+after a two-element all_reduce that agrees on the width and on the first failure
+(RCCL over xGMI with the ``nccl`` backend, ``gloo`` on CPU for tests). The gather
+buffers are kept across calls.
 
 On the GPU path every rank runs its block on its own device (LOCAL_RANK, see
 ``_native.default_device``) through ``Deconvoluter._run_device``; the tables
@@ -14,8 +16,8 @@ stay in HBM from the batch call through the RCCL gather, and come to the host
 once, after it.
 
 The fail-fast Result collect of the reference (deconvoluter.rs:704-707) is
-reproduced after the gather: every rank raises the error of the FIRST failing
-spectrum in global order.
+reproduced on every rank from the all_reduce: each raises the error of the FIRST
+failing spectrum in global order.
 """
 from __future__ import annotations
 
@@ -33,10 +35,27 @@ def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
     return lo, lo + base + (1 if rank < rem else 0)
 
 
-def _gather(out, inp, dst, group):
-    """all_gather_into_tensor, or (dst given) a gather of every rank's tensor to
-    rank ``dst`` only: one transfer per peer over its own link instead of a ring
-    through every rank. Returns the gathered tensor on the receiving ranks, else None."""
+_BUFS: dict = {}
+
+
+def _buf(key, shape, dtype, dev):
+    """A grow-only tensor kept across calls (no per-call allocation of the gather
+    buffers); the returned view is valid until the next call with the same key."""
+    import torch
+    n = 1
+    for d in shape:
+        n *= int(d)
+    t = _BUFS.get((key, dtype, str(dev)))
+    if t is None or t.numel() < n:
+        t = torch.empty(max(n, 1), dtype=dtype, device=dev)
+        _BUFS[(key, dtype, str(dev))] = t
+    return t[:n].view(*shape)
+
+
+def _collect(out, inp, dst, group):
+    """all_gather_into_tensor (dst None), or a gather of every rank's tensor to rank
+    ``dst`` only: one transfer per peer over its own link instead of a ring through
+    every rank. Returns the gathered tensor on the receiving ranks, else None."""
     import torch.distributed as dist
     if dst is None:
         dist.all_gather_into_tensor(out, inp, group=group)
@@ -48,44 +67,73 @@ def _gather(out, inp, dst, group):
     return None
 
 
-def gather_tables(status, counts, mse, tables, n_total: int, group=None, dst=None):
-    """Gather one rank's block results (torch tensors, all on the collective's
-    device: CUDA for nccl, CPU for gloo) into global order: on every rank
-    (all_gather, the default) or on rank ``dst`` only (the other ranks get None).
+_FAIL_NONE = -(1 << 62)  # header value when no spectrum failed
 
-    status/counts: int32[b], mse: f64[b], tables: f64[b, w, 3] (rows past a
-    spectrum's count are ignored). Returns (status, counts, mse, tables) of all
-    ``n_total`` spectra, tables padded to the largest count over all ranks. Two
-    gathers (records, tables) and one all_reduce (the table width)."""
+
+def gather_packed(status, counts, mse, tables, n_total: int, group=None, dst=0):
+    """The exchange of one multi-GPU call: every rank's block results in one buffer,
+    one gather. Returns (first_error, gathered) where first_error is (global index,
+    status) of the first failing spectrum in global order or None -- the same on
+    every rank -- and gathered is (status int32[n], counts int32[n], mse f64[n],
+    tables f64[n, w, 3]) on rank ``dst`` (every rank when dst is None), else None.
+
+    status/counts: int32[b], mse: f64[b], tables: f64[b, >= count, 3], all on the
+    collective's device (CUDA for nccl, CPU for gloo). Two collectives in all: a
+    two-element all_reduce(MAX) that agrees on the table width (the largest count of
+    any rank) and on the first failure (encoded as -(index * 1024 + status)), then
+    ONE gather of [status, count, mse, table rows] per spectrum, padded to that width.
+    The buffers are reused across calls (the returned tensors are views into them,
+    valid until the next call)."""
     import torch
     import torch.distributed as dist
-    world = dist.get_world_size(group)
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
     dev = tables.device
     per_rank = [shard_range(n_total, r, world) for r in range(world)]
     max_items = max(hi - lo for lo, hi in per_rank)
-    b = status.shape[0]
-    # record: status, count, mse as f64 (exact for counts/status < 2^53)
-    rec = torch.zeros((max_items, 3), dtype=torch.float64, device=dev)
-    rec[:b, 0] = status.to(torch.float64)
-    rec[:b, 1] = counts.to(torch.float64)
-    rec[:b, 2] = mse
-    all_rec = torch.empty((world * max_items, 3), dtype=torch.float64, device=dev)
-    all_rec = _gather(all_rec, rec, dst, group)
-    width = torch.tensor([int(tables.shape[1]) if b else 1], dtype=torch.int64, device=dev)
-    dist.all_reduce(width, op=dist.ReduceOp.MAX, group=group)
-    cap = max(int(width.item()), 1)
-    tab = torch.zeros((max_items, cap, 3), dtype=torch.float64, device=dev)
+    b = int(status.shape[0])
+    lo = per_rank[rank][0]
+    hdr = _buf("hdr", (2,), torch.int64, dev)
     if b:
-        tab[:b, : tables.shape[1]] = tables
-    all_tab = torch.empty((world * max_items, cap, 3), dtype=torch.float64, device=dev)
-    all_tab = _gather(all_tab, tab, dst, group)
-    if all_rec is None:
-        return None
-    keep = torch.tensor([r * max_items + k for r, (lo, hi) in enumerate(per_rank)
-                         for k in range(hi - lo)], dtype=torch.int64, device=dev)
-    all_rec, all_tab = all_rec[keep], all_tab[keep]
-    return (all_rec[:, 0].to(torch.int32), all_rec[:, 1].to(torch.int32), all_rec[:, 2],
-            all_tab)
+        width = counts.max().clamp(min=1, max=max(1, int(tables.shape[1]))).to(torch.int64)
+        code = torch.arange(lo, lo + b, device=dev, dtype=torch.int64) * 1024 + status.to(torch.int64)
+        code = torch.where(status != 0, -code, torch.full_like(code, _FAIL_NONE))
+        hdr[0] = width
+        hdr[1] = code.max()
+    else:
+        hdr[0] = 1
+        hdr[1] = _FAIL_NONE
+    dist.all_reduce(hdr, op=dist.ReduceOp.MAX, group=group)
+    w_all, f_all = (int(v) for v in hdr.tolist())
+    first = None if f_all == _FAIL_NONE else ((-f_all) // 1024, (-f_all) % 1024)
+    cols = 3 + 3 * w_all
+    pack = _buf("pack", (max_items, cols), torch.float64, dev)
+    if b:
+        pack[:b, 0] = status
+        pack[:b, 1] = counts
+        pack[:b, 2] = mse
+        wt = min(w_all, int(tables.shape[1]))
+        pack[:b, 3:3 + 3 * wt] = tables[:, :wt].reshape(b, 3 * wt)
+    recv = _buf("recv", (world * max_items, cols), torch.float64, dev)
+    got = _collect(recv, pack, dst, group)
+    if got is None:
+        return first, None
+    if all(hi - l == max_items for l, hi in per_rank):
+        rows = got
+    else:  # uneven shards: the first hi - lo rows of every rank's part, in rank order
+        rows = torch.cat([got[r * max_items: r * max_items + (hi - l)]
+                          for r, (l, hi) in enumerate(per_rank)])
+    return first, (rows[:, 0].to(torch.int32), rows[:, 1].to(torch.int32), rows[:, 2],
+                   rows[:, 3:].reshape(-1, w_all, 3))
+
+
+def gather_tables(status, counts, mse, tables, n_total: int, group=None, dst=0):
+    """Gather one rank's block results into global order on rank ``dst`` (the
+    default: the caller that collects; every rank when dst is None); other ranks get
+    None. status/counts int32[b], mse f64[b], tables f64[b, w, 3] (rows past a
+    spectrum's count are ignored). Returns (status, counts, mse, tables) of all
+    ``n_total`` spectra, tables padded to the largest count over all ranks
+    (gather_packed: one width/failure all_reduce and one gather)."""
+    return gather_packed(status, counts, mse, tables, n_total, group, dst)[1]
 
 
 def _to_results(status, counts, mse, tables) -> list[Result]:
@@ -106,7 +154,7 @@ def gather_results(local: Sequence[Result], n_total: int, group=None) -> list[Re
     for i, (_, p, _) in enumerate(local):
         if p.shape[0]:
             tables[i, : p.shape[0]] = torch.from_numpy(np.ascontiguousarray(p))
-    return _to_results(*gather_tables(status, counts, mse, tables, n_total, group))
+    return _to_results(*gather_tables(status, counts, mse, tables, n_total, group, dst=None))
 
 
 def deconvolute_distributed(spectra: Sequence, compute: Callable[[Sequence], list[Result]],
@@ -120,16 +168,19 @@ def deconvolute_distributed(spectra: Sequence, compute: Callable[[Sequence], lis
     return gather_results(local, len(spectra), group)
 
 
-def par_deconvolute_spectra(deconvoluter, spectra: Sequence, group=None):
+def par_deconvolute_spectra(deconvoluter, spectra: Sequence, group=None, dst=0):
     """Deconvoluter.par_deconvolute_spectra across all ranks of ``group`` (nccl):
-    each rank runs its shard on its own GPU, results stay in HBM through the RCCL
-    gather; every rank returns the full list of ``Deconvolution`` objects, or
-    raises the first error in global order."""
+    each rank runs its shard on its own GPU, and the results stay in HBM through the
+    RCCL exchange (gather_packed: one width/failure all_reduce, one gather). Rank
+    ``dst`` (every rank when dst is None) returns the full list of
+    ``Deconvolution`` objects in input order, the other ranks None; every rank
+    raises the error of the first failing spectrum in global order, like the
+    reference's fail-fast Result collect (deconvoluter.rs:704-707)."""
     import torch
-    import torch.distributed as dist
     from . import _native as nat
     from ._deconvolution import Deconvolution
     from .exceptions import from_status
+    import torch.distributed as dist
 
     spectra = list(spectra)
     world, rank = dist.get_world_size(group), dist.get_rank(group)
@@ -144,10 +195,10 @@ def par_deconvolute_spectra(deconvoluter, spectra: Sequence, group=None):
         counts = torch.zeros(0, dtype=torch.int32, device=dev)
         mse = torch.zeros(0, dtype=torch.float64, device=dev)
         tables = torch.zeros((0, 1, 3), dtype=torch.float64, device=dev)
-    results = _to_results(*gather_tables(status, counts, mse, tables, len(spectra), group))
-    out = []
-    for st, params, m in results:
-        if st:
-            raise from_status(st)
-        out.append(Deconvolution(params, m, deconvoluter.settings))
-    return out
+    first, got = gather_packed(status, counts, mse, tables, len(spectra), group, dst)
+    if first is not None:
+        raise from_status(first[1])
+    if got is None:
+        return None
+    settings = deconvoluter.settings
+    return [Deconvolution(params, m, settings) for _, params, m in _to_results(*got)]

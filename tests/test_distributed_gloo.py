@@ -36,7 +36,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, n_spectra=7):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "metabodecon-rust_amd")]
@@ -48,7 +48,7 @@ def _worker(rank, world, port, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        names = [f"sim_{i:02d}" for i in range(1, 8)]
+        names = [f"sim_{i:02d}" for i in range(1, 8)][:n_spectra]
         spectra = [load_case(n) for n in names]
         # inject one failing spectrum (flat -> NoPeaksDetected) and one more failure later
         x, y, sb, st, ign = spectra[2]
@@ -69,20 +69,22 @@ def _worker(rank, world, port, q):
 
 
 @pytest.mark.timeout(300)
-def test_gloo_world2_gather_matches_serial():
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_gloo_gather_matches_serial(world):
+    """The 7 sim spectra with two injected failures over 2-4 ranks (uneven blocks)."""
     import oracle
     from tests.golden.cases import load_case
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     got = dict(q.get(timeout=240) for _ in procs)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert got[0] == got[1]  # every rank holds the full, identical result list
+    assert all(got[r] == got[0] for r in range(world))  # every rank: the full, identical list
     names = [f"sim_{i:02d}" for i in range(1, 8)]
     for k, n in enumerate(names):
         x, y, sb, st, ign = load_case(n)
@@ -132,52 +134,71 @@ def test_bench_rejects_gpus_world_mismatch():
     assert p.returncode == 2
 
 
-def _gather_worker(rank, world, port, q):
+def _gather_worker(rank, world, port, n, q):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "metabodecon-rust_amd")]
     import torch
     import torch.distributed as dist
-    from metabodecon.distributed import gather_tables, shard_range
+    from metabodecon.distributed import gather_packed, gather_tables, shard_range
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        n = 7
         lo, hi = shard_range(n, rank, world)
         b = hi - lo
-        st = torch.tensor([10 * (lo + k) % 3 for k in range(b)], dtype=torch.int32)
-        cnt = torch.tensor([(lo + k) % 4 for k in range(b)], dtype=torch.int32)
-        mse = torch.tensor([0.5 * (lo + k) for k in range(b)], dtype=torch.float64)
-        w = 2 + rank  # ranks hold tables of different widths
-        tab = torch.arange(b * w * 3, dtype=torch.float64).reshape(b, w, 3) + 100 * rank
-        everyone = gather_tables(st, cnt, mse, tab, n)
-        root_only = gather_tables(st, cnt, mse, tab, n, dst=0)
-        if rank == 0:
-            same = all(torch.equal(a, c) for a, c in zip(everyone, root_only))
-        else:
-            same = root_only is None
-        q.put((rank, same, [t.tolist() for t in everyone[:3]]))
+
+        def block(fail_at=()):
+            st = torch.tensor([(10 + (lo + k) % 3) if (lo + k) in fail_at else 0
+                               for k in range(b)], dtype=torch.int32)
+            cnt = torch.tensor([1 + (lo + k) % 4 for k in range(b)], dtype=torch.int32)
+            mse = torch.tensor([0.5 * (lo + k) for k in range(b)], dtype=torch.float64)
+            w = 2 + rank  # ranks hold tables of different widths (>= their counts? not always)
+            tab = torch.arange(b * max(w, 4) * 3, dtype=torch.float64).reshape(b, max(w, 4), 3) \
+                + 100 * rank
+            return st, cnt, mse, tab
+        st, cnt, mse, tab = block()
+        everyone = gather_tables(st, cnt, mse, tab, n, dst=None)
+        root_only = gather_tables(st, cnt, mse, tab, n)  # dst=0: the default
+        same = (all(torch.equal(a, c) for a, c in zip(everyone, root_only)) if rank == 0
+                else root_only is None)
+        everyone = [t.clone() for t in everyone]  # views into reused buffers
+        # the first failure in global order is known to every rank, results only to dst
+        fails = (n - 1, 1) if n > 1 else (0,)
+        first, got = gather_packed(*block(fails), n, dst=0)
+        ok_first = first == (min(fails), 10 + min(fails) % 3)
+        ok_got = (got is not None) == (rank == 0)
+        q.put((rank, same, ok_first and ok_got, [t.tolist() for t in everyone]))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.timeout(300)
-def test_gather_tables_to_rank0_equals_all_gather():
-    """gather_tables(dst=0) (the bench's multi-rank gather: every peer sends to rank 0
-    over its own link) gives rank 0 exactly the all_gather result, in global order with
-    padded tables, and the other ranks None."""
+@pytest.mark.parametrize("world,n", [(2, 7), (3, 7), (4, 10), (3, 2), (4, 1)])
+def test_gather_tables_worlds_uneven_and_empty_ranks(world, n):
+    """gather_tables / gather_packed at world sizes 2-4 with uneven shards and ranks
+    that own no spectrum (n < world): rank 0's gather (the default, one transfer per
+    peer) equals the all-gather, which holds every record and every table row up to
+    the spectrum's count in global order; the first failure in global order is the
+    same on every rank and the results reach rank 0 only."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_gather_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, n, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = dict((r, (same, recs)) for r, same, recs in (q.get(timeout=240) for _ in procs))
+    got = {r: rest for r, *rest in (q.get(timeout=240) for _ in procs)}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert got[0][0] and got[1][0]
-    status, counts, mse = got[0][1]
-    assert status == [10 * i % 3 for i in range(7)] and counts == [i % 4 for i in range(7)]
-    assert mse == [0.5 * i for i in range(7)]
+    assert all(got[r][0] and got[r][1] for r in range(world)), got
+    status, counts, mse, tables = got[0][2]
+    assert status == [0] * n and counts == [1 + i % 4 for i in range(n)]
+    assert mse == [0.5 * i for i in range(n)]
+    for i in range(n):
+        r = next(r for r in range(world) if shard_range(n, r, world)[0] <= i < shard_range(n, r, world)[1])
+        k = i - shard_range(n, r, world)[0]
+        w = max(2 + r, 4)
+        want = [[float(k * w * 3 + j * 3 + c + 100 * r) for c in range(3)] for j in range(counts[i])]
+        assert tables[i][: counts[i]] == want, (i, r)
+    assert all(got[r][2] == got[0][2] for r in range(world))  # the all-gather, everywhere
