@@ -100,7 +100,8 @@ def parse(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = len(sched_getaffinity)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-configs", action="store_true", help="headline only")
-    ap.add_argument("--configs", default="0,2,3,4", help="secondary configs to measure")
+    ap.add_argument("--configs", default="0,1h,2,3,4",
+                    help="secondary configs to measure (1h: configs[1] from page-locked host rows)")
     ap.add_argument("--no-profile", action="store_true", help="no per-stage HIP events")
     ap.add_argument("--copy-io", action="store_true",
                     help="stage each step's spectrum and results through the context's own rows")
@@ -689,6 +690,91 @@ def headline_queue(args, nat, torch, dist, dev, rank, world):
     return res
 
 
+def host_rows_config(args, nat, torch, dev, threads):
+    """configs[1] from host memory: the headline's synthetic 131072-pt/2048-peak
+    spectra held in page-locked host rows (mdg_host_alloc; a reference caller's
+    Spectrum rows live in host memory, deconvoluter.rs:530-552), deconvoluted by
+    mdg_deconvolute_rows in batches of --max-batch on --lanes engine contexts, one
+    host thread per lane: each call DMAs its batch's rows in (one transfer for the
+    adjacent rows; the shared axis once), runs the pipeline and copies the filled
+    result rows back, so PCIe is inside the timed region and one lane's transfers
+    overlap the other lane's kernels. A step is max_batch x lanes spectra, as in the
+    headline; 2 spectra per timed batch are checked against the oracle afterwards."""
+    import threading
+    n, cap, B, L = args.n, args.cap, args.max_batch, args.lanes
+    R = 4 * B * L  # distinct spectra, cycled (page-locked host rows: R MiB)
+    gen = nat.Context(dev.index)
+    xd, yd = synth_device(nat, gen, torch, R, n, args.peaks, 0, dev, args.hw_scale)
+    gen.close()
+    X = nat.pinned_empty((n,))
+    Y = nat.pinned_empty((R, n))
+    if X is None or Y is None:
+        return {"error": "page-locked host memory unavailable"}
+    X[...] = xd.cpu().numpy()
+    Y[...] = yd.cpu().numpy()
+    del xd, yd
+    torch.cuda.empty_cache()
+    settings = nat.default_settings()
+    lanes = [nat.Context(dev.index) for _ in range(L)]
+    xr = np.array([X.ctypes.data] * B, dtype=np.uintp)  # one shared axis (uploaded once)
+    sb = np.array([SB] * B, dtype=np.float64)
+    outs = [nat.pinned_empty((B, cap, 3)) for _ in range(L)]
+    res = [(np.zeros(B, dtype=np.uintp), np.zeros(B), np.zeros(B, dtype=np.intc)) for _ in range(L)]
+    picks = []  # (batch index, row in batch, params, mse, status, count) kept for the check
+
+    def run(j, batch):
+        yr = np.array([Y[(batch * B + r) % R].ctypes.data for r in range(B)], dtype=np.uintp)
+        cnt, mse, st = res[j]
+        rc = nat.lib().mdg_deconvolute_rows(
+            lanes[j].handle, B, n, xr.ctypes.data_as(ctypes.POINTER(nat._dp)),
+            yr.ctypes.data_as(ctypes.POINTER(nat._dp)), nat.ptr(sb), ctypes.byref(settings), None,
+            0, nat.ptr(outs[j]), cap, nat.ptr(cnt, nat._szp), nat.ptr(mse),
+            st.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+        assert rc == 0, nat.strerror(rc)
+
+    def lane_loop(j, n_batches, keep):
+        for k in range(j, n_batches, L):
+            run(j, k)
+            if keep:
+                cnt, mse, st = res[j]
+                for r in (0, B - 1):
+                    picks.append((k, r, outs[j][r, : int(cnt[r])].copy(), float(mse[r]),
+                                  int(st[r]), int(cnt[r])))
+
+    def timed(n_batches, keep):
+        th = [threading.Thread(target=lane_loop, args=(j, n_batches, keep)) for j in range(L)]
+        t0 = time.perf_counter()
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        return time.perf_counter() - t0
+
+    timed(L * max(1, args.warmup), False)  # warm-up: workspaces, staging, pinned rows
+    n_batches = L * args.steps
+    el = timed(n_batches, True)
+    spectra = n_batches * B
+    # the checker, after timing: the oracle on the sampled rows
+    import oracle
+    rows = np.stack([Y[(k * B + r) % R] for k, r, *_ in picks])
+    ost, ocnt, oout, omse = oracle.deconvolute_batch(np.asarray(X), rows, np.array([SB] * len(picks)),
+                                                     threads=threads, cap=cap)
+    ok = sum(int(st == int(ost[i]) and c == int(ocnt[i]) and np.array_equal(p, oout[i][:c]) and
+                 abs(m - float(omse[i])) <= 1e-12 * abs(float(omse[i])))
+             for i, (_, _, p, m, st, c) in enumerate(picks))
+    for c in lanes:
+        c.close()
+    h2d = spectra * 8 * n + n_batches * 8 * n
+    return {"value": spectra / el, "unit": "spectra/s", "ms_per_step": el / args.steps * 1e3,
+            "steps": args.steps, "warmup": args.warmup, "spectra_per_step": B * L,
+            "max_batch": B, "lanes": L, "verified": f"{ok}/{len(picks)}",
+            "pcie_h2d_gb_per_s": h2d / el / 1e9,
+            "workload": ("configs[1] spectra in page-locked host rows (mdg_host_alloc) through "
+                         "mdg_deconvolute_rows: batches of max_batch on lanes engine contexts, one "
+                         "host thread each; H2D of the rows, the pipeline and the D2H of the filled "
+                         "result rows inside the timed region")}
+
+
 def batch_config(args, nat, torch, dev, B, n, peaks, steps, warmup, tag, hw_scale=1.0):
     """One resident batch of B synthetic spectra per step (configs[2], configs[3])."""
     settings = nat.default_settings()
@@ -1204,13 +1290,13 @@ def finish(args, line, value, nat, torch, dist, dev, rank, world, local):
         line["configs" if world > 1 else "configs_dist"] = dc
     if rank == 0 and world == 1:
         torch.cuda.synchronize()
-        want = set() if args.no_configs else {int(c) for c in args.configs.split(",") if c}
+        want = set() if args.no_configs else {c.strip() for c in args.configs.split(",") if c.strip()}
         configs = {}
         blood_sp = blood_set = c3 = None
         # configs[4] first: measured after configs[0] and configs[2] (their contexts'
         # streams created before the 16 lanes') its sets took 5.5 instead of 3.9 ms
         # (tools/c4_order.sh), the others are single-stream and order-insensitive
-        if 4 in want:
+        if "4" in want:
             import metabodecon as md
             # measured in a child process, as a fresh user process runs it: in this
             # one the headline's contexts and torch's streams already hold hardware
@@ -1228,15 +1314,17 @@ def finish(args, line, value, nat, torch, dist, dev, rank, world, local):
                     configs[key]["process"] = "child (bench.py --c4-only)"
                 except (ValueError, IndexError):
                     configs[key] = {"error": p.stderr[-500:]}
-        if 0 in want:
+        if "1h" in want:
+            configs["configs[1]_host"] = host_rows_config(args, nat, torch, dev, host_threads(args)[0])
+        if "0" in want:
             blood_sp, configs["configs[0]"] = blood_gpu(args, nat, torch, dev)
             configs["optimize_settings"] = optimize_gpu(args, nat, torch, dev, blood_sp)
-        if 2 in want:
+        if "2" in want:
             configs["configs[2]"] = batch_config(args, nat, torch, dev, 256, 131072, 2048, 3, 1,
                                                  "b256")
             configs["configs[2]"]["workload"] = ("256 synthetic 131072-pt/2048-peak spectra per "
                                                  "step, one batched pipeline, resident in HBM")
-        if 3 in want:
+        if "3" in want:
             configs["configs[3]"] = batch_config(args, nat, torch, dev, 4096, 65536, 1024, 2, 1,
                                                  "b4096_n65536", hw_scale=2.0)
             configs["configs[3]"]["workload"] = (
@@ -1250,7 +1338,7 @@ def finish(args, line, value, nat, torch, dist, dev, rank, world, local):
             ctx = nat.Context(local)
             xd, yd = synth_device(nat, ctx, torch, 2 * threads, args.n, args.peaks, 0, dev)
             xh, Yh = xd.cpu().numpy(), yd.cpu().numpy()
-            if 3 in want:
+            if "3" in want:
                 x3, y3 = synth_device(nat, ctx, torch, 2 * threads, 65536, 1024, 0, dev, 2.0)
                 c3 = (x3.cpu().numpy(), y3.cpu().numpy())
             ctx.close()

@@ -2256,6 +2256,13 @@ __device__ __forceinline__ void fit_tf_body(const Workspace& w, int s, int P, in
         } else {
             double acc = -0.0;
             const int q = lane < Q ? lane : Q - 1;
+            // the stencil update's operands, loaded before the fold so their latency
+            // hides behind it (this tile's stencils are only written below, by this wave)
+            const double yq = w.ry[3 * base + min(p0 + q, npts - 1)];
+            const int kq = lane < Q / 3 ? lane : 0;
+            const int pkq = min(p0 / 3 + kq, P - 1);
+            const double* stq = w.stencil + 6 * base + 6 * (size_t)pkq;
+            const double s0 = stq[0], s1 = stq[1], s2 = stq[2], s3 = stq[3], s4 = stq[4], s5 = stq[5];
             // acc = fma(t, 1, acc) rounds as acc + t; the VOP2 v_fmac_f64 chain issues
             // a cycle faster per term than dependent v_add_f64 (eval_cost.hip)
             double one = 1.0;
@@ -2283,15 +2290,15 @@ __device__ __forceinline__ void fit_tf_body(const Workspace& w, int s, int P, in
             }
             // stencil update of the tile's peaks (k_fit_update): lane k gathers the
             // ratios y/sup of its peak's three points from lanes 3k..3k+2
-            const double ratio = w.ry[3 * base + min(p0 + q, npts - 1)] / acc;
-            const int k = lane < Q / 3 ? lane : 0;
+            const double ratio = yq / acc;
+            const int k = kq;
             const double r0 = __shfl(ratio, 3 * k, 64);
             const double r1 = __shfl(ratio, 3 * k + 1, 64);
             const double r2 = __shfl(ratio, 3 * k + 2, 64);
             const int pk = p0 / 3 + lane;
             if (lane < Q / 3 && pk < P) {
                 double* st = w.stencil + 6 * base + 6 * (size_t)pk;
-                Stencil sq{st[0], st[1], st[2], st[3], st[4], st[5]};
+                Stencil sq{s0, s1, s2, s3, s4, s5};
                 sq.y1 = sq.y1 * r0;
                 sq.y2 = sq.y2 * r1;
                 sq.y3 = sq.y3 * r2;
@@ -2393,6 +2400,13 @@ __device__ __forceinline__ void fit_tw_body(const Workspace& w, int s, int P, in
         } else {
             double acc = -0.0;
             const int q = lane < QQ ? lane : QQ - 1;
+            // the stencil update's operands, loaded before the fold so their latency
+            // hides behind it (this tile's stencils are only written below, by this wave)
+            const double yq = w.ry[3 * base + min(p0 + q, npts - 1)];
+            const int kq = lane < QQ / 3 ? lane : 0;
+            const int pkq = min(p0 / 3 + kq, P - 1);
+            const double* stq = w.stencil + 6 * base + 6 * (size_t)pkq;
+            const double s0 = stq[0], s1 = stq[1], s2 = stq[2], s3 = stq[3], s4 = stq[4], s5 = stq[5];
             double one = 1.0;
             asm volatile("" : "+v"(one));
             lds_barrier();  // chunk 0 written
@@ -2417,15 +2431,15 @@ __device__ __forceinline__ void fit_tw_body(const Workspace& w, int s, int P, in
             }
             // stencil update of the tile's peaks: lane k gathers the ratios y/sup of
             // its peak's three points from lanes 3k..3k+2
-            const double ratio = w.ry[3 * base + min(p0 + q, npts - 1)] / acc;
-            const int k = lane < QQ / 3 ? lane : 0;
+            const double ratio = yq / acc;
+            const int k = kq;
             const double r0 = __shfl(ratio, 3 * k, 64);
             const double r1 = __shfl(ratio, 3 * k + 1, 64);
             const double r2 = __shfl(ratio, 3 * k + 2, 64);
             const int pk = p0 / 3 + lane;
             if (lane < QQ / 3 && pk < P) {
                 double* st = w.stencil + 6 * base + 6 * (size_t)pk;
-                Stencil sq{st[0], st[1], st[2], st[3], st[4], st[5]};
+                Stencil sq{s0, s1, s2, s3, s4, s5};
                 sq.y1 = sq.y1 * r0;
                 sq.y2 = sq.y2 * r1;
                 sq.y3 = sq.y3 * r2;

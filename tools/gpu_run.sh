@@ -14,7 +14,10 @@
 #   prof         the round's profile set (tools/prof_all.sh)
 #   c4           configs[4] by lanes and hardware queues (bench.py --c4-only)
 #   fitdiag      small-batch fit: PMC passes of tools/blood_trace.py 16 and the stamped
-#                tools/ubench/fit_diag (tools/pmc_fit.sh; build fit_diag first)
+#                tools/ubench/fit_diag over term-fold shapes (build fit_diag first)
+#   c0diag       configs[0]: host/device breakdown (tools/c0_breakdown.py) and the phase
+#                stamps of one pipeline (tools/stage_diag.py; the diag library first:
+#                make -C metabodecon-rust_amd diag && cp .../build/libmdgpu_diag.so tools/ubench/)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/run
 log=gpurun_out/run/session.log
@@ -48,9 +51,13 @@ for step in "$@"; do
       run c4 1200 bash tools/ab.sh c4 "${cfgs[@]}" ;;
     fitdiag)
       run pmc_fit 600 bash tools/pmc_fit.sh 16 16 992 tw7,tf,plain
-      for g in 16 32 48 64; do run "fit_diag_g$g" 60 env MDG_TW_G=$g tools/ubench/fit_diag 16 992 tw7; done
-      run fit_diag_b8 60 tools/ubench/fit_diag 8 992 tw7,tf
-      run fit_diag_b1 60 tools/ubench/fit_diag 1 992 tw7,tf ;;
+      run fit_shapes_b16 120 tools/ubench/fit_diag 16 992 s63.1.7@98,s63.2.7@16,s63.2.7@48,s63.1.7@16,s60.1.15@16,s60.1.15@50,s60.2.6@16,s63.2.3@16,s48.1.6@62,s63.1.9@98
+      run fit_shapes_b8 120 tools/ubench/fit_diag 8 992 s63.1.7@98,s63.2.7@32,s63.2.7@48,s60.1.15@32,s60.2.6@32
+      run fit_shapes_b1 120 tools/ubench/fit_diag 1 992 tf,s63.1.7@98,s63.2.7@48,s60.1.15@50 ;;
+    c0diag)
+      run c0_breakdown 300 python tools/c0_breakdown.py 200
+      run stage_diag_b1 120 python tools/stage_diag.py 1
+      run stage_diag_b16 120 python tools/stage_diag.py 16 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

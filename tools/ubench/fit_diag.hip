@@ -1,7 +1,9 @@
 // Phase breakdown and timing of the fit-superposition kernels on synthetic peak
 // tables (P peaks, 3P reduced points per spectrum): builds the library kernel source
 // with -DMDG_DIAG. usage: fit_diag [B] [P] [kinds, comma-separated; MDG_FITSUP names,
-// '/noeval' suffix = tf without evaluation]
+// '/noeval' suffix = tf without evaluation; "sQ.PB.PS@G" = the term fold
+// k_fit_sup_tw<TwShape<Q, PB, PS>> on a (G, B) grid, for the shapes listed in
+// launch_shape (experiments: G workgroups per spectrum, tiles grid-strided)]
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -DMDG_DIAG \
 //       tools/ubench/fit_diag.hip -o tools/ubench/fit_diag
 #include "../../metabodecon-rust_amd/csrc/mdg_kernels.hip"
@@ -9,6 +11,26 @@
 #include <cstdio>
 #include <vector>
 using namespace mdg;
+
+// experimental term-fold shapes (not in the library): returns EW, or 0 if unknown
+template <int Q, int PB, int PS>
+static int launch_one(const BatchArgs& a, const Workspace& w, int g) {
+    using SH = TwShape<Q, PB, PS>;
+    hipLaunchKernelGGL((k_fit_sup_tw<SH>), dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, 0, a, w, 0);
+    return SH::EW;
+}
+static int launch_shape(int q, int pb, int ps, const BatchArgs& a, const Workspace& w, int g) {
+    if (q == 63 && pb == 1 && ps == 7) return launch_one<63, 1, 7>(a, w, g);
+    if (q == 63 && pb == 2 && ps == 7) return launch_one<63, 2, 7>(a, w, g);
+    if (q == 63 && pb == 1 && ps == 3) return launch_one<63, 1, 3>(a, w, g);
+    if (q == 63 && pb == 2 && ps == 3) return launch_one<63, 2, 3>(a, w, g);
+    if (q == 60 && pb == 1 && ps == 15) return launch_one<60, 1, 15>(a, w, g);
+    if (q == 60 && pb == 2 && ps == 6) return launch_one<60, 2, 6>(a, w, g);
+    if (q == 48 && pb == 1 && ps == 6) return launch_one<48, 1, 6>(a, w, g);
+    if (q == 63 && pb == 1 && ps == 9) return launch_one<63, 1, 9>(a, w, g);
+    return 0;
+}
+
 int main(int argc, char** argv) {
     const int B = argc > 1 ? atoi(argv[1]) : 1, P = argc > 2 ? atoi(argv[2]) : 2048;
     const int N = 131072, capD = N / 2 + 2;
@@ -62,14 +84,18 @@ int main(int argc, char** argv) {
         const char* k = ks.c_str();
         const int mode = ks.find("/nostore") != std::string::npos ? 1 : ks.find("/noeval") != std::string::npos ? 2 : 0;
         (void)hipMemcpyToSymbol(HIP_SYMBOL(g_tf_mode), &mode, sizeof(mode));
-        setenv("MDG_FITSUP", ks.substr(0, ks.find('/')).c_str(), 1);
+        int sq = 0, spb = 0, sps = 0, sg = 0;
+        const bool shape = ks[0] == 's' && sscanf(k, "s%d.%d.%d@%d", &sq, &spb, &sps, &sg) == 4;
+        setenv("MDG_FITSUP", shape ? "tw7" : ks.substr(0, ks.find('/')).c_str(), 1);
         w.params_alt = fit_sup_fused(a) ? d_alt : nullptr;
         float best = 1e30f;
+        int shape_ew = 0;
         for (int rep = 0; rep < 6; ++rep) {
             (void)hipMemset(diag, 0, nd * 8);
             hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
             (void)hipEventRecord(e0);
-            launch_fit_sup(a, w, 24, 0, 0);
+            if (shape) shape_ew = launch_shape(sq, spb, sps, a, w, sg);
+            else launch_fit_sup(a, w, 24, 0, 0);
             (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
             float ms; (void)hipEventElapsedTime(&ms, e0, e1);
             if (rep > 0 && ms < best) best = ms;
@@ -82,15 +108,16 @@ int main(int argc, char** argv) {
         const double evals = 3.0 * P * P * B;
         printf("%-6s B=%d P=%d  %.2f us/launch  %.3f T evals/s  same_as_dpp=%d\n", k, B, P, best * 1e3,
                evals / (best * 1e-3) / 1e12, (int)same);
-        if (ks.rfind("tw", 0) == 0) {
+        if (shape && !shape_ew) { printf("%s: unknown shape\n", k); continue; }
+        if (ks.rfind("tw", 0) == 0 || shape) {
             // tw: waves 0..EW-1 evaluators, wave EW the fold wave; grid (g, B); a block
             // with blockIdx.x >= tiles has no work. Slots: see fit_tw_body.
             std::vector<long long> d(nd);
             (void)hipMemcpy(d.data(), diag, nd * 8, hipMemcpyDeviceToHost);
-            const int EW = ks == "tw7" ? 7 : ks == "tw3" ? 3 : ks == "tw9" ? 9 : ks == "tw4" ? 4 : ks == "tw14" ? 14 : 6;
-            const int QQ = ks == "tw4" ? 60 : 63;
+            const int EW = shape ? shape_ew : 7;
+            const int QQ = shape ? sq : 63;
             const char* tg = std::getenv("MDG_TW_G");
-            const int g = tg ? std::max(1, std::atoi(tg)) : (3 * 2048 + 62) / 63;
+            const int g = shape ? sg : tg ? std::max(1, std::atoi(tg)) : (3 * 2048 + 62) / 63;
             const int tiles = (3 * P + QQ - 1) / QQ, active = std::min(g, tiles);
             double ev[8] = {0}, fo[8] = {0};
             long long t0 = -1, t1 = 0;
