@@ -286,6 +286,27 @@ def roofline_from_stages(ctx, stages, work, tag, n):
     return r
 
 
+def rocprof_check(roof):
+    """The rocprof figure the live roofline is checked against: the newest committed
+    tools/alone_kernels.py summary of a rocprofv3 kernel trace of this bench
+    (profiles/r*_bench_alone.json): the same kernel's average duration over the
+    launches that ran alone on the GPU -- the profiled pass `achieved` is taken from."""
+    if not roof or not roof.get("kernel"):
+        return None
+    k = roof["kernel"].split("(")[0].replace("void ", "").strip()
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_bench_alone.json")), reverse=True):
+        try:
+            d = json.load(open(path))["kernels"][k]["alone"]
+        except (OSError, KeyError, ValueError):
+            continue
+        ms = d["avg_us"] / 1e3
+        return {"source": os.path.relpath(path, ROOT), "kernel": k, "launches": d["launches"],
+                "avg_launch_ms": ms, "frac": roof["algorithmic_per_launch"] / (ms / 1e3) /
+                (1e12 if roof["unit"] == "TFLOP/s" else 1e9) / roof["peak"],
+                "live_over_rocprof": roof["avg_launch_ms"] / ms}
+    return None
+
+
 def work_per_launch(nat, ctx, B, n, counts, settings, x0, x1, sb):
     """Algorithmic flops/bytes per launch of each work stage for the last batch run
     (SURVEY 8d): 5 flops per Lorentzian evaluation; fit 3*P_sel^2 evaluations per
@@ -663,6 +684,8 @@ def headline_queue(args, nat, torch, dist, dev, rank, world):
     work, P_sel = work_per_launch(nat, lane, B, n, counts, settings, 14.8,
                                   14.8 - 20.0 / (n - 1.0), SB)
     roof = roofline_from_stages(lane, prof, work, f"q{B}", n) if prof else None
+    if roof:
+        roof["rocprof"] = rocprof_check(roof)
     if roof and qprof.get(roof["stage"], (0, 0))[1]:
         ms, cnt = qprof[roof["stage"]]
         roof["in_queue"] = {

@@ -125,6 +125,16 @@ int mdg_synth_lorentzians_hw(uint64_t seed, size_t n_peaks, double lo, double hi
 /* Irwin-Hall(12) noise, exact in binary64: sigma * (sum of 12 u48 - 6). */
 int mdg_synth_noise(uint64_t seed, size_t n, double sigma, double* out);
 
+/* Host (no GPU): decode one JCAMP-DX data block (the text after ##XYDATA= / ##DATA TABLE=,
+ * trimmed) into intensities times `factor` <- JcampDx::decode_asdf / decode_affn,
+ * spectrum/formats/jcampdx.rs:892-1091 (the reference's rewriting passes, then every
+ * line minus its first token). *n_out receives the value count; MDG_CAPACITY when it
+ * exceeds cap (nothing written). MDG_INVALID_ARGUMENT for blocks it leaves to the
+ * Python reader: non-ASCII text, or data the reference rejects (the reader then raises
+ * the reference's error). */
+int mdg_jcampdx_decode(const char* data, size_t len, double factor, double* out, size_t cap,
+                       size_t* n_out);
+
 /* ---- device contexts ------------------------------------------------------ */
 int mdg_device_count(int* count);
 /* Page-locked host memory for spectrum rows and result tables (the storage behind

@@ -54,6 +54,7 @@ EXPORTS = [
     "mdg_queue_create", "mdg_queue_submit", "mdg_queue_flush", "mdg_queue_set_flush_us",
     "mdg_queue_synchronize",
     "mdg_queue_lane", "mdg_queue_stats", "mdg_queue_destroy", "mdg_queue_fail_next_launch",
+    "mdg_jcampdx_decode",
 ]
 
 
@@ -97,7 +98,7 @@ _lib_lock = threading.Lock()
 # the engine sources in the Makefile's order (SRC then HDR): their sha256 is compiled
 # into the library (mdg_build_info) so a stale build is refused at load time
 _PKG_ROOT = os.path.dirname(_HERE)
-SOURCE_FILES = ["csrc/mdg_kernels.hip", "csrc/mdg_capi.hip", "csrc/mdg_common.hpp",
+SOURCE_FILES = ["csrc/mdg_kernels.hip", "csrc/mdg_capi.hip", "csrc/mdg_jcampdx.cpp", "csrc/mdg_common.hpp",
                 "csrc/mdg_kernels.hpp", "csrc/mdg_chain_asm.inc", "../include/mdgpu.h"]
 
 
@@ -272,6 +273,7 @@ def _declare(L):
     L.mdg_queue_stats.argtypes = [_vp, _u64p, _u64p, _szp]
     L.mdg_queue_destroy.argtypes = [_vp]
     L.mdg_queue_fail_next_launch.argtypes = [_vp, ctypes.c_int]
+    L.mdg_jcampdx_decode.argtypes = [ctypes.c_char_p, _sz, ctypes.c_double, _dp, _sz, _szp]
     L.mdg_synth_batch_device_hw.argtypes = [_vp, _sz, _sz, ctypes.c_double, ctypes.c_double,
                                             ctypes.c_uint64, _sz, ctypes.c_double, ctypes.c_double,
                                             ctypes.c_double, ctypes.c_double, _vp, _vp]
