@@ -102,6 +102,7 @@ struct mdg_ctx {
     void* hsmall = nullptr;
     size_t hsmall_bytes = 0;
     bool hsmall_busy = false;  // a call that failed midway may still have copies in flight
+    size_t rows_guess = 0;     // batch_host: result rows fetched with the records (last count + 1/8)
     // profiling
     uint32_t profile_mask = 0;  // stages timed with hipEvents (bit = stage)
     std::vector<Pending> pending;
@@ -1145,9 +1146,12 @@ static int upload_rows(mdg_ctx* c, hipStream_t st, char* dst, const void* const*
     return MDG_OK;
 }
 
-// Host-buffer batch: staging buffers, the caller's uploads (upload(dx, dy, st)
-// enqueues the H2D copies of x and y into the staging rows), the pipeline, and the
-// results back (only the rows the spectra filled). shared_x: one axis row.
+// Host-buffer batch: staging buffers, the caller's uploads (upload(dx, dy, st, &sent)
+// enqueues the H2D copies of x and y into the staging rows; an upload with
+// descriptors of its own sends them in the same copy as the signal boundaries and
+// sets sent), the pipeline, and the results back in one round trip (the per-spectrum
+// records and the first rows_guess rows of every table; more rows, if a spectrum has
+// them, in a second copy). shared_x: one axis row.
 template <typename Upload>
 static int batch_host(mdg_ctx* c, size_t b, size_t n, bool shared_x, Upload upload, const double* sb,
                       const mdg_settings* s, const double* ignore, size_t n_ignore, mdg_lorentzian* out,
@@ -1159,7 +1163,7 @@ static int batch_host(mdg_ctx* c, size_t b, size_t n, bool shared_x, Upload uplo
     int rc;
     if ((rc = ensure(c->st_x, xrows * n * 8))) return rc;
     if ((rc = ensure(c->st_y, b * n * 8))) return rc;
-    if ((rc = ensure(c->st_sb, b * 16))) return rc;
+    if ((rc = ensure(c->st_sb, b * 48))) return rc;  // [sb: 2b doubles][descriptors: 4b]
     if ((rc = ensure(c->st_out, std::max<size_t>(1, b * cap) * 24))) return rc;
     // the per-spectrum results in one device row, [mse: 8 b][counts: 4 b][statuses:
     // 4 b] like the host scratch below, so they come back in one copy
@@ -1169,8 +1173,8 @@ static int batch_host(mdg_ctx* c, size_t b, size_t n, bool shared_x, Upload uplo
     int32_t* d_st = d_cnt + b;
     double* dx = (double*)c->st_x.p;
     double* dy = (double*)c->st_y.p;
-    // page-locked scratch: [sb: 16 b][mse: 8 b][counts: 4 b][statuses: 4 b][the
-    // upload's own descriptors: 32 b (mdg_deconvolute_rows_i32)]
+    // page-locked scratch: [sb: 16 b][the upload's own descriptors: 32 b
+    // (mdg_deconvolute_rows_i32)][mse: 8 b][counts: 4 b][statuses: 4 b]
     const size_t hs_need = b * 64;
     if (c->hsmall_busy) {
         HIPCHK(hipStreamSynchronize(st));
@@ -1187,7 +1191,7 @@ static int batch_host(mdg_ctx* c, size_t b, size_t n, bool shared_x, Upload uplo
         c->hsmall_bytes = want;
     }
     double* h_sb = (double*)c->hsmall;
-    double* h_mse = h_sb + 2 * b;
+    double* h_mse = h_sb + 6 * b;
     int32_t* h_cnt = (int32_t*)(h_mse + b);
     int32_t* h_st = h_cnt + b;
     c->hsmall_busy = true;
@@ -1199,16 +1203,26 @@ static int batch_host(mdg_ctx* c, size_t b, size_t n, bool shared_x, Upload uplo
         c->hsmall_busy = false;
         return code;
     };
-    if ((rc = upload(dx, dy, st))) return fail(rc);
     std::memcpy(h_sb, sb, b * 16);
-    hipError_t he = hipMemcpyAsync(c->st_sb.p, h_sb, b * 16, hipMemcpyHostToDevice, st);
+    bool sent_sb = false;
+    if ((rc = upload(dx, dy, st, &sent_sb))) return fail(rc);
+    hipError_t he = hipSuccess;
+    if (!sent_sb) he = hipMemcpyAsync(c->st_sb.p, h_sb, b * 16, hipMemcpyHostToDevice, st);
     if (he != hipSuccess) return fail(hip_fail(he));
     BatchArgs a;
     if ((rc = fill_args(c, a, b, n, dx, shared_x ? 0 : n, dy, n, (const double*)c->st_sb.p, ignore,
                         n_ignore, (double*)c->st_out.p, cap, d_cnt, d_mse, d_st)))
         return fail(rc);
     if ((rc = run_pipeline(c, a, s))) return fail(rc);
+    // Only the rows the spectra filled travel back (cap is usually N/2 + 2 rows, 1.5
+    // MiB per 131072-point spectrum, against ~24 KiB of Lorentzians), and their count
+    // is known only after the pipeline: the first rows_guess rows (the context's last
+    // largest count and an eighth more) come back with the records, in the same round
+    // trip, and a second copy follows only when a spectrum has more rows than that.
+    const size_t guess = std::min(cap, c->rows_guess);
     he = hipMemcpyAsync(h_mse, d_mse, b * 16, hipMemcpyDeviceToHost, st);
+    if (he == hipSuccess && guess)
+        he = hipMemcpy2DAsync(out, cap * 24, c->st_out.p, cap * 24, guess * 24, b, hipMemcpyDeviceToHost, st);
     if (he != hipSuccess) return fail(hip_fail(he));
     he = hipStreamSynchronize(st);
     if (he != hipSuccess) return fail(hip_fail(he));
@@ -1216,14 +1230,14 @@ static int batch_host(mdg_ctx* c, size_t b, size_t n, bool shared_x, Upload uplo
     std::memcpy(mse, h_mse, b * 8);
     const int32_t* cnt = h_cnt;
     const int32_t* stv = h_st;
-    // only the rows the spectra filled travel back (cap is usually N/2 + 2 rows,
-    // 1.5 MiB per 131072-point spectrum, against ~24 KiB of Lorentzians)
     size_t rows = 0;
     for (size_t i = 0; i < b; ++i) rows = std::max(rows, std::min(cap, (size_t)std::max(0, cnt[i])));
-    if (rows)
-        HIPCHK(hipMemcpy2DAsync(out, cap * 24, c->st_out.p, cap * 24, rows * 24, b,
-                                hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    if (rows > guess) {
+        HIPCHK(hipMemcpy2DAsync((char*)out + guess * 24, cap * 24, (const char*)c->st_out.p + guess * 24,
+                                cap * 24, (rows - guess) * 24, b, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+    }
+    c->rows_guess = rows + rows / 8 + 16;
     drain_timers(c);
     int first = MDG_OK;
     for (size_t i = 0; i < b; ++i) {
@@ -1248,7 +1262,7 @@ int mdg_deconvolute_batch(mdg_ctx* c, size_t b, size_t n, const double* x, size_
     if (n < 2 || n > (size_t)INT32_MAX / 2 || b > (size_t)INT32_MAX) return MDG_INVALID_ARGUMENT;
     if (!x || !y || !sb || !counts || !mse || !status || (!out && cap)) return MDG_INVALID_ARGUMENT;
     const size_t xrows = x_stride ? b : 1;
-    auto upload = [&](double* dx, double* dy, hipStream_t st) -> int {
+    auto upload = [&](double* dx, double* dy, hipStream_t st, bool*) -> int {
         HIPCHK((x_stride == 0 || x_stride == n)
                    ? hipMemcpyAsync(dx, x, xrows * n * 8, hipMemcpyHostToDevice, st)
                    : hipMemcpy2DAsync(dx, n * 8, x, x_stride * 8, n * 8, b, hipMemcpyHostToDevice, st));
@@ -1274,7 +1288,7 @@ int mdg_deconvolute_rows(mdg_ctx* c, size_t b, size_t n, const double* const* x_
         if (!x_rows[i] || !y_rows[i]) return MDG_INVALID_ARGUMENT;
         shared = shared && x_rows[i] == x_rows[0];
     }
-    auto upload = [&](double* dx, double* dy, hipStream_t st) -> int {
+    auto upload = [&](double* dx, double* dy, hipStream_t st, bool*) -> int {
         int rc = upload_rows(c, st, (char*)dx, (const void* const*)x_rows, shared ? 1 : b, n * 8);
         return rc ? rc : upload_rows(c, st, (char*)dy, (const void* const*)y_rows, b, n * 8);
     };
@@ -1301,20 +1315,21 @@ int mdg_deconvolute_rows_i32(mdg_ctx* c, size_t b, size_t n, const double* axes,
         if (axes[3 * i + 2] == 0.0 || !std::isfinite(y_scale[i])) return MDG_INVALID_ARGUMENT;
         shared = shared && std::memcmp(axes + 3 * i, axes, 3 * sizeof(double)) == 0;
     }
-    auto upload = [&](double* dx, double* dy, hipStream_t st) -> int {
+    auto upload = [&](double* dx, double* dy, hipStream_t st, bool* sent_sb) -> int {
         int rc;
         if ((rc = ensure(c->st_raw, b * n * 4))) return rc;
-        if ((rc = ensure(c->st_desc, b * 32))) return rc;
         if ((rc = upload_rows(c, st, (char*)c->st_raw.p, (const void* const*)y_rows, b, n * 4))) return rc;
-        double* h = (double*)c->hsmall + 4 * b;  // batch_host's scratch, descriptor part
+        // batch_host's scratch holds [sb: 2b][descriptors: 4b] doubles: one copy sends both
+        double* h = (double*)c->hsmall + 2 * b;
         for (size_t i = 0; i < b; ++i) {
             h[4 * i] = axes[3 * i];
             h[4 * i + 1] = axes[3 * i + 1];
             h[4 * i + 2] = axes[3 * i + 2];
             h[4 * i + 3] = y_scale[i];
         }
-        HIPCHK(hipMemcpyAsync(c->st_desc.p, h, b * 32, hipMemcpyHostToDevice, st));
-        launch_decode_rows_i32((const int32_t*)c->st_raw.p, (const double*)c->st_desc.p, (int)b,
+        HIPCHK(hipMemcpyAsync(c->st_sb.p, c->hsmall, b * 48, hipMemcpyHostToDevice, st));
+        *sent_sb = true;
+        launch_decode_rows_i32((const int32_t*)c->st_raw.p, (const double*)c->st_sb.p + 2 * b, (int)b,
                                (int64_t)n, shared ? 1 : 0, dx, dy, st);
         HIPCHK(hipGetLastError());
         return MDG_OK;
