@@ -1912,12 +1912,18 @@ __device__ __forceinline__ void fit_init_pair(const BatchArgs& a, const Workspac
                                               int p1, int l1, int c1, int r1, int p2, int l2, int c2,
                                               int r2);
 
-constexpr int kSelLds = 4096;  // selected peaks staged in k_select's LDS (48 KB)
+// k_select's LDS: the SFR terms of the two windowed folds (up to kSfrLds; more go
+// through the workspace), reused afterwards for the selected peaks (up to kSelLds)
+constexpr int kSfrLds = 8192;          // 64 KB
+constexpr int kSelLds = 4096;          // 3 ints each: 48 KB of the same buffer
+constexpr int kSelCountDirect = 8;     // centers per thread counted directly
+static_assert(3 * kSelLds * sizeof(int) <= kSfrLds * sizeof(double), "selection fits the SFR buffer");
 template <int BS>
 __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double threshold) {
     const int s = blockIdx.x;
     __shared__ int lds_i[BS / 64 + 1];
-    __shared__ int sel_lds[3 * kSelLds];
+    __shared__ __attribute__((aligned(16))) double sfr_lds[kSfrLds];
+    int* const sel_lds = (int*)sfr_lds;
     __shared__ long long lds_l[BS / 64 + 1];
     __shared__ double thr_sh;
     __shared__ WinLds wl;
@@ -1935,43 +1941,60 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
     double* scores = w.scores + base;
     KSTAMP(10);
     // #(center <= sbi0) and #(center <= sbi1) over the ascending centers (scores:
-    // k_scores), by a two-level search: every step-th center first, then the step-1
-    // centers after the last sampled one that passed (both counts packed in one sum)
+    // k_peaks), both counts packed in one sum: up to kSelCountDirect centers per
+    // thread counted at once (their loads in flight together); beyond, a two-level
+    // search (every step-th center first, then the step-1 centers after the last
+    // sampled one that passed)
     const int step = (P + BS - 1) / BS;
-    long long k01;
-    {
-        const int i = threadIdx.x * step;
+    long long cnt0, cnt1;
+    if (step <= kSelCountDirect) {
+        const int i0 = threadIdx.x * step;
         long long v = 0;
-        if (i < P) {
-            const int64_t c = pc[i];
-            v = ((long long)(c <= sbi0) << 32) | (long long)(c <= sbi1);
+#pragma unroll
+        for (int u = 0; u < kSelCountDirect; ++u) {
+            const int64_t c = pc[min(i0 + u, P - 1)];
+            if (u < step && i0 + u < P) v += ((long long)(c <= sbi0) << 32) | (long long)(c <= sbi1);
         }
-        k01 = block_sum_ll<BS>(v, lds_l);
-    }
-    const long long k0 = k01 >> 32, k1 = k01 & 0xffffffffll;
-    long long cnt0 = k0 > 0 ? (k0 - 1) * step + 1 : 0, cnt1 = k1 > 0 ? (k1 - 1) * step + 1 : 0;
-    if (2 * (step - 1) > BS) {  // more than 2 * 513 * BS / 2 peaks: plain count
-        long long c0 = 0, c1 = 0;
-        for (int p = threadIdx.x; p < P; p += BS) {
-            const int64_t c = pc[p];
-            c0 += c <= sbi0;
-            c1 += c <= sbi1;
+        const long long k01 = block_sum_ll<BS>(v, lds_l);
+        cnt0 = k01 >> 32;
+        cnt1 = k01 & 0xffffffffll;
+    } else {
+        long long k01;
+        {
+            const int i = threadIdx.x * step;
+            long long v = 0;
+            if (i < P) {
+                const int64_t c = pc[i];
+                v = ((long long)(c <= sbi0) << 32) | (long long)(c <= sbi1);
+            }
+            k01 = block_sum_ll<BS>(v, lds_l);
         }
-        cnt0 = block_sum_ll<BS>(c0, lds_l);
-        cnt1 = block_sum_ll<BS>(c1, lds_l);
-    } else if (step > 1) {
-        const int t = threadIdx.x;
-        long long v = 0;
-        if (t < step - 1 && k0 > 0) {
-            const long long i = (k0 - 1) * step + 1 + t;
-            if (i < P) v += (long long)(pc[i] <= sbi0) << 32;
-        } else if (t >= step - 1 && t < 2 * (step - 1) && k1 > 0) {
-            const long long i = (k1 - 1) * step + 1 + (t - (step - 1));
-            if (i < P) v += (long long)(pc[i] <= sbi1);
+        const long long k0 = k01 >> 32, k1 = k01 & 0xffffffffll;
+        cnt0 = k0 > 0 ? (k0 - 1) * step + 1 : 0;
+        cnt1 = k1 > 0 ? (k1 - 1) * step + 1 : 0;
+        if (2 * (step - 1) > BS) {  // more than 2 * 513 * BS / 2 peaks: plain count
+            long long c0 = 0, c1 = 0;
+            for (int p = threadIdx.x; p < P; p += BS) {
+                const int64_t c = pc[p];
+                c0 += c <= sbi0;
+                c1 += c <= sbi1;
+            }
+            cnt0 = block_sum_ll<BS>(c0, lds_l);
+            cnt1 = block_sum_ll<BS>(c1, lds_l);
+        } else if (step > 1) {
+            const int t = threadIdx.x;
+            long long v = 0;
+            if (t < step - 1 && k0 > 0) {
+                const long long i = (k0 - 1) * step + 1 + t;
+                if (i < P) v += (long long)(pc[i] <= sbi0) << 32;
+            } else if (t >= step - 1 && t < 2 * (step - 1) && k1 > 0) {
+                const long long i = (k1 - 1) * step + 1 + (t - (step - 1));
+                if (i < P) v += (long long)(pc[i] <= sbi1);
+            }
+            const long long r = block_sum_ll<BS>(v, lds_l);
+            cnt0 += r >> 32;
+            cnt1 += r & 0xffffffffll;
         }
-        const long long r = block_sum_ll<BS>(v, lds_l);
-        cnt0 += r >> 32;
-        cnt1 += r & 0xffffffffll;
     }
     // centers ascend: position(center > sb) == #(center <= sb)
     const int left = cnt0 < P ? (int)cnt0 : 0;
@@ -1994,7 +2017,10 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
     // scores and squared deviations are >= +0: the windowed fold applies (one wave
     // folds short sets itself)
     const bool win = n_sfr >= 4 * kWinSeg;
-    double* sfr = w.tmp0 + (size_t)s * a.N;
+    // staged in LDS when they fit (the folds' loads are then LDS reads, not L2
+    // round trips); the short-set dpp_fold below stays off its asm global-load loop
+    // (n_sfr < 4 * kWinSeg, far below its 24-group threshold)
+    double* sfr = n_sfr <= kSfrLds ? sfr_lds : w.tmp0 + (size_t)s * a.N;
     for (int k = threadIdx.x; k < n_sfr; k += BS) sfr[k] = scores[k < left ? k : right + (k - left)];
     __syncthreads();
     KSTAMP(15);
@@ -2343,7 +2369,8 @@ struct TwShape {
 
 
 template <bool FAST, class SH>
-__device__ __forceinline__ void fit_tw_body(const Workspace& w, int s, int P, int it, double* T) {
+__device__ __forceinline__ void fit_tw_body(const Workspace& w, int s, int P, int it, double* T,
+                                            int tile0, int tstep) {
     constexpr int QQ = SH::LDS / (2 * SH::RS), EW = SH::EW, J = SH::J, RS = SH::RS, QS = SH::QS;
     constexpr int PB = J / 64;
     const size_t base = (size_t)s * w.capD;
@@ -2361,7 +2388,7 @@ __device__ __forceinline__ void fit_tw_body(const Workspace& w, int s, int P, in
 #ifdef MDG_DIAG
     _d_acc[7] = _d_t;
 #endif
-    for (int tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+    for (int tile = tile0; tile < tiles; tile += tstep) {
         const int p0 = tile * QQ;
         if (!folder) {
             const int pb = wv % PB, ps = wv / PB;
@@ -2462,8 +2489,54 @@ __global__ __launch_bounds__(64 * (SH::EW + 1)) void k_fit_sup_tw(BatchArgs a, W
     if (w.status[s] || fit_done(w, s, it)) return;
     const int P = w.sel_count[s];
     if (blockIdx.x == 0 && threadIdx.x == 0) w.unsafe[4 * s + (it + 2) % 3] = 0;
-    if (w.x_ok[s] && w.unsafe[4 * s + it % 3] == 0) fit_tw_body<true, SH>(w, s, P, it, T);
-    else fit_tw_body<false, SH>(w, s, P, it, T);
+    if (w.x_ok[s] && w.unsafe[4 * s + it % 3] == 0) fit_tw_body<true, SH>(w, s, P, it, T, blockIdx.x, gridDim.x);
+    else fit_tw_body<false, SH>(w, s, P, it, T, blockIdx.x, gridDim.x);
+}
+
+// K6i  the same term-fold tiles over ONE batch-wide list ("twf"): the tiles of all
+// spectra, spectrum after spectrum, grid-strided over a 1-D grid of about one
+// workgroup per slot of the chip. A (G, B) grid with a fixed G per spectrum leaves
+// a tail whenever the batch's tiles are not a multiple of the slots (B = 16 at
+// P = 992: 768 tiles of 63 points on 512 slots, 1.5 rounds); one list spreads them
+// evenly whatever B and the spectra's peak counts. Each workgroup reads the
+// batch's per-spectrum state once (B <= kTwfMaxB, one lane per spectrum) into LDS.
+constexpr int kTwfMaxB = 64;
+template <class SH>
+__global__ __launch_bounds__(64 * (SH::EW + 1)) void k_fit_sup_twf(BatchArgs a, Workspace w, int it) {
+    __shared__ __attribute__((aligned(16))) double T[SH::LDS];
+    __shared__ int first[kTwfMaxB + 1];  // first list item of spectrum s; first[B] = items
+    __shared__ int pk[kTwfMaxB];         // peaks of spectrum s
+    __shared__ int fastf[kTwfMaxB];
+    constexpr int QQ = SH::LDS / (2 * SH::RS);
+    if (threadIdx.x < 64) {
+        const int s = threadIdx.x;
+        int tiles = 0, P = 0, fast = 0;
+        if (s < a.B && !w.status[s] && !fit_done(w, s, it)) {
+            P = w.sel_count[s];
+            tiles = (3 * P + QQ - 1) / QQ;
+            fast = w.x_ok[s] && w.unsafe[4 * s + it % 3] == 0;
+            if (blockIdx.x == 0) w.unsafe[4 * s + (it + 2) % 3] = 0;
+        }
+        int x = tiles;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o, 64);
+            if (s >= o) x += y;
+        }
+        first[s + 1] = x;
+        if (s == 0) first[0] = 0;
+        pk[s] = P;
+        fastf[s] = fast;
+    }
+    __syncthreads();
+    const int items = first[a.B];
+    int s = 0;
+    for (int item = blockIdx.x; item < items; item += gridDim.x) {
+        while (first[s + 1] <= item) ++s;  // items ascend: the search resumes
+        const int tile = item - first[s];
+        if (fastf[s]) fit_tw_body<true, SH>(w, s, pk[s], it, T, tile, 1 << 20);
+        else fit_tw_body<false, SH>(w, s, pk[s], it, T, tile, 1 << 20);
+    }
 }
 
 // 1-D grid, spectrum = block % B (as k_mse_partial): round-robin dispatch puts the
@@ -3293,7 +3366,7 @@ const char* launch_select(const BatchArgs& a, const Workspace& w, int detector_o
 static std::string fit_choice(const BatchArgs& a) {
     if (const char* force = std::getenv("MDG_FITSUP")) {
         const std::string f(force);
-        if (f == "tf" || f == "tw7" || f == "plain") return f;
+        if (f == "tf" || f == "tw7" || f == "twf" || f == "twf1" || f == "plain") return f;
     }
     if (a.B == 1 && a.contexts > 1) return "tw7";
     return a.B <= 2 ? "tf" : a.B <= 24 ? "tw7" : "plain";
@@ -3311,7 +3384,28 @@ const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int i
         launch_k(k_fit_sup_tw<SH>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
         return "k_fit_sup_tw<63, 1, 7>";
     }
-    if (f == "tf") {
+    if ((f == "twf" || f == "twf1") && a.B <= kTwfMaxB) {
+        // one list of the batch's tiles over about one workgroup per slot: <63, 2, 7>
+        // (15 waves, 131 KB of LDS) one per CU, <63, 1, 7> (8 waves, 66 KB) two
+        static int cus = 0;
+        if (!cus) {
+            int dev = 0;
+            (void)hipGetDevice(&dev);
+            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+                cus = 256;
+        }
+        if (f == "twf") {
+            using SH = TwShape<63, 2, 7>;
+            const int g = tg ? std::max(1, std::atoi(tg)) : cus;
+            launch_k(k_fit_sup_twf<SH>, dim3(g), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
+            return "k_fit_sup_twf<63, 2, 7>";
+        }
+        using SH = TwShape<63, 1, 7>;
+        const int g = tg ? std::max(1, std::atoi(tg)) : 2 * cus;
+        launch_k(k_fit_sup_twf<SH>, dim3(g), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
+        return "k_fit_sup_twf<63, 1, 7>";
+    }
+    if (f == "tf" || f == "twf" || f == "twf1") {
         // 24 points per workgroup: one workgroup per tile of a 2048-peak spectrum (256)
         const int g = tg ? std::max(1, std::atoi(tg)) : (3 * 2048 + 23) / 24;
         launch_k(k_fit_sup_tf, dim3(g, a.B), dim3(64 * (kTfEW + 1)), 0, st, a, w, it);

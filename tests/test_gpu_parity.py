@@ -464,7 +464,16 @@ def test_chain_smoother_repeated_launches(ctx, monkeypatch):
             assert np.array_equal(row, oracle.moving_average(ys[s], 3, 3)), (rep, s)
 
 
-FIT_KERNELS = ["tf", "tw7", "plain"]  # the library's fit kernels (fit_choice, mdg_kernels.hip)
+# the library's fit kernels (fit_choice, mdg_kernels.hip); "twf"/"twf1" are the
+# batch-wide tile lists, "twf:5" the same with 5 workgroups (many tiles per workgroup)
+FIT_KERNELS = ["tf", "tw7", "twf", "twf1", "twf:5", "plain"]
+
+
+def _force_fit(monkeypatch, path):
+    kernel, _, g = path.partition(":")
+    monkeypatch.setenv("MDG_FITSUP", kernel)
+    if g:
+        monkeypatch.setenv("MDG_TW_G", g)
 
 
 @pytest.mark.parametrize("path", FIT_KERNELS)
@@ -472,7 +481,7 @@ def test_fit_superposition_kernels(ctx, path, monkeypatch):
     """Every fit-superposition kernel the library ships (24- and 63-point term folds,
     one thread per point; forced by MDG_FITSUP) gives the oracle's Lorentzians bit for
     bit, including peak counts that are not multiples of the tiles and chunks."""
-    monkeypatch.setenv("MDG_FITSUP", path)
+    _force_fit(monkeypatch, path)
     names = ["sim_03", "blood_03", "synth_128k_2k_s1"]
     for name in names:
         x, y, sb, st, ign = load_case(name)
@@ -487,7 +496,7 @@ def test_fit_superposition_kernels(ctx, path, monkeypatch):
 def test_fit_superposition_kernels_batch(ctx, path, monkeypatch):
     """The fit kernels on a batch whose spectra have different peak counts (tail
     tiles, grid-stride loops, per-spectrum range flags) against the oracle."""
-    monkeypatch.setenv("MDG_FITSUP", path)
+    _force_fit(monkeypatch, path)
     rows, ref = [], []
     for seed in (3, 4, 5):
         x, y = synth_spectrum(seed, n=65536, n_peaks=700 + 300 * seed)[:2]

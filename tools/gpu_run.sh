@@ -51,9 +51,9 @@ for step in "$@"; do
       run c4 1200 bash tools/ab.sh c4 "${cfgs[@]}" ;;
     fitdiag)
       run pmc_fit 600 bash tools/pmc_fit.sh 16 16 992 tw7,tf,plain
-      run fit_shapes_b16 120 tools/ubench/fit_diag 16 992 s63.1.7@98,s63.2.7@16,s63.2.7@48,s63.1.7@16,s60.1.15@16,s60.1.15@50,s60.2.6@16,s63.2.3@16,s48.1.6@62,s63.1.9@98
-      run fit_shapes_b8 120 tools/ubench/fit_diag 8 992 s63.1.7@98,s63.2.7@32,s63.2.7@48,s60.1.15@32,s60.2.6@32
-      run fit_shapes_b1 120 tools/ubench/fit_diag 1 992 tf,s63.1.7@98,s63.2.7@48,s60.1.15@50 ;;
+      run fit_shapes_b16 120 tools/ubench/fit_diag 16 992 twf,twf1,tw7,s63.1.7@98,s63.2.7@16,s63.2.7@48,s63.1.7@16,s60.1.15@16,s60.1.15@50,s60.2.6@16,s63.2.3@16,s48.1.6@62,s63.1.9@98
+      run fit_shapes_b8 120 tools/ubench/fit_diag 8 992 twf,twf1,s63.1.7@98,s63.2.7@32,s63.2.7@48,s60.1.15@32,s60.2.6@32
+      run fit_shapes_b1 120 tools/ubench/fit_diag 1 992 twf,twf1,tf,s63.1.7@98,s63.2.7@48,s60.1.15@50 ;;
     c0diag)
       run c0_breakdown 300 python tools/c0_breakdown.py 200
       run stage_diag_b1 120 python tools/stage_diag.py 1

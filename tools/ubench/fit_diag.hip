@@ -109,7 +109,7 @@ int main(int argc, char** argv) {
         printf("%-6s B=%d P=%d  %.2f us/launch  %.3f T evals/s  same_as_dpp=%d\n", k, B, P, best * 1e3,
                evals / (best * 1e-3) / 1e12, (int)same);
         if (shape && !shape_ew) { printf("%s: unknown shape\n", k); continue; }
-        if (ks.rfind("tw", 0) == 0 || shape) {
+        if (ks.rfind("tw7", 0) == 0 || shape) {
             // tw: waves 0..EW-1 evaluators, wave EW the fold wave; grid (g, B); a block
             // with blockIdx.x >= tiles has no work. Slots: see fit_tw_body.
             std::vector<long long> d(nd);
