@@ -220,7 +220,11 @@ def hbm_pipeline(tag, batch, iterations, value, n):
                        reverse=True):
         try:
             kern = json.load(open(path))["kernels"]
-            per = {k: kern[k]["hbm_bytes_per_launch"] * m / batch for k, m in launches.items()}
+            # matched by base name: template arguments differ between rounds
+            # (k_peaks -> k_peaks<256, 1024>)
+            by_base = {k.split("<")[0].strip(): v for k, v in kern.items()}
+            per = {k: by_base[k.split("<")[0].strip()]["hbm_bytes_per_launch"] * m / batch
+                   for k, m in launches.items()}
         except (OSError, KeyError, ValueError):
             continue
         total = sum(per.values())

@@ -301,7 +301,7 @@ int ensure_workspace(mdg_ctx* c, int B, int N, int n_ignore) {
         const size_t o_nig = take(Bs * 4), o_panic = take(Bs * 4), o_status = take(Bs * 4);
         const size_t o_dcnt = take(Bs * 4), o_scnt = take(Bs * 4), o_kcnt = take(Bs * 4);
         const size_t o_xok = take(Bs * 4), o_unsafe = take(Bs * 16), o_uk = take(Bs * 4);
-        const size_t o_pcnt = take(Bs * 2 * ((W + 255) / 256) * 4);
+        const size_t o_pcnt = take(Bs * 2 * ((W + kPkSlotWords - 1) / kPkSlotWords) * 4);
         const size_t o_mcnt = take(Bs * 4);
 
         if (c->arena.p) (void)hipFree(c->arena.p);
@@ -982,7 +982,7 @@ int run_pipeline_graphed(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     // the kernel-choice overrides (tests, diagnostics) select other kernels, so
     // they are part of the key too
     std::string envs;
-    for (const char* e : {"MDG_SMOOTH", "MDG_CHAIN_EXCL", "MDG_FITSUP", "MDG_GFIT", "MDG_TW_G", "MDG_MSE_NEARCAP",
+    for (const char* e : {"MDG_SMOOTH", "MDG_CHAIN_EXCL", "MDG_FITSUP", "MDG_GFIT", "MDG_TW_G", "MDG_PEAKS", "MDG_MSE_NEARCAP",
                           "MDG_DIAG_SKIP", "MDG_DIAG_DUP", "MDG_DIAG_PAD", "MDG_DIAG_PAD_SMALL", "MDG_PREP"}) {
         const char* v = std::getenv(e);
         envs += v ? v : "\x01";
@@ -1173,9 +1173,15 @@ static int batch_host(mdg_ctx* c, size_t b, size_t n, bool shared_x, Upload uplo
     int32_t* d_st = d_cnt + b;
     double* dx = (double*)c->st_x.p;
     double* dy = (double*)c->st_y.p;
+    // the first rows_guess result rows of every spectrum come back with the records
+    // (below); their count is known only after the pipeline
+    // (above 64 MiB of guessed rows, every spectrum's rows are copied on their own)
+    size_t guess = std::min(cap, c->rows_guess);
+    if (b * guess * 24 > ((size_t)64 << 20)) guess = 0;
     // page-locked scratch: [sb: 16 b][the upload's own descriptors: 32 b
-    // (mdg_deconvolute_rows_i32)][mse: 8 b][counts: 4 b][statuses: 4 b]
-    const size_t hs_need = b * 64;
+    // (mdg_deconvolute_rows_i32)][mse: 8 b][counts: 4 b][statuses: 4 b][the guessed
+    // result rows: 24 guess b]
+    const size_t hs_need = b * 64 + b * guess * 24;
     if (c->hsmall_busy) {
         HIPCHK(hipStreamSynchronize(st));
         c->hsmall_busy = false;
@@ -1194,6 +1200,7 @@ static int batch_host(mdg_ctx* c, size_t b, size_t n, bool shared_x, Upload uplo
     double* h_mse = h_sb + 6 * b;
     int32_t* h_cnt = (int32_t*)(h_mse + b);
     int32_t* h_st = h_cnt + b;
+    mdg_lorentzian* h_rows = (mdg_lorentzian*)(h_sb + 8 * b);
     c->hsmall_busy = true;
     // From here on DMAs may read the caller's page-locked rows (upload_rows sends
     // mdg_host_alloc rows without copying them): a failure must not return while they
@@ -1218,11 +1225,12 @@ static int batch_host(mdg_ctx* c, size_t b, size_t n, bool shared_x, Upload uplo
     // MiB per 131072-point spectrum, against ~24 KiB of Lorentzians), and their count
     // is known only after the pipeline: the first rows_guess rows (the context's last
     // largest count and an eighth more) come back with the records, in the same round
-    // trip, and a second copy follows only when a spectrum has more rows than that.
-    const size_t guess = std::min(cap, c->rows_guess);
+    // trip, into the page-locked scratch, and each spectrum's own rows go on to `out`
+    // from there (rows at and past counts[i] are never written: the device rows there
+    // are stale); a spectrum with more rows than the guess has the rest copied after.
     he = hipMemcpyAsync(h_mse, d_mse, b * 16, hipMemcpyDeviceToHost, st);
     if (he == hipSuccess && guess)
-        he = hipMemcpy2DAsync(out, cap * 24, c->st_out.p, cap * 24, guess * 24, b, hipMemcpyDeviceToHost, st);
+        he = hipMemcpy2DAsync(h_rows, guess * 24, c->st_out.p, cap * 24, guess * 24, b, hipMemcpyDeviceToHost, st);
     if (he != hipSuccess) return fail(hip_fail(he));
     he = hipStreamSynchronize(st);
     if (he != hipSuccess) return fail(hip_fail(he));
@@ -1231,12 +1239,18 @@ static int batch_host(mdg_ctx* c, size_t b, size_t n, bool shared_x, Upload uplo
     const int32_t* cnt = h_cnt;
     const int32_t* stv = h_st;
     size_t rows = 0;
-    for (size_t i = 0; i < b; ++i) rows = std::max(rows, std::min(cap, (size_t)std::max(0, cnt[i])));
-    if (rows > guess) {
-        HIPCHK(hipMemcpy2DAsync((char*)out + guess * 24, cap * 24, (const char*)c->st_out.p + guess * 24,
-                                cap * 24, (rows - guess) * 24, b, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
+    bool more = false;
+    for (size_t i = 0; i < b; ++i) {
+        const size_t r = std::min(cap, (size_t)std::max(0, cnt[i]));
+        rows = std::max(rows, r);
+        std::memcpy(out + i * cap, h_rows + i * guess, std::min(r, guess) * 24);
+        if (r > guess) {
+            more = true;
+            HIPCHK(hipMemcpyAsync(out + i * cap + guess, (const mdg_lorentzian*)c->st_out.p + i * cap + guess,
+                                  (r - guess) * 24, hipMemcpyDeviceToHost, st));
+        }
     }
+    if (more) HIPCHK(hipStreamSynchronize(st));
     c->rows_guess = rows + rows / 8 + 16;
     drain_timers(c);
     int first = MDG_OK;

@@ -173,9 +173,11 @@ __device__ __forceinline__ double superpose(double x, const double* __restrict__
 __device__ long long* g_diag = nullptr;
 __device__ int g_tf_mode = 0;
 __device__ int g_chain_mode = 0;  // chain_diag: 1 = feeder publishes everything at once, no scaler; 2 = no scaler; 3 = instant feeder; 4 = passes one after another  // fit_diag: 1 = evaluators skip LDS stores, 2 = skip evaluation
+// g_diag layout: DIAG_FLUSH records in [0, kDiagStampBase), KSTAMP slots after it
+constexpr size_t kDiagStampBase = (size_t)1 << 22;
 #define KSTAMP(slot)                                                           \
     if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0 && g_diag)      \
-        g_diag[(1 << 16) + (slot)] = (long long)__builtin_amdgcn_s_memtime()
+        g_diag[kDiagStampBase + (slot)] = (long long)__builtin_amdgcn_s_memtime()
 #define DIAG_DECL unsigned long long _d_t = __builtin_amdgcn_s_memtime(); unsigned long long _d_acc[8] = {0};
 #define DIAG_STAMP(i)                                                       \
     do {                                                                    \
@@ -187,9 +189,9 @@ __device__ int g_chain_mode = 0;  // chain_diag: 1 = feeder publishes everything
     } while (0)
 #define DIAG_FLUSH()                                                        \
     do {                                                                    \
-        if ((threadIdx.x & 63) == 0 && g_diag)                              \
-            for (int _i = 0; _i < 8; ++_i)                                  \
-                g_diag[((blockIdx.y * gridDim.x + blockIdx.x) * 16 + (threadIdx.x >> 6)) * 8 + _i] = (long long)_d_acc[_i]; \
+        const size_t _r = ((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * 16 + (threadIdx.x >> 6)) * 8; \
+        if ((threadIdx.x & 63) == 0 && g_diag && _r + 8 <= kDiagStampBase)  \
+            for (int _i = 0; _i < 8; ++_i) g_diag[_r + _i] = (long long)_d_acc[_i]; \
     } while (0)
 #else
 #define KSTAMP(slot)
@@ -1170,6 +1172,8 @@ __global__ void k_smooth(BatchArgs a, Workspace w, int iters, int ws) {
 // The per-center border scans of the reference become next/previous-set-bit
 // searches on these masks (K3): the predicates do not depend on the center.
 // ----------------------------------------------------------------------------------
+// look-back slots of k_peaks per spectrum (one per kPkSlotWords mask words)
+__device__ __forceinline__ int peak_slots(int W) { return (W + kPkSlotWords - 1) / kPkSlotWords; }
 __global__ void k_flags(BatchArgs a, Workspace w) {
     const int s = blockIdx.y;
     // the smoother has finished: its progress counters go back to zero for the
@@ -1188,8 +1192,7 @@ __global__ void k_flags(BatchArgs a, Workspace w) {
         fl = d0 > dp && (d0 >= dm || (d0 < 0. && dm >= 0.));
     }
     // k_peaks' per-chunk slots start empty
-    if (blockIdx.x == 0 && (int)threadIdx.x < (w.W + 255) / 256)
-        ((unsigned long long*)w.peak_cnt)[(size_t)s * ((w.W + 255) / 256) + threadIdx.x] = 0;
+    if (k < peak_slots(w.W)) ((unsigned long long*)w.peak_cnt)[(size_t)s * peak_slots(w.W) + k] = 0;
     const uint64_t bc = __ballot(fc), br = __ballot(fr), bl = __ballot(fl);
     if ((threadIdx.x & 63) == 0 && k < N) {
         const int word = k >> 6;
@@ -1310,9 +1313,12 @@ __device__ __forceinline__ double score_peak(const double* __restrict__ sm, int 
     return fmin(left, right);
 }
 
-// K3 per chunk of kPkWords mask words (one word per thread, many workgroups per
-// spectrum: a single-workgroup version took 46-53 us at N = 131072).
-constexpr int kPkWords = 256;
+// K3 per chunk of WORDS mask words (one word per thread, many workgroups per
+// spectrum: a single-workgroup version took 46-53 us at N = 131072). Large batches
+// take chunks of 256 words on 1024 threads; small ones chunks of 64 words on 256
+// threads, four times the workgroups per spectrum (a B = 1 launch is otherwise 8
+// workgroups on 8 CUs, each scoring ~2000 peaks). The slots are laid out for the
+// finer chunking (kPkSlotWords, mdg_common.hpp) whichever is launched.
 // K3 in one pass (decoupled look-back): every chunk counts its peaks, publishes
 // {bordered, kept} in its slot of w.peak_cnt (cleared by k_flags), then reads the
 // slots of all chunks of its spectrum -- they publish before they wait, so one
@@ -1320,20 +1326,20 @@ constexpr int kPkWords = 256;
 // chunks before it. Replaces k_peaks_count + k_peaks_write (one launch and one
 // word scan fewer).
 constexpr unsigned long long kPkValid = 1ull << 62;
-// kPkThreads threads per chunk: the first kPkWords own one mask word each; all of
-// them score the chunk's peaks afterwards (four times the threads for that part)
-constexpr int kPkThreads = 1024;
-__global__ __launch_bounds__(kPkThreads) void k_peaks(BatchArgs a, Workspace w, int detector_only, int score) {
-    constexpr int BS = kPkThreads;
+// BS threads per chunk: the first WORDS own one mask word each; all of them score
+// the chunk's peaks afterwards (four times the threads for that part)
+template <int WORDS, int BS>
+__global__ __launch_bounds__(BS) void k_peaks(BatchArgs a, Workspace w, int detector_only, int score) {
+    static_assert(WORDS % kPkSlotWords == 0 && WORDS <= BS, "chunk shape");
     const int s = blockIdx.y, chunk = blockIdx.x;
     __shared__ int lds_i[BS / 64 + 1];
     __shared__ long long lds_l[BS / 64 + 1];
     if (w.status[s]) return;  // uniform per spectrum: no chunk waits for a returned one
-    const int nch = (w.W + kPkWords - 1) / kPkWords;
-    unsigned long long* slot = (unsigned long long*)w.peak_cnt + (size_t)s * nch;
-    const int wd = chunk * kPkWords + threadIdx.x;
+    const int nch = (w.W + WORDS - 1) / WORDS;
+    unsigned long long* slot = (unsigned long long*)w.peak_cnt + (size_t)s * peak_slots(w.W);
+    const int wd = chunk * WORDS + threadIdx.x;
     int bordered = 0, kept = 0;
-    if ((int)threadIdx.x < kPkWords && wd < w.W) kept = word_peaks<false>(a, w, s, wd, detector_only, &bordered, 0);
+    if ((int)threadIdx.x < WORDS && wd < w.W) kept = word_peaks<false>(a, w, s, wd, detector_only, &bordered, 0);
     int total;
     const int o = block_exclusive_scan<BS>(kept, lds_i, &total);
     const long long b_tot = block_sum_ll<BS>(bordered, lds_l);
@@ -1733,9 +1739,26 @@ __device__ __noinline__ double seg_fold(double acc, const double* __restrict__ t
     return acc;
 }
 
-template <int BS>
-__device__ double window_fold(double acc0, WinLds& L, const double* __restrict__ t, int n,
-                              int stamp = 40) {
+// the same fold on terms staged in LDS: every lane reads each term from the same LDS
+// address (a broadcast read, no bank conflict) and adds it with a plain VOP2 fma --
+// no DPP: the term is already in every lane
+typedef const __attribute__((address_space(3))) double* lds_f64_ptr;
+__device__ __forceinline__ double seg_fold(double acc, lds_f64_ptr t, int n) {
+    int k = 0;
+    for (; k + 8 <= n; k += 8) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = t[k + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc = __builtin_fma(v[u], 1.0, acc);
+    }
+    for (; k < n; ++k) acc = __builtin_fma(t[k], 1.0, acc);
+    return acc;
+}
+
+// t: global terms (const double*) or LDS terms (lds_f64_ptr)
+template <int BS, typename TP>
+__device__ double window_fold(double acc0, WinLds& L, TP t, int n, int stamp = 40) {
     constexpr int NW = BS / 64;
     static_assert(kWinSeg <= 64, "one lane per segment in the prefix scan");
     KSTAMP(stamp + 5);
@@ -1831,7 +1854,7 @@ __device__ double window_fold(double acc0, WinLds& L, const double* __restrict__
                 const int i0 = min(n, k * seg), i1 = min(n, (k + 1) * seg);
                 tru = seg_fold(tru, t + i0, i1 - i0);
 #ifdef MDG_DIAG
-                if (lane == 0 && blockIdx.x == 0 && g_diag) g_diag[(1 << 16) + stamp + 7] += 1;
+                if (lane == 0 && blockIdx.x == 0 && g_diag) g_diag[kDiagStampBase + stamp + 7] += 1;
 #endif
             }
         }
@@ -1914,7 +1937,7 @@ __device__ __forceinline__ void fit_init_pair(const BatchArgs& a, const Workspac
 
 // k_select's LDS: the SFR terms of the two windowed folds (up to kSfrLds; more go
 // through the workspace), reused afterwards for the selected peaks (up to kSelLds)
-constexpr int kSfrLds = 8192;          // 64 KB
+constexpr int kSfrLds = 12288;         // 96 KB
 constexpr int kSelLds = 4096;          // 3 ints each: 48 KB of the same buffer
 constexpr int kSelCountDirect = 8;     // centers per thread counted directly
 static_assert(3 * kSelLds * sizeof(int) <= kSfrLds * sizeof(double), "selection fits the SFR buffer");
@@ -2020,12 +2043,18 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
     // staged in LDS when they fit (the folds' loads are then LDS reads, not L2
     // round trips); the short-set dpp_fold below stays off its asm global-load loop
     // (n_sfr < 4 * kWinSeg, far below its 24-group threshold)
-    double* sfr = n_sfr <= kSfrLds ? sfr_lds : w.tmp0 + (size_t)s * a.N;
+    const bool staged = n_sfr <= kSfrLds;
+    double* sfr = staged ? sfr_lds : w.tmp0 + (size_t)s * a.N;
     for (int k = threadIdx.x; k < n_sfr; k += BS) sfr[k] = scores[k < left ? k : right + (k - left)];
     __syncthreads();
     KSTAMP(15);
+    // every thread calls window_fold (barriers inside)
+    auto wfold = [&](int stamp) {
+        return staged ? window_fold<BS>(-0.0, wl, (lds_f64_ptr)sfr_lds, n_sfr, stamp)
+                      : window_fold<BS>(-0.0, wl, (const double*)sfr, n_sfr, stamp);
+    };
     if (win) {
-        const double sum = window_fold<BS>(-0.0, wl, sfr, n_sfr);  // every thread: barriers inside
+        const double sum = wfold(40);
         if (threadIdx.x == 0) thr_sh = sum / (double)n_sfr;
     } else if (threadIdx.x < 64) {
         const double mean = dpp_fold(-0.0, sfr, n_sfr) / (double)n_sfr;
@@ -2040,7 +2069,7 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
     }
     __syncthreads();
     double var = 0.0;
-    if (win) var = window_fold<BS>(-0.0, wl, sfr, n_sfr, 50) / (double)n_sfr;
+    if (win) var = wfold(50) / (double)n_sfr;
     else if (threadIdx.x < 64) var = dpp_fold(-0.0, sfr, n_sfr) / (double)n_sfr;
     KSTAMP(17);
     if (threadIdx.x == 0) {
@@ -2533,9 +2562,15 @@ __global__ __launch_bounds__(64 * (SH::EW + 1)) void k_fit_sup_twf(BatchArgs a, 
     int s = 0;
     for (int item = blockIdx.x; item < items; item += gridDim.x) {
         while (first[s + 1] <= item) ++s;  // items ascend: the search resumes
-        const int tile = item - first[s];
-        if (fastf[s]) fit_tw_body<true, SH>(w, s, pk[s], it, T, tile, 1 << 20);
-        else fit_tw_body<false, SH>(w, s, pk[s], it, T, tile, 1 << 20);
+        // LDS values are uniform here, but the compiler cannot know it: readfirstlane
+        // puts the spectrum, its tile and its peak count in SGPRs, so the body's
+        // addresses and x values are scalar (as under k_fit_sup_tw's blockIdx.y) and
+        // the FAST branch is a scalar branch
+        s = __builtin_amdgcn_readfirstlane(s);
+        const int tile = __builtin_amdgcn_readfirstlane(item - first[s]);
+        const int P = __builtin_amdgcn_readfirstlane(pk[s]);
+        if (__builtin_amdgcn_readfirstlane(fastf[s])) fit_tw_body<true, SH>(w, s, P, it, T, tile, 1 << 20);
+        else fit_tw_body<false, SH>(w, s, P, it, T, tile, 1 << 20);
     }
 }
 
@@ -3336,11 +3371,17 @@ void launch_flags(const BatchArgs& a, const Workspace& w, hipStream_t st) {
     launch_k(k_flags, dim3(cdiv(a.N, 256), a.B), dim3(256), 0, st, a, w);
 }
 const char* launch_peaks(const BatchArgs& a, const Workspace& w, int detector_only, hipStream_t st) {
-    const int nch = cdiv(w.W, kPkWords);
-    static_assert(kPkWords == 256, "k_flags clears ceil(W / 256) slots");
-    // k_peaks scores the peaks it writes (scorer.rs:65-75) for the selector
-    launch_k(k_peaks, dim3(nch, a.B), dim3(kPkThreads), 0, st, a, w, detector_only, 1);
-    return "k_flags+k_peaks";
+    // k_peaks scores the peaks it writes (scorer.rs:65-75) for the selector. Fine
+    // chunks while the batch gives fewer than 64 workgroups of 256-word chunks
+    // (B <= 7 at N = 131072); MDG_PEAKS = fine | coarse forces one (tests)
+    const char* force = std::getenv("MDG_PEAKS");
+    const bool fine = force ? std::string(force) == "fine" : (size_t)cdiv(w.W, 256) * a.B < 64;
+    if (fine) {
+        launch_k(k_peaks<64, 256>, dim3(cdiv(w.W, 64), a.B), dim3(256), 0, st, a, w, detector_only, 1);
+        return "k_flags+k_peaks<64>";
+    }
+    launch_k(k_peaks<256, 1024>, dim3(cdiv(w.W, 256), a.B), dim3(1024), 0, st, a, w, detector_only, 1);
+    return "k_flags+k_peaks<256>";
 }
 const char* launch_select(const BatchArgs& a, const Workspace& w, int detector_only,
                           double threshold, hipStream_t st) {

@@ -82,7 +82,7 @@ struct Workspace {
                               // (k_fit_update path: version & 1; fused k_fit_sup_tf: version % 3)
     int32_t* unsafe_kept;     // B: same for the retained Lorentzians
     int32_t* mse_done;        // B: k_mse_local workgroups finished (the last one folds, resets)
-    int32_t* peak_cnt;        // B x ceil(W/256) u64: k_peaks slots {valid, bordered, kept} per mask chunk
+    int32_t* peak_cnt;        // B x ceil(W/64) u64: k_peaks slots {valid, bordered, kept} per mask chunk
     // k_smooth_chain (allocated on first use; null otherwise)
     double* chain_raw;        // P x B x chain_stride: raw running sums of every pass
     double* chain_tmp;        // (P-1) x B x chain_stride: scaled outputs of passes 0..P-2

@@ -409,6 +409,39 @@ def test_deterministic_bits(ctx):
     assert np.array_equal(a[2], b[2]) and a[3][0] == b[3][0]
 
 
+def test_rows_past_counts_untouched(ctx):
+    """mdg_deconvolute_batch writes only rows below counts[i] (mdgpu.h): the result rows
+    come back with a guessed row count (the context's last one), so a call after one
+    with more peaks must leave the caller's rows past its own counts alone."""
+    big = load_case("synth_128k_2k_s1")
+    small = load_case("blood_07")
+    gpu_batch(ctx, big[0], big[1][None, :], [big[2]], big[3])  # a large guess
+    for rows_x, rows_y, sbs, st in (
+            (small[0], small[1][None, :], [small[2]], small[3]),
+            (small[0], np.stack([small[1], small[1] * 1.5, small[1]]), [small[2]] * 3, small[3])):
+        ys = np.ascontiguousarray(rows_y)
+        b, n = ys.shape
+        s = nat.Settings()
+        for f, _ in nat.Settings._fields_:
+            setattr(s, f, getattr(st, f))
+        cap = n // 2 + 2
+        out = np.full((b, cap, 3), 7.25)
+        counts = np.zeros(b, dtype=np.uintp)
+        mse = np.zeros(b)
+        status = np.zeros(b, dtype=np.intc)
+        sbv = np.ascontiguousarray(np.broadcast_to(np.asarray(sbs, dtype=np.float64), (b, 2)))
+        rc = nat.lib().mdg_deconvolute_batch(
+            ctx.handle, b, n, nat.ptr(np.ascontiguousarray(rows_x)), 0, nat.ptr(ys), n, nat.ptr(sbv),
+            ctypes.byref(s), None, 0, nat.ptr(out), cap, nat.ptr(counts, nat._szp), nat.ptr(mse),
+            status.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+        assert rc < 100, nat.strerror(rc)
+        for i in range(b):
+            k = int(counts[i])
+            assert 0 < k < 4000
+            assert not np.any(out[i, :k] == 7.25)
+            assert np.all(out[i, k:] == 7.25), i
+
+
 def test_stage_profiling(ctx):
     ctx.reset_stage_times()
     ctx.set_profiling(True)
@@ -467,6 +500,29 @@ def test_chain_smoother_repeated_launches(ctx, monkeypatch):
 # the library's fit kernels (fit_choice, mdg_kernels.hip); "twf"/"twf1" are the
 # batch-wide tile lists, "twf:5" the same with 5 workgroups (many tiles per workgroup)
 FIT_KERNELS = ["tf", "tw7", "twf", "twf1", "twf:5", "plain"]
+
+
+@pytest.mark.parametrize("mode", ["fine", "coarse"])
+def test_peak_chunkings(ctx, mode, monkeypatch):
+    """k_peaks over 64-word chunks (small batches) and 256-word chunks (large ones),
+    forced by MDG_PEAKS, on a single spectrum and a batch of three: the oracle's
+    results either way (peak lists, scores and the selection behind them)."""
+    monkeypatch.setenv("MDG_PEAKS", mode)
+    for name in ("blood_03", "sim_03"):
+        x, y, sb, st, ign = load_case(name)
+        o = oracle.deconvolute(x, y, sb, st, ignore=ign)
+        status, counts, out, mse = gpu_batch(ctx, x, y[None, :], [sb], st, ignore=ign)
+        assert status[0] == o.status, name
+        assert np.array_equal(out[0, : counts[0]], o.params), name
+    rows, ref = [], []
+    for seed in (6, 7, 8):
+        x, y = synth_spectrum(seed, n=65536, n_peaks=500 + 200 * seed)[:2]
+        rows.append(y)
+        ref.append(oracle.deconvolute(x, y, (11.8, -2.2)))
+    status, counts, out, mse = gpu_batch(ctx, x, np.stack(rows), [(11.8, -2.2)], oracle.default_settings())
+    for s, o in enumerate(ref):
+        assert status[s] == o.status == 0
+        assert np.array_equal(out[s, : counts[s]], o.params), s
 
 
 def _force_fit(monkeypatch, path):

@@ -29,7 +29,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 PROTOCOL_KERNELS = {
     "k_smooth_chain": r"^_ZN3mdg14k_smooth_chainI",
-    "k_peaks": r"^_ZN3mdg7k_peaksE",
+    "k_peaks": r"^_ZN3mdg7k_peaksILi",
     "k_mse_local": r"^_ZN3mdg11k_mse_localI",
 }
 NARROW = re.compile(r"^\s+(s_and_saveexec_b64|s_andn2_saveexec_b64|s_or_saveexec_b64|"

@@ -15,6 +15,8 @@
 #   c4           configs[4] by lanes and hardware queues (bench.py --c4-only)
 #   fitdiag      small-batch fit: PMC passes of tools/blood_trace.py 16 and the stamped
 #                tools/ubench/fit_diag over term-fold shapes (build fit_diag first)
+#   twfdiag      the batch-wide tile-list fit (k_fit_sup_twf) against the (G, B) grids
+#   timeline     rocprofv3 kernel timelines of one blood call at B = 1 and 16
 #   c0diag       configs[0]: host/device breakdown (tools/c0_breakdown.py) and the phase
 #                stamps of one pipeline (tools/stage_diag.py; the diag library first:
 #                make -C metabodecon-rust_amd diag && cp .../build/libmdgpu_diag.so tools/ubench/)
@@ -54,6 +56,17 @@ for step in "$@"; do
       run fit_shapes_b16 120 tools/ubench/fit_diag 16 992 twf,twf1,tw7,s63.1.7@98,s63.2.7@16,s63.2.7@48,s63.1.7@16,s60.1.15@16,s60.1.15@50,s60.2.6@16,s63.2.3@16,s48.1.6@62,s63.1.9@98
       run fit_shapes_b8 120 tools/ubench/fit_diag 8 992 twf,twf1,s63.1.7@98,s63.2.7@32,s63.2.7@48,s60.1.15@32,s60.2.6@32
       run fit_shapes_b1 120 tools/ubench/fit_diag 1 992 twf,twf1,tf,s63.1.7@98,s63.2.7@48,s60.1.15@50 ;;
+    twfdiag)
+      run twf_b16 120 tools/ubench/fit_diag 16 992 tw7,twf,twf1,s63.1.7@98,s63.2.7@16
+      MDG_TW_G=768 run twf_b16_g768 120 tools/ubench/fit_diag 16 992 twf1
+      MDG_TW_G=256 run twf_b16_g256 120 tools/ubench/fit_diag 16 992 twf,twf1
+      MDG_TW_G=48 run twf_b1_g48 120 tools/ubench/fit_diag 1 992 twf,twf1 ;;
+    timeline)
+      for b in 1 16; do
+        run trace_b$b 180 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/bt$b -o run -- python3 tools/blood_trace.py $b
+        f=$(ls gpurun_out/bt$b/*/*/run_kernel_trace.csv 2>/dev/null | head -1)
+        [ -n "$f" ] && run timeline_b$b 60 python tools/blood_trace.py --summary "$f"
+      done ;;
     c0diag)
       run c0_breakdown 300 python tools/c0_breakdown.py 200
       run stage_diag_b1 120 python tools/stage_diag.py 1

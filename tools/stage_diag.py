@@ -28,7 +28,8 @@ out = torch.zeros((B, 4096, 3), dtype=torch.float64, device=dev)
 cnt = torch.zeros(B, dtype=torch.int32, device=dev)
 mse = torch.zeros(B, dtype=torch.float64, device=dev)
 st = torch.zeros(B, dtype=torch.int32, device=dev)
-diag = torch.zeros((1 << 16) + 1024, dtype=torch.int64, device=dev)  # DIAG_FLUSH: [0, 2^16), KSTAMP: 2^16 + slot
+STAMPS = 1 << 22  # kDiagStampBase (mdg_kernels.hip): DIAG_FLUSH records below, KSTAMP slots after
+diag = torch.zeros(STAMPS + 1024, dtype=torch.int64, device=dev)
 assert L.mdg_debug_set_diag(diag.data_ptr()) == 0
 s = nat.default_settings()
 for _ in range(3):
@@ -38,7 +39,7 @@ for _ in range(3):
                                         4096, cnt.data_ptr(), mse.data_ptr(), st.data_ptr())
     assert rc == 0
     torch.cuda.synchronize()
-d = diag.cpu().tolist()[1 << 16:]
+d = diag[STAMPS:].cpu().tolist()
 groups = {"select": range(10, 19), "peaks": range(0, 5), "fit_dpp": range(20, 24),
           "mse": range(30, 34), "window_mean": [45, 46, 40, 41, 42], "window_var": [55, 56, 50, 51, 52]}
 for name, r in groups.items():

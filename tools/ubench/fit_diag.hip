@@ -61,13 +61,19 @@ int main(int argc, char** argv) {
     (void)hipMalloc(&sel, 4 * B); (void)hipMemcpy(sel, selv.data(), 4 * B, hipMemcpyHostToDevice);
     (void)hipMalloc(&xok, 4 * B); (void)hipMemcpy(xok, ones.data(), 4 * B, hipMemcpyHostToDevice);
     (void)hipMalloc(&unsafe, 16 * B); (void)hipMemset(unsafe, 0, 16 * B);
-    const size_t nd = 4096 * 16 * 8;
+    const size_t nd = kDiagStampBase + 1024;  // every DIAG_FLUSH record the guard allows
     (void)hipMalloc(&diag, nd * 8);
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_diag), &diag, sizeof(diag));
     BatchArgs a{}; a.B = B; a.N = N;
     Workspace w{}; w.capD = capD; w.status = status; w.sel_count = sel; w.params = d_par;
     w.rx = d_rx; w.ry = d_ry; w.ratio = d_ratio; w.x_ok = xok; w.unsafe = unsafe;
     w.stencil = d_st; w.fit_iters = 10;
+    {
+        int cus = 0, dev = 0;
+        (void)hipGetDevice(&dev);
+        const hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        printf("device %d: %d CUs (rc %d)\n", dev, cus, (int)e);
+    }
     std::vector<std::string> kinds;
     {
         std::string all = argc > 3 ? argv[3] : "dpp,plain,tf,tf/noeval";
