@@ -1712,53 +1712,64 @@ __device__ __forceinline__ void two_sum(double a, double b, double& s, double& e
     e = (a - (s - bb)) + (b - bb);
 }
 
-// dpp_fold for one window segment (a few hundred terms): groups of 16 terms are
-// loaded 8 groups at a time, the next 8 in flight while the current 8 are folded
-// (dpp_fold's own steady loop starts at 24 groups; below that it waits on every load)
-__device__ __noinline__ double seg_fold(double acc, const double* __restrict__ t, int n) {
-    const int sub = threadIdx.x & 15;
-    const double one = 1.0;
-    const int G = n / 16;
-    double cur[8], nxt[8];
+// The fold of one window segment (a few hundred terms) from 64 candidate start
+// values, one per lane: every lane adds the same terms in the same order, so the
+// terms are wave-uniform and come through the scalar cache into SGPRs (address space
+// 4, as the fit's parameters), and each add is one VOP2 v_fmac_f64 acc, s_term, 1.0:
+// 4.34 cycles per dependent add and 4 of issue, against 7.75 of issue for the DPP
+// broadcast -- the four waves a SIMD holds here share its issue.
+// Groups of 16 terms alternate between two SGPR buffers; a group's successor is
+// loaded behind the group's first add. fma(t, 1, acc) rounds exactly as acc + t.
+// The terms must not have been read through the scalar cache earlier in the launch
+// and written since (k_select folds each term set from its own buffer).
+constexpr int kSegG = 16;
+__device__ __forceinline__ void seg_group(double& acc, const double (&c)[kSegG], double (&nx)[kSegG],
+                                          const_f64_ptr next, bool load_next, double one) {
+    acc = __builtin_fma(c[0], one, acc);
+    __builtin_amdgcn_sched_barrier(0);
+    if (load_next) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) cur[u] = t[min(16 * u + sub, max(n - 1, 0))];
-    for (int g0 = 0; g0 < G; g0 += 8) {
-#pragma unroll
-        for (int u = 0; u < 8; ++u) nxt[u] = t[min(16 * (g0 + 8 + u) + sub, max(n - 1, 0))];
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-            if (g0 + u < G) fold16(acc, cur[u], one);
-#pragma unroll
-        for (int u = 0; u < 8; ++u) cur[u] = nxt[u];
+        for (int k = 0; k < kSegG; ++k) nx[k] = next[k];
     }
-    const int r = n - 16 * G;
-    if (r > 0) {
-        const double v = t[min(16 * G + sub, n - 1)];
-        for (int k = 0; k < r; ++k) acc += readlane_f64(v, k);
+#pragma unroll
+    for (int k = 1; k < kSegG; ++k) acc = __builtin_fma(c[k], one, acc);
+}
+__device__ __noinline__ double seg_fold(double acc, const double* tg, int n) {
+    // the address and count are wave-uniform; a call passes them in VGPRs, so say so
+    const unsigned long long ta = (unsigned long long)tg;
+    const const_f64_ptr t = (const_f64_ptr)(((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane(
+                                                 (int)(ta >> 32)) << 32) |
+                                             (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)ta));
+    n = __builtin_amdgcn_readfirstlane(n);
+    double one = 1.0;
+    asm volatile("" : "+v"(one));  // a VGPR operand: v_fmac_f64, not folded into an add
+    const int G = n / kSegG;
+    int g = 0;
+    if (G > 0) {
+        double A[kSegG], Bf[kSegG];
+#pragma unroll
+        for (int k = 0; k < kSegG; ++k) A[k] = t[k];
+        for (; g + 2 < G; g += 2) {
+            seg_group(acc, A, Bf, t + kSegG * (g + 1), true, one);
+            seg_group(acc, Bf, A, t + kSegG * (g + 2), true, one);
+        }
+        if (g + 1 < G) {
+            seg_group(acc, A, Bf, t + kSegG * (g + 1), true, one);
+            seg_group(acc, Bf, A, t, false, one);
+        } else {
+            seg_group(acc, A, Bf, t, false, one);
+        }
     }
+    for (int k = kSegG * G; k < n; ++k) acc = __builtin_fma(t[k], one, acc);
     return acc;
 }
 
-// the same fold on terms staged in LDS: every lane reads each term from the same LDS
-// address (a broadcast read, no bank conflict) and adds it with a plain VOP2 fma --
-// no DPP: the term is already in every lane
+// t: the terms in global memory (stages B and C read them through the scalar cache);
+// tl, when LA: the same terms in LDS, for stage A's vector reads
 typedef const __attribute__((address_space(3))) double* lds_f64_ptr;
-__device__ __forceinline__ double seg_fold(double acc, lds_f64_ptr t, int n) {
-    int k = 0;
-    for (; k + 8 <= n; k += 8) {
-        double v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = t[k + u];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) acc = __builtin_fma(v[u], 1.0, acc);
-    }
-    for (; k < n; ++k) acc = __builtin_fma(t[k], 1.0, acc);
-    return acc;
-}
-
-// t: global terms (const double*) or LDS terms (lds_f64_ptr)
-template <int BS, typename TP>
-__device__ double window_fold(double acc0, WinLds& L, TP t, int n, int stamp = 40) {
+template <int BS, bool LA>
+__device__ double window_fold(double acc0, WinLds& L, const double* t, lds_f64_ptr tl, int n,
+                              int stamp = 40) {
     constexpr int NW = BS / 64;
     static_assert(kWinSeg <= 64, "one lane per segment in the prefix scan");
     KSTAMP(stamp + 5);
@@ -1774,7 +1785,7 @@ __device__ double window_fold(double acc0, WinLds& L, TP t, int n, int stamp = 4
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 const int i = c + 64 * u + lane;
-                v[u] = i < i1 ? t[i] : 0.0;
+                v[u] = i < i1 ? (LA ? tl[i] : t[i]) : 0.0;
             }
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
@@ -1869,7 +1880,7 @@ __device__ double window_fold(double acc0, WinLds& L, TP t, int n, int stamp = 4
 __global__ __launch_bounds__(1024) void k_ordered_sum(const double* __restrict__ t, int n, double acc0,
                                                       double* out) {
     __shared__ WinLds wl;
-    const double r = window_fold<1024>(acc0, wl, t, n);
+    const double r = window_fold<1024, false>(acc0, wl, t, nullptr, n);
     if (threadIdx.x == 0) out[0] = r;
 }
 void launch_ordered_sum(const double* t, int n, double acc0, double* out, hipStream_t st) {
@@ -2040,37 +2051,43 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
     // scores and squared deviations are >= +0: the windowed fold applies (one wave
     // folds short sets itself)
     const bool win = n_sfr >= 4 * kWinSeg;
-    // staged in LDS when they fit (the folds' loads are then LDS reads, not L2
-    // round trips); the short-set dpp_fold below stays off its asm global-load loop
-    // (n_sfr < 4 * kWinSeg, far below its 24-group threshold)
+    // The scores go to the workspace (tmp0: the folds' scalar loads) and, when they
+    // fit, to LDS too (stage A's vector reads); the squared deviations to tmp1 (never
+    // read through the scalar cache before in this launch) and in place in LDS
     const bool staged = n_sfr <= kSfrLds;
-    double* sfr = staged ? sfr_lds : w.tmp0 + (size_t)s * a.N;
-    for (int k = threadIdx.x; k < n_sfr; k += BS) sfr[k] = scores[k < left ? k : right + (k - left)];
+    double* sfr_g = w.tmp0 + (size_t)s * a.N;
+    double* sq_g = w.tmp1 + (size_t)s * a.N;
+    for (int k = threadIdx.x; k < n_sfr; k += BS) {
+        const double v = scores[k < left ? k : right + (k - left)];
+        sfr_g[k] = v;
+        if (staged) sfr_lds[k] = v;
+    }
     __syncthreads();
     KSTAMP(15);
     // every thread calls window_fold (barriers inside)
-    auto wfold = [&](int stamp) {
-        return staged ? window_fold<BS>(-0.0, wl, (lds_f64_ptr)sfr_lds, n_sfr, stamp)
-                      : window_fold<BS>(-0.0, wl, (const double*)sfr, n_sfr, stamp);
+    auto wfold = [&](const double* tg, int stamp) {
+        return staged ? window_fold<BS, true>(-0.0, wl, tg, (lds_f64_ptr)sfr_lds, n_sfr, stamp)
+                      : window_fold<BS, false>(-0.0, wl, tg, nullptr, n_sfr, stamp);
     };
     if (win) {
-        const double sum = wfold(40);
+        const double sum = wfold(sfr_g, 40);
         if (threadIdx.x == 0) thr_sh = sum / (double)n_sfr;
     } else if (threadIdx.x < 64) {
-        const double mean = dpp_fold(-0.0, sfr, n_sfr) / (double)n_sfr;
+        const double mean = dpp_fold(-0.0, sfr_g, n_sfr) / (double)n_sfr;
         if (threadIdx.x == 0) thr_sh = mean;
     }
     __syncthreads();
     KSTAMP(16);
     const double mean = thr_sh;
     for (int k = threadIdx.x; k < n_sfr; k += BS) {
-        const double d = sfr[k] - mean;
-        sfr[k] = d * d;
+        const double d = (staged ? sfr_lds[k] : sfr_g[k]) - mean;
+        sq_g[k] = d * d;
+        if (staged) sfr_lds[k] = d * d;
     }
     __syncthreads();
     double var = 0.0;
-    if (win) var = wfold(50) / (double)n_sfr;
-    else if (threadIdx.x < 64) var = dpp_fold(-0.0, sfr, n_sfr) / (double)n_sfr;
+    if (win) var = wfold(sq_g, 50) / (double)n_sfr;
+    else if (threadIdx.x < 64) var = dpp_fold(-0.0, sq_g, n_sfr) / (double)n_sfr;
     KSTAMP(17);
     if (threadIdx.x == 0) {
         const double sd = __builtin_sqrt(var);
@@ -2389,10 +2406,20 @@ __global__ __launch_bounds__(64 * (kTfEW + 1)) void k_fit_sup_tf(BatchArgs a, Wo
 // in k_fit_sup_tf, so the sums are the same left folds, bit for bit. A spectrum
 // needs 98 workgroups instead of 256 at P = 2048: the same latency on fewer CUs,
 // which is what concurrent pipelines need.
-template <int Q, int PB, int PS>
+//
+// SB (single buffer): one LDS chunk buffer instead of two, half the LDS (33 KB at
+// Q = 63), so four workgroups fit a CU where two did. The evaluators compute chunk
+// c + 1 into registers while the fold wave reads chunk c, wait for it to finish,
+// store, and release it (two barriers per chunk instead of one). With three
+// evaluator waves a workgroup is four waves, and four of them -- 16 waves, VGPRs
+// for 4 per SIMD -- make 1024 tile slots: a B = 16 batch of ~1000-peak spectra
+// (768 tiles) runs in one round instead of 1.5.
+template <int Q_, int PB, int PS, bool SB_ = false>
 struct TwShape {
+    static constexpr int Q = Q_;
+    static constexpr bool SB = SB_;
     static constexpr int EW = PB * PS, J = 64 * PB, RS = J + kTfPad, QS = Q / PS;
-    static constexpr int LDS = 2 * Q * RS;
+    static constexpr int LDS = (SB ? 1 : 2) * Q * RS;
     static_assert(Q % 3 == 0 && Q / 3 <= 64 && Q <= 64 && Q % PS == 0, "tile shape");
 };
 
@@ -2400,7 +2427,7 @@ struct TwShape {
 template <bool FAST, class SH>
 __device__ __forceinline__ void fit_tw_body(const Workspace& w, int s, int P, int it, double* T,
                                             int tile0, int tstep) {
-    constexpr int QQ = SH::LDS / (2 * SH::RS), EW = SH::EW, J = SH::J, RS = SH::RS, QS = SH::QS;
+    constexpr int QQ = SH::Q, EW = SH::EW, J = SH::J, RS = SH::RS, QS = SH::QS;
     constexpr int PB = J / 64;
     const size_t base = (size_t)s * w.capD;
     const int npts = 3 * P;
@@ -2434,6 +2461,30 @@ __device__ __forceinline__ void fit_tw_body(const Workspace& w, int s, int P, in
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::"v"(f), "v"(h), "v"(m), "s"(xq[0]));
             DIAG_STAMP(5);
 #endif
+            if constexpr (SH::SB) {
+                // chunk c into registers while the fold wave reads chunk c - 1; then
+                // A: it has finished, store; B: chunk c is in LDS
+                double* Tb = T + ps * QS * RS + jl;
+                for (int c = 0; c < nch; ++c) {
+                    const double cf = f, ch = h, cm = m;
+                    j = min((c + 1) * J + jl, P - 1);
+                    f = params[3 * j];
+                    h = params[3 * j + 1];
+                    m = params[3 * j + 2];
+                    double tv[QS];
+#pragma unroll
+                    for (int q = 0; q < QS; ++q) tv[q] = lorentz_t<FAST>(xq[q], cf, ch, cm);
+                    DIAG_STAMP(0);
+                    lds_barrier();  // A
+                    DIAG_STAMP(1);
+#pragma unroll
+                    for (int q = 0; q < QS; ++q) Tb[q * RS] = tv[q];
+                    lds_barrier();  // B
+                    DIAG_STAMP(1);
+                }
+                lds_barrier();  // A: the fold wave has read the last chunk
+                DIAG_STAMP(1);
+            } else
             for (int c = 0; c <= nch; ++c) {
                 if (c < nch) {
                     double* Tb = T + (c & 1) * QQ * RS + ps * QS * RS + jl;
@@ -2465,10 +2516,15 @@ __device__ __forceinline__ void fit_tw_body(const Workspace& w, int s, int P, in
             const double s0 = stq[0], s1 = stq[1], s2 = stq[2], s3 = stq[3], s4 = stq[4], s5 = stq[5];
             double one = 1.0;
             asm volatile("" : "+v"(one));
-            lds_barrier();  // chunk 0 written
+            if constexpr (!SH::SB) lds_barrier();  // chunk 0 written
             DIAG_STAMP(6);
             for (int c = 0; c < nch; ++c) {
-                const double2* row = (const double2*)(T + (c & 1) * QQ * RS + q * RS);
+                if constexpr (SH::SB) {
+                    lds_barrier();  // A
+                    lds_barrier();  // B: chunk c written
+                    DIAG_STAMP(3);
+                }
+                const double2* row = (const double2*)(T + (SH::SB ? 0 : (c & 1) * QQ * RS) + q * RS);
                 const int cn = min(J, P - c * J);
                 if (cn == J) {
 #pragma unroll 16
@@ -2482,7 +2538,13 @@ __device__ __forceinline__ void fit_tw_body(const Workspace& w, int s, int P, in
                     for (int k = 0; k < cn; ++k) acc = __builtin_fma(r1[k], one, acc);
                 }
                 DIAG_STAMP(2);
-                lds_barrier();
+                if constexpr (!SH::SB) {
+                    lds_barrier();
+                    DIAG_STAMP(3);
+                }
+            }
+            if constexpr (SH::SB) {
+                lds_barrier();  // A: the evaluators may refill the buffer
                 DIAG_STAMP(3);
             }
             // stencil update of the tile's peaks: lane k gathers the ratios y/sup of
@@ -2536,7 +2598,7 @@ __global__ __launch_bounds__(64 * (SH::EW + 1)) void k_fit_sup_twf(BatchArgs a, 
     __shared__ int first[kTwfMaxB + 1];  // first list item of spectrum s; first[B] = items
     __shared__ int pk[kTwfMaxB];         // peaks of spectrum s
     __shared__ int fastf[kTwfMaxB];
-    constexpr int QQ = SH::LDS / (2 * SH::RS);
+    constexpr int QQ = SH::Q;
     if (threadIdx.x < 64) {
         const int s = threadIdx.x;
         int tiles = 0, P = 0, fast = 0;
@@ -3407,7 +3469,8 @@ const char* launch_select(const BatchArgs& a, const Workspace& w, int detector_o
 static std::string fit_choice(const BatchArgs& a) {
     if (const char* force = std::getenv("MDG_FITSUP")) {
         const std::string f(force);
-        if (f == "tf" || f == "tw7" || f == "twf" || f == "twf1" || f == "plain") return f;
+        if (f == "tf" || f == "tw7" || f == "tw3s" || f == "twf" || f == "twf1" || f == "twf3s" || f == "plain")
+            return f;
     }
     if (a.B == 1 && a.contexts > 1) return "tw7";
     return a.B <= 2 ? "tf" : a.B <= 24 ? "tw7" : "plain";
@@ -3425,7 +3488,14 @@ const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int i
         launch_k(k_fit_sup_tw<SH>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
         return "k_fit_sup_tw<63, 1, 7>";
     }
-    if ((f == "twf" || f == "twf1") && a.B <= kTwfMaxB) {
+    if (f == "tw3s") {
+        // single-buffered 63-point tiles, 3 evaluator waves: four workgroups per CU
+        using SH = TwShape<63, 1, 3, true>;
+        const int g = tg ? std::max(1, std::atoi(tg)) : (3 * 2048 + 62) / 63;
+        launch_k(k_fit_sup_tw<SH>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
+        return "k_fit_sup_tw<63, 1, 3, SB>";
+    }
+    if ((f == "twf" || f == "twf1" || f == "twf3s") && a.B <= kTwfMaxB) {
         // one list of the batch's tiles over about one workgroup per slot: <63, 2, 7>
         // (15 waves, 131 KB of LDS) one per CU, <63, 1, 7> (8 waves, 66 KB) two
         static int cus = 0;
@@ -3434,6 +3504,12 @@ const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int i
             (void)hipGetDevice(&dev);
             if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
                 cus = 256;
+        }
+        if (f == "twf3s") {
+            using SH = TwShape<63, 1, 3, true>;
+            const int g = tg ? std::max(1, std::atoi(tg)) : 4 * cus;
+            launch_k(k_fit_sup_twf<SH>, dim3(g), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
+            return "k_fit_sup_twf<63, 1, 3, SB>";
         }
         if (f == "twf") {
             using SH = TwShape<63, 2, 7>;
@@ -3446,7 +3522,7 @@ const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int i
         launch_k(k_fit_sup_twf<SH>, dim3(g), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
         return "k_fit_sup_twf<63, 1, 7>";
     }
-    if (f == "tf" || f == "twf" || f == "twf1") {
+    if (f == "tf" || f == "twf" || f == "twf1" || f == "twf3s") {
         // 24 points per workgroup: one workgroup per tile of a 2048-peak spectrum (256)
         const int g = tg ? std::max(1, std::atoi(tg)) : (3 * 2048 + 23) / 24;
         launch_k(k_fit_sup_tf, dim3(g, a.B), dim3(64 * (kTfEW + 1)), 0, st, a, w, it);

@@ -497,9 +497,9 @@ def test_chain_smoother_repeated_launches(ctx, monkeypatch):
             assert np.array_equal(row, oracle.moving_average(ys[s], 3, 3)), (rep, s)
 
 
-# the library's fit kernels (fit_choice, mdg_kernels.hip); "twf"/"twf1" are the
-# batch-wide tile lists, "twf:5" the same with 5 workgroups (many tiles per workgroup)
-FIT_KERNELS = ["tf", "tw7", "twf", "twf1", "twf:5", "plain"]
+# the library's fit kernels (fit_choice, mdg_kernels.hip); "twf*" are the batch-wide
+# tile lists, "tw3s"/"twf3s" single-buffered; ":G" = G workgroups (many tiles each)
+FIT_KERNELS = ["tf", "tw7", "tw3s", "twf", "twf1", "twf3s", "twf:5", "twf3s:7", "plain"]
 
 
 @pytest.mark.parametrize("mode", ["fine", "coarse"])

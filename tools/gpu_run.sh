@@ -44,7 +44,10 @@ for step in "$@"; do
     default) run default 600 python bench.py ;;
     forcedist) run forcedist 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
         --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 1 --force-dist --steps 4 --warmup 1 --no-cpu-baseline ;;
-    prof) run prof_all 1200 bash tools/prof_all.sh ;;
+    prof) run prof_all 1200 bash tools/prof_all.sh
+      f=$(ls gpurun_out/prof_q256/*/*/run_kernel_trace.csv 2>/dev/null | head -1)
+      [ -n "$f" ] && run alone_q256 60 python tools/alone_kernels.py "$f" --out gpurun_out/bench_alone_q256.json \
+          --command "rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu-baseline --no-configs --steps 6 --warmup 2 --verify 0" ;;
     c4)
       cfgs=()
       for q in 4 32; do for l in 1 2 3 4 8 16; do
@@ -57,15 +60,24 @@ for step in "$@"; do
       run fit_shapes_b8 120 tools/ubench/fit_diag 8 992 twf,twf1,s63.1.7@98,s63.2.7@32,s63.2.7@48,s60.1.15@32,s60.2.6@32
       run fit_shapes_b1 120 tools/ubench/fit_diag 1 992 twf,twf1,tf,s63.1.7@98,s63.2.7@48,s60.1.15@50 ;;
     twfdiag)
-      run twf_b16 120 tools/ubench/fit_diag 16 992 tw7,twf,twf1,s63.1.7@98,s63.2.7@16
+      run twf_b16 120 tools/ubench/fit_diag 16 992 tw7,twf,twf1,tw3s,twf3s,s63.1.7@98,s63.2.7@16,S63.1.3@98,S63.1.3@48,S63.1.7@98,S63.2.3@98
+      run twf_b8 120 tools/ubench/fit_diag 8 992 tw7,tw3s,twf3s,S63.1.3@98
+      run twf_b1 120 tools/ubench/fit_diag 1 992 tf,tw7,tw3s,twf3s,S63.1.3@98
       MDG_TW_G=768 run twf_b16_g768 120 tools/ubench/fit_diag 16 992 twf1
       MDG_TW_G=256 run twf_b16_g256 120 tools/ubench/fit_diag 16 992 twf,twf1
       MDG_TW_G=48 run twf_b1_g48 120 tools/ubench/fit_diag 1 992 twf,twf1 ;;
-    timeline)
+    timeline|timeline:*)
+      # timeline:<fit kernel> forces MDG_FITSUP for the B = 16 trace
+      fk=${step#timeline}; fk=${fk#:}
       for b in 1 16; do
-        run trace_b$b 180 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/bt$b -o run -- python3 tools/blood_trace.py $b
-        f=$(ls gpurun_out/bt$b/*/*/run_kernel_trace.csv 2>/dev/null | head -1)
-        [ -n "$f" ] && run timeline_b$b 60 python tools/blood_trace.py --summary "$f"
+        tag=bt$b${fk:+_$fk}
+        if [ $b = 16 ] && [ -n "$fk" ]; then
+          MDG_FITSUP=$fk run trace_$tag 180 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/$tag -o run -- python3 tools/blood_trace.py $b
+        else
+          run trace_$tag 180 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/$tag -o run -- python3 tools/blood_trace.py $b
+        fi
+        f=$(find gpurun_out/$tag -name run_kernel_trace.csv | head -1)
+        [ -n "$f" ] && run timeline_$tag 60 python tools/blood_trace.py --summary "$f"
       done ;;
     c0diag)
       run c0_breakdown 300 python tools/c0_breakdown.py 200

@@ -1,7 +1,8 @@
 // Phase breakdown and timing of the fit-superposition kernels on synthetic peak
 // tables (P peaks, 3P reduced points per spectrum): builds the library kernel source
 // with -DMDG_DIAG. usage: fit_diag [B] [P] [kinds, comma-separated; MDG_FITSUP names,
-// '/noeval' suffix = tf without evaluation; "sQ.PB.PS@G" = the term fold
+// '/noeval' suffix = tf without evaluation; "sQ.PB.PS@G" ("SQ.PB.PS@G": single
+// buffer) = the term fold
 // k_fit_sup_tw<TwShape<Q, PB, PS>> on a (G, B) grid, for the shapes listed in
 // launch_shape (experiments: G workgroups per spectrum, tiles grid-strided)]
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -DMDG_DIAG \
@@ -13,13 +14,19 @@
 using namespace mdg;
 
 // experimental term-fold shapes (not in the library): returns EW, or 0 if unknown
-template <int Q, int PB, int PS>
+template <int Q, int PB, int PS, bool SB = false>
 static int launch_one(const BatchArgs& a, const Workspace& w, int g) {
-    using SH = TwShape<Q, PB, PS>;
+    using SH = TwShape<Q, PB, PS, SB>;
     hipLaunchKernelGGL((k_fit_sup_tw<SH>), dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, 0, a, w, 0);
     return SH::EW;
 }
-static int launch_shape(int q, int pb, int ps, const BatchArgs& a, const Workspace& w, int g) {
+static int launch_shape(int q, int pb, int ps, const BatchArgs& a, const Workspace& w, int g, bool sb) {
+    if (sb) {  // "Sq.pb.ps@g": single-buffered
+        if (q == 63 && pb == 1 && ps == 3) return launch_one<63, 1, 3, true>(a, w, g);
+        if (q == 63 && pb == 1 && ps == 7) return launch_one<63, 1, 7, true>(a, w, g);
+        if (q == 63 && pb == 2 && ps == 3) return launch_one<63, 2, 3, true>(a, w, g);
+        return 0;
+    }
     if (q == 63 && pb == 1 && ps == 7) return launch_one<63, 1, 7>(a, w, g);
     if (q == 63 && pb == 2 && ps == 7) return launch_one<63, 2, 7>(a, w, g);
     if (q == 63 && pb == 1 && ps == 3) return launch_one<63, 1, 3>(a, w, g);
@@ -91,7 +98,8 @@ int main(int argc, char** argv) {
         const int mode = ks.find("/nostore") != std::string::npos ? 1 : ks.find("/noeval") != std::string::npos ? 2 : 0;
         (void)hipMemcpyToSymbol(HIP_SYMBOL(g_tf_mode), &mode, sizeof(mode));
         int sq = 0, spb = 0, sps = 0, sg = 0;
-        const bool shape = ks[0] == 's' && sscanf(k, "s%d.%d.%d@%d", &sq, &spb, &sps, &sg) == 4;
+        const bool sbuf = ks[0] == 'S';
+        const bool shape = (ks[0] == 's' || sbuf) && sscanf(k + 1, "%d.%d.%d@%d", &sq, &spb, &sps, &sg) == 4;
         setenv("MDG_FITSUP", shape ? "tw7" : ks.substr(0, ks.find('/')).c_str(), 1);
         w.params_alt = fit_sup_fused(a) ? d_alt : nullptr;
         float best = 1e30f;
@@ -100,7 +108,7 @@ int main(int argc, char** argv) {
             (void)hipMemset(diag, 0, nd * 8);
             hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
             (void)hipEventRecord(e0);
-            if (shape) shape_ew = launch_shape(sq, spb, sps, a, w, sg);
+            if (shape) shape_ew = launch_shape(sq, spb, sps, a, w, sg, sbuf);
             else launch_fit_sup(a, w, 24, 0, 0);
             (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
             float ms; (void)hipEventElapsedTime(&ms, e0, e1);
