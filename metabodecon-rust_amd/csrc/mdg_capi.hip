@@ -982,7 +982,7 @@ int run_pipeline_graphed(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     // the kernel-choice overrides (tests, diagnostics) select other kernels, so
     // they are part of the key too
     std::string envs;
-    for (const char* e : {"MDG_SMOOTH", "MDG_CHAIN_EXCL", "MDG_FITSUP", "MDG_GFIT", "MDG_TW_G", "MDG_PEAKS", "MDG_MSE_NEARCAP",
+    for (const char* e : {"MDG_SMOOTH", "MDG_CHAIN_EXCL", "MDG_FITSUP", "MDG_GFIT", "MDG_TW_G", "MDG_PEAKS", "MDG_MSE_NEARCAP", "MDG_MSE_NPT", "MDG_MSE_PARTS",
                           "MDG_DIAG_SKIP", "MDG_DIAG_DUP", "MDG_DIAG_PAD", "MDG_DIAG_PAD_SMALL", "MDG_PREP"}) {
         const char* v = std::getenv(e);
         envs += v ? v : "\x01";

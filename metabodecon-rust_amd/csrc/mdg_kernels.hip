@@ -1712,63 +1712,37 @@ __device__ __forceinline__ void two_sum(double a, double b, double& s, double& e
     e = (a - (s - bb)) + (b - bb);
 }
 
-// The fold of one window segment (a few hundred terms) from 64 candidate start
-// values, one per lane: every lane adds the same terms in the same order, so the
-// terms are wave-uniform and come through the scalar cache into SGPRs (address space
-// 4, as the fit's parameters), and each add is one VOP2 v_fmac_f64 acc, s_term, 1.0:
-// 4.34 cycles per dependent add and 4 of issue, against 7.75 of issue for the DPP
-// broadcast -- the four waves a SIMD holds here share its issue.
-// Groups of 16 terms alternate between two SGPR buffers; a group's successor is
-// loaded behind the group's first add. fma(t, 1, acc) rounds exactly as acc + t.
-// The terms must not have been read through the scalar cache earlier in the launch
-// and written since (k_select folds each term set from its own buffer).
-constexpr int kSegG = 16;
-__device__ __forceinline__ void seg_group(double& acc, const double (&c)[kSegG], double (&nx)[kSegG],
-                                          const_f64_ptr next, bool load_next, double one) {
-    acc = __builtin_fma(c[0], one, acc);
-    __builtin_amdgcn_sched_barrier(0);
-    if (load_next) {
+// dpp_fold for one window segment (a few hundred terms): groups of 16 terms are
+// loaded 8 groups at a time, the next 8 in flight while the current 8 are folded
+// (dpp_fold's own steady loop starts at 24 groups; below that it waits on every load)
+__device__ __noinline__ double seg_fold(double acc, const double* __restrict__ t, int n) {
+    const int sub = threadIdx.x & 15;
+    const double one = 1.0;
+    const int G = n / 16;
+    double cur[8], nxt[8];
 #pragma unroll
-        for (int k = 0; k < kSegG; ++k) nx[k] = next[k];
+    for (int u = 0; u < 8; ++u) cur[u] = t[min(16 * u + sub, max(n - 1, 0))];
+    for (int g0 = 0; g0 < G; g0 += 8) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) nxt[u] = t[min(16 * (g0 + 8 + u) + sub, max(n - 1, 0))];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (g0 + u < G) fold16(acc, cur[u], one);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) cur[u] = nxt[u];
     }
-#pragma unroll
-    for (int k = 1; k < kSegG; ++k) acc = __builtin_fma(c[k], one, acc);
-}
-__device__ __noinline__ double seg_fold(double acc, const double* tg, int n) {
-    // the address and count are wave-uniform; a call passes them in VGPRs, so say so
-    const unsigned long long ta = (unsigned long long)tg;
-    const const_f64_ptr t = (const_f64_ptr)(((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane(
-                                                 (int)(ta >> 32)) << 32) |
-                                             (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)ta));
-    n = __builtin_amdgcn_readfirstlane(n);
-    double one = 1.0;
-    asm volatile("" : "+v"(one));  // a VGPR operand: v_fmac_f64, not folded into an add
-    const int G = n / kSegG;
-    int g = 0;
-    if (G > 0) {
-        double A[kSegG], Bf[kSegG];
-#pragma unroll
-        for (int k = 0; k < kSegG; ++k) A[k] = t[k];
-        for (; g + 2 < G; g += 2) {
-            seg_group(acc, A, Bf, t + kSegG * (g + 1), true, one);
-            seg_group(acc, Bf, A, t + kSegG * (g + 2), true, one);
-        }
-        if (g + 1 < G) {
-            seg_group(acc, A, Bf, t + kSegG * (g + 1), true, one);
-            seg_group(acc, Bf, A, t, false, one);
-        } else {
-            seg_group(acc, A, Bf, t, false, one);
-        }
+    const int r = n - 16 * G;
+    if (r > 0) {
+        const double v = t[min(16 * G + sub, n - 1)];
+        for (int k = 0; k < r; ++k) acc += readlane_f64(v, k);
     }
-    for (int k = kSegG * G; k < n; ++k) acc = __builtin_fma(t[k], one, acc);
     return acc;
 }
 
-// t: the terms in global memory (stages B and C read them through the scalar cache);
-// tl, when LA: the same terms in LDS, for stage A's vector reads
-typedef const __attribute__((address_space(3))) double* lds_f64_ptr;
-template <int BS, bool LA>
-__device__ double window_fold(double acc0, WinLds& L, const double* t, lds_f64_ptr tl, int n,
+// t: global memory or LDS (a generic pointer: the windowed fold of k_select reads its
+// LDS-staged terms through it)
+template <int BS>
+__device__ double window_fold(double acc0, WinLds& L, const double* __restrict__ t, int n,
                               int stamp = 40) {
     constexpr int NW = BS / 64;
     static_assert(kWinSeg <= 64, "one lane per segment in the prefix scan");
@@ -1785,7 +1759,7 @@ __device__ double window_fold(double acc0, WinLds& L, const double* t, lds_f64_p
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 const int i = c + 64 * u + lane;
-                v[u] = i < i1 ? (LA ? tl[i] : t[i]) : 0.0;
+                v[u] = i < i1 ? t[i] : 0.0;
             }
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
@@ -1880,7 +1854,7 @@ __device__ double window_fold(double acc0, WinLds& L, const double* t, lds_f64_p
 __global__ __launch_bounds__(1024) void k_ordered_sum(const double* __restrict__ t, int n, double acc0,
                                                       double* out) {
     __shared__ WinLds wl;
-    const double r = window_fold<1024, false>(acc0, wl, t, nullptr, n);
+    const double r = window_fold<1024>(acc0, wl, t, n);
     if (threadIdx.x == 0) out[0] = r;
 }
 void launch_ordered_sum(const double* t, int n, double acc0, double* out, hipStream_t st) {
@@ -1950,7 +1924,7 @@ __device__ __forceinline__ void fit_init_pair(const BatchArgs& a, const Workspac
 // through the workspace), reused afterwards for the selected peaks (up to kSelLds)
 constexpr int kSfrLds = 12288;         // 96 KB
 constexpr int kSelLds = 4096;          // 3 ints each: 48 KB of the same buffer
-constexpr int kSelCountDirect = 8;     // centers per thread counted directly
+constexpr int kSelCountDirect = 16;    // centers per thread counted directly (P <= 16384)
 static_assert(3 * kSelLds * sizeof(int) <= kSfrLds * sizeof(double), "selection fits the SFR buffer");
 template <int BS>
 __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double threshold) {
@@ -2051,43 +2025,32 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
     // scores and squared deviations are >= +0: the windowed fold applies (one wave
     // folds short sets itself)
     const bool win = n_sfr >= 4 * kWinSeg;
-    // The scores go to the workspace (tmp0: the folds' scalar loads) and, when they
-    // fit, to LDS too (stage A's vector reads); the squared deviations to tmp1 (never
-    // read through the scalar cache before in this launch) and in place in LDS
-    const bool staged = n_sfr <= kSfrLds;
-    double* sfr_g = w.tmp0 + (size_t)s * a.N;
-    double* sq_g = w.tmp1 + (size_t)s * a.N;
-    for (int k = threadIdx.x; k < n_sfr; k += BS) {
-        const double v = scores[k < left ? k : right + (k - left)];
-        sfr_g[k] = v;
-        if (staged) sfr_lds[k] = v;
-    }
+    // staged in LDS when they fit (the folds' loads are then LDS reads, not L2 round
+    // trips; the windowed fold's DPP segment folds measured 18.4k cycles against 29k
+    // with scalar-loaded terms and 38k with LDS broadcast reads, blood_01, round 4);
+    // the short-set dpp_fold stays off its asm global-load loop (n_sfr < 4 * kWinSeg)
+    double* sfr = n_sfr <= kSfrLds ? sfr_lds : w.tmp0 + (size_t)s * a.N;
+    for (int k = threadIdx.x; k < n_sfr; k += BS) sfr[k] = scores[k < left ? k : right + (k - left)];
     __syncthreads();
     KSTAMP(15);
-    // every thread calls window_fold (barriers inside)
-    auto wfold = [&](const double* tg, int stamp) {
-        return staged ? window_fold<BS, true>(-0.0, wl, tg, (lds_f64_ptr)sfr_lds, n_sfr, stamp)
-                      : window_fold<BS, false>(-0.0, wl, tg, nullptr, n_sfr, stamp);
-    };
     if (win) {
-        const double sum = wfold(sfr_g, 40);
+        const double sum = window_fold<BS>(-0.0, wl, sfr, n_sfr);  // every thread: barriers inside
         if (threadIdx.x == 0) thr_sh = sum / (double)n_sfr;
     } else if (threadIdx.x < 64) {
-        const double mean = dpp_fold(-0.0, sfr_g, n_sfr) / (double)n_sfr;
+        const double mean = dpp_fold(-0.0, sfr, n_sfr) / (double)n_sfr;
         if (threadIdx.x == 0) thr_sh = mean;
     }
     __syncthreads();
     KSTAMP(16);
     const double mean = thr_sh;
     for (int k = threadIdx.x; k < n_sfr; k += BS) {
-        const double d = (staged ? sfr_lds[k] : sfr_g[k]) - mean;
-        sq_g[k] = d * d;
-        if (staged) sfr_lds[k] = d * d;
+        const double d = sfr[k] - mean;
+        sfr[k] = d * d;
     }
     __syncthreads();
     double var = 0.0;
-    if (win) var = wfold(sq_g, 50) / (double)n_sfr;
-    else if (threadIdx.x < 64) var = dpp_fold(-0.0, sq_g, n_sfr) / (double)n_sfr;
+    if (win) var = window_fold<BS>(-0.0, wl, sfr, n_sfr, 50) / (double)n_sfr;
+    else if (threadIdx.x < 64) var = dpp_fold(-0.0, sfr, n_sfr) / (double)n_sfr;
     KSTAMP(17);
     if (threadIdx.x == 0) {
         const double sd = __builtin_sqrt(var);
@@ -3454,18 +3417,17 @@ const char* launch_select(const BatchArgs& a, const Workspace& w, int detector_o
     launch_k(k_select<1024>, dim3(a.B), dim3(1024), 0, st, a, w, threshold);
     return "k_select<1024>";
 }
-// Fit kernel choice by batch size, fit time per spectrum alone: B <= 2
-// the 24-point term fold over one workgroup per tile ("tf": 212 / 149 us at B = 1 /
-// 2, latency 0.88 ms at B = 1 against 0.95 for "tw7"); B <= 24 the 63-point term
-// fold over one workgroup per tile ("tw7": 120 / 113 / 93 us at B = 4 / 8 / 16);
-// beyond, one point per lane with the update separate ("plain": 79 / 57 us at B =
-// 32 / 256). When other engine contexts on the device have run pipelines, B = 1
-// keeps "tw7": "tf"'s lead alone is gone as soon as a second context has been used
-// (latency 0.95 ms either way), and 18 concurrent B = 1 pipelines run 6.6k
-// spectra/s with "tf" against 7.8-8.1k with "tw7". The kernels measured and
-// rejected in rounds 2-3 are not in the library. MDG_FITSUP = tf |
-// tw7 | plain forces one of the three (all bit-identical; tests, measurements);
-// any other value is ignored.
+// Fit kernel choice by batch size. B <= 4: the 24-point term fold
+// over one workgroup per tile ("tf"); B <= 24: the 63-point term fold over one
+// batch-wide tile list on two workgroups per CU ("twf1"; blood set, ten launches:
+// 373 us at B = 16 against 403 for the (98, B) grid "tw7", 270 / 268 at B = 8, 204
+// against tf's 185 at B = 4); beyond, one point per lane with the update separate
+// ("plain": 79 / 57 us per spectrum at B = 32 / 256). When other engine contexts on
+// the device have run pipelines, B = 1 keeps "tw7": "tf"'s lead alone is gone as
+// soon as a second context has been used, and 18 concurrent B = 1 pipelines run
+// 6.6k spectra/s with "tf" against 7.8-8.1k with "tw7". MDG_FITSUP = tf | tw7 |
+// tw3s | twf | twf1 | twf3s | plain forces one (all bit-identical; tests,
+// measurements); any other value is ignored.
 static std::string fit_choice(const BatchArgs& a) {
     if (const char* force = std::getenv("MDG_FITSUP")) {
         const std::string f(force);
@@ -3473,7 +3435,7 @@ static std::string fit_choice(const BatchArgs& a) {
             return f;
     }
     if (a.B == 1 && a.contexts > 1) return "tw7";
-    return a.B <= 2 ? "tf" : a.B <= 24 ? "tw7" : "plain";
+    return a.B <= 4 ? "tf" : a.B <= 24 ? "twf1" : "plain";
 }
 bool fit_sup_fused(const BatchArgs& a) { return fit_choice(a) != "plain"; }
 const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st) {
@@ -3544,8 +3506,17 @@ void launch_retain(const BatchArgs& a, const Workspace& w, hipStream_t st) {
 // k_mse_quad / k_mse_partial_n / k_mse_partial; those are not in the
 // library any more.
 constexpr int kLocNPT = 2;
+// MDG_MSE_NPT = 2 | 4 (points per thread) and MDG_MSE_PARTS (tile workgroups per
+// spectrum, <= kMseMaxParts): measurement knobs for small batches
+// Default: 4 points per thread from B = 8 to 64 (blood set, B = 16: 55 against 81 us
+// per launch; B = 1: 24 against 18 -- a single spectrum wants the finer tiles)
+static int mse_npt(const BatchArgs& a) {
+    if (const char* e = std::getenv("MDG_MSE_NPT")) return std::atoi(e) == 4 ? 4 : kLocNPT;
+    return a.B >= 8 && a.B <= 64 ? 4 : kLocNPT;
+}
 int mse_nparts(const BatchArgs& a) {
-    const int tp = kLocTP * kLocNPT;
+    if (const char* e = std::getenv("MDG_MSE_PARTS")) return std::max(1, std::min(kMseMaxParts, std::atoi(e)));
+    const int tp = kLocTP * mse_npt(a);
     return std::max(1, std::min({kMseMaxParts, (a.N + tp - 1) / tp, std::max(1, 8192 / a.B)}));
 }
 const char* launch_mse(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st) {
@@ -3554,6 +3525,10 @@ const char* launch_mse(const BatchArgs& a, const Workspace& w, int nparts, hipSt
     int cap = kLocNear;
     if (const char* e = std::getenv("MDG_MSE_NEARCAP")) cap = std::max(0, std::min(kLocNear, std::atoi(e)));
     // nparts tile workgroups per spectrum plus its retain workgroup
+    if (mse_npt(a) == 4) {
+        launch_k(k_mse_local<4>, dim3((nparts + 1) * a.B), dim3(256), 0, st, a, w, nparts, cap);
+        return "k_mse_local<4>";
+    }
     launch_k(k_mse_local<kLocNPT>, dim3((nparts + 1) * a.B), dim3(256), 0, st, a, w, nparts, cap);
     return "k_mse_local<2>";
 }

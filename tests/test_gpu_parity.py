@@ -566,12 +566,14 @@ def test_fit_superposition_kernels_batch(ctx, path, monkeypatch):
         assert abs(mse[s] - o.mse) <= MSE_RTOL * abs(o.mse), s
 
 
+@pytest.mark.parametrize("npt", ["2", "4"])
 @pytest.mark.parametrize("near_cap", [None, "8", "0"])
-def test_mse_cases(ctx, near_cap, monkeypatch):
-    """The MSE (k_mse_local) against the oracle: ignore regions (two in one spectrum),
-    a short signal region (sim) and a batch whose spectra differ in peak count; also
-    with a tiny near-list capacity (crowded tiles take the kernel's direct sum) and
-    none at all (every tile direct)."""
+def test_mse_cases(ctx, near_cap, npt, monkeypatch):
+    """The MSE (k_mse_local, 2 and 4 points per thread) against the oracle: ignore
+    regions (two in one spectrum), a short signal region (sim) and a batch whose
+    spectra differ in peak count; also with a tiny near-list capacity (crowded tiles
+    take the kernel's direct sum) and none at all (every tile direct)."""
+    monkeypatch.setenv("MDG_MSE_NPT", npt)
     if near_cap is not None:
         monkeypatch.setenv("MDG_MSE_NEARCAP", near_cap)
     for name in ["blood_01_water", "blood_02_two_regions_increasing", "sim_05", "synth_128k_2k_s0"]:

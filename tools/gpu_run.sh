@@ -79,6 +79,33 @@ for step in "$@"; do
         f=$(find gpurun_out/$tag -name run_kernel_trace.csv | head -1)
         [ -n "$f" ] && run timeline_$tag 60 python tools/blood_trace.py --summary "$f"
       done ;;
+    ab_r4)
+      # round 4 small-batch defaults (twf1 fit, 4-point MSE tiles from B = 8) against the
+      # round-3 choices, configs[4] alone; and the headline's MSE tile shape
+      ROUNDS=2 run ab_c4 900 bash tools/ab.sh r4c4 "c4_new --c4-only" "c4_old MDG_FITSUP=tw7 MDG_MSE_NPT=2 --c4-only"
+      ROUNDS=2 BENCH="--steps 8 --warmup 2" run ab_q 900 bash tools/ab.sh r4q "q_npt2" "q_npt4 MDG_MSE_NPT=4"
+      cat gpurun_out/ab_r4c4/summary.txt gpurun_out/ab_r4q/summary.txt | tee -a $log ;;
+    fitb:*)
+      # fitb:<B>: the fit kernels' launch durations in one blood call of B spectra
+      b=${step#fitb:}
+      for fk in tw7 twf1 twf3s tf plain; do
+        tag=fit_b${b}_$fk
+        MDG_FITSUP=$fk timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/$tag -o run -- python3 tools/blood_trace.py $b > gpurun_out/run/$tag.log 2>&1 || { echo "STOP $tag"; exit 3; }
+        f=$(find gpurun_out/$tag -name run_kernel_trace.csv | head -1)
+        echo "== $tag $(python tools/blood_trace.py --summary "$f" | grep -E "fit|total" | awk '{s+=$4; n++} END {print n, s}')" | tee -a $log
+      done ;;
+    msediag)
+      # the MSE kernel at small batches: tile workgroups per spectrum and points per thread
+      for v in "" "MDG_MSE_PARTS=128" "MDG_MSE_PARTS=64" "MDG_MSE_NPT=4" "MDG_MSE_NPT=4 MDG_MSE_PARTS=64"; do
+        tag=mse_$(echo "$v" | tr ' =' '__')
+        env $v MDG_FITSUP=twf1 timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/$tag -o run -- python3 tools/blood_trace.py 16 > gpurun_out/run/$tag.log 2>&1 || { echo "STOP $tag"; exit 3; }
+        f=$(find gpurun_out/$tag -name run_kernel_trace.csv | head -1)
+        echo "== $tag" | tee -a $log
+        python tools/blood_trace.py --summary "$f" | grep -E "mse|total" | tee -a $log
+        env $v timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/${tag}_b1 -o run -- python3 tools/blood_trace.py 1 > gpurun_out/run/${tag}_b1.log 2>&1 || { echo "STOP $tag b1"; exit 3; }
+        f=$(find gpurun_out/${tag}_b1 -name run_kernel_trace.csv | head -1)
+        python tools/blood_trace.py --summary "$f" | grep -E "mse|select|total" | tee -a $log
+      done ;;
     c0diag)
       run c0_breakdown 300 python tools/c0_breakdown.py 200
       run stage_diag_b1 120 python tools/stage_diag.py 1
