@@ -3508,11 +3508,13 @@ void launch_retain(const BatchArgs& a, const Workspace& w, hipStream_t st) {
 constexpr int kLocNPT = 2;
 // MDG_MSE_NPT = 2 | 4 (points per thread) and MDG_MSE_PARTS (tile workgroups per
 // spectrum, <= kMseMaxParts): measurement knobs for small batches
-// Default: 4 points per thread from B = 8 to 64 (blood set, B = 16: 55 against 81 us
-// per launch; B = 1: 24 against 18 -- a single spectrum wants the finer tiles)
+// Default: 4 points per thread from B = 8 (blood set, B = 16: 55 against 81 us per
+// launch; the headline queue, B = 256: 3.6 against 3.8 us per spectrum, 15.76-15.78k
+// against 15.67-15.68k spectra/s; B = 1: 24 against 18 -- a single spectrum wants the
+// finer tiles)
 static int mse_npt(const BatchArgs& a) {
     if (const char* e = std::getenv("MDG_MSE_NPT")) return std::atoi(e) == 4 ? 4 : kLocNPT;
-    return a.B >= 8 && a.B <= 64 ? 4 : kLocNPT;
+    return a.B >= 8 ? 4 : kLocNPT;
 }
 int mse_nparts(const BatchArgs& a) {
     if (const char* e = std::getenv("MDG_MSE_PARTS")) return std::max(1, std::min(kMseMaxParts, std::atoi(e)));
