@@ -107,6 +107,8 @@ def parse(argv=None):
                     help="stage each step's spectrum and results through the context's own rows")
     ap.add_argument("--fit-iterations", type=int, default=0,
                     help="diagnostics only: override the analytical fit's iterations (0 = 10)")
+    ap.add_argument("--exact-mse", action="store_true",
+                    help="MDG_OPTION_EXACT_MSE: the reference's MSE summation order (stream/queue modes)")
     ap.add_argument("--idle-streams", type=int, default=0,
                     help="diagnostics: keep this many extra idle HIP streams alive (each "
                          "used once) during the headline, as RCCL's own streams would be")
@@ -411,6 +413,8 @@ def headline(args, nat, torch, dist, dev, rank, world):
     settings = nat.default_settings()
     if args.fit_iterations:
         settings.fit_iterations = args.fit_iterations
+    if args.exact_mse:
+        settings.options = nat.OPTION_EXACT_MSE
     slots = [Slot(nat, torch, dev, B, n, cap) for _ in range(S)]
     R = max(KS, WS, 1)  # distinct spectra (B each), seeds rank*R*B ...
     x, Y = synth_device(nat, slots[0].ctx, torch, R * B, n, args.peaks, rank * R * B, dev,
@@ -538,6 +542,8 @@ def headline_queue(args, nat, torch, dist, dev, rank, world):
     settings = nat.default_settings()
     if args.fit_iterations:
         settings.fit_iterations = args.fit_iterations
+    if args.exact_mse:
+        settings.options = nat.OPTION_EXACT_MSE
     q = nat.SpectrumQueue(dev.index, n, args.max_batch, args.lanes, settings)
     gen = nat.Context(dev.index)
     R = max(KS, WS, 1)  # distinct spectra, seeds rank*R ...

@@ -240,11 +240,13 @@ def _declare(L):
                                   _sz, _dp, _sz, _szp, _dp]
     L.mdg_deconvolute_batch.argtypes = [_vp, _sz, _sz, _dp, _sz, _dp, _sz, _dp, sp, _dp, _sz,
                                         _dp, _sz, _szp, _dp, ctypes.POINTER(ctypes.c_int)]
-    L.mdg_deconvolute_rows.argtypes = [_vp, _sz, _sz, ctypes.POINTER(_dp), ctypes.POINTER(_dp), _dp,
-                                       sp, _dp, _sz, _dp, _sz, _szp, _dp, ctypes.POINTER(ctypes.c_int)]
-    L.mdg_deconvolute_rows_i32.argtypes = [_vp, _sz, _sz, _dp, ctypes.POINTER(_i32p), _dp, _dp, sp,
-                                           _dp, _sz, _dp, _sz, _szp, _dp,
-                                           ctypes.POINTER(ctypes.c_int)]
+    # the host-row entry points take plain addresses (ints) as well as ctypes pointers:
+    # the per-call ctypes.cast of numpy's data_as costs ~4 us a pointer here, a dozen
+    # per batched call (Deconvoluter._run_batch / _run_one)
+    L.mdg_deconvolute_rows.argtypes = [_vp, _sz, _sz, _vp, _vp, _vp, sp, _vp, _sz, _vp, _sz, _vp,
+                                       _vp, _vp]
+    L.mdg_deconvolute_rows_i32.argtypes = [_vp, _sz, _sz, _vp, _vp, _vp, _vp, sp, _vp, _sz, _vp,
+                                           _sz, _vp, _vp, _vp]
     L.mdg_decode_rows_i32_device.argtypes = [_vp, _sz, _sz, _vp, _vp, _vp, _vp]
     L.mdg_deconvolute_batch_device.argtypes = [_vp, _sz, _sz, _vp, _sz, _vp, _sz, _vp, sp, _dp,
                                                _sz, _vp, _sz, _vp, _vp, _vp]

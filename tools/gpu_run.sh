@@ -85,6 +85,12 @@ for step in "$@"; do
       ROUNDS=2 run ab_c4 900 bash tools/ab.sh r4c4 "c4_new --c4-only" "c4_old MDG_FITSUP=tw7 MDG_MSE_NPT=2 --c4-only"
       ROUNDS=2 BENCH="--steps 8 --warmup 2" run ab_q 900 bash tools/ab.sh r4q "q_npt2" "q_npt4 MDG_MSE_NPT=4"
       cat gpurun_out/ab_r4c4/summary.txt gpurun_out/ab_r4q/summary.txt | tee -a $log ;;
+    c4b) run c4_breakdown 300 python tools/c4_breakdown.py ;;
+    exactmse)
+      # the exact-order MSE option's cost: the headline queue and one spectrum at a time
+      ROUNDS=2 BENCH="--steps 8 --warmup 2" run ab_exact 900 bash tools/ab.sh r4exact "q" "q_exact --exact-mse" \
+          "b1 --mode stream --batch 1 --streams 1 --steps 40 --warmup 5" "b1_exact --mode stream --batch 1 --streams 1 --steps 40 --warmup 5 --exact-mse"
+      cat gpurun_out/ab_r4exact/summary.txt | tee -a $log ;;
     fitb:*)
       # fitb:<B>: the fit kernels' launch durations in one blood call of B spectra
       b=${step#fitb:}
