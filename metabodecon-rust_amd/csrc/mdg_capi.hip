@@ -51,7 +51,8 @@ struct mdg_ctx {
     int device = 0;
     hipStream_t own = nullptr;
     hipStream_t stream = nullptr;
-    bool counted = false;  // in g_live_ctx (has run a pipeline)
+    bool counted = false;  // in g_active (has run a pipeline)
+    std::atomic<long long> last_pipeline_ns{0};  // steady clock at its last pipeline
     std::mutex mu;
     // workspace arena
     Buffer arena;
@@ -546,12 +547,39 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
 // uploaded only when the regions differ from the ones it holds (the usual caller
 // passes the same Deconvoluter's regions every call): no host-to-device copy, and
 // no pageable-copy stall, in a stream of calls.
-// Engine contexts per device that have run a pipeline (and are not destroyed):
-// the B = 1 fit kernel differs when the spectrum is likely to have the GPU to
-// itself (fit_choice). A context counts from its first pipeline on,
-// so the idle lanes of a Deconvoluter do not.
+// Engine contexts per device that ran a pipeline in the last kActiveNs: the B = 1
+// fit kernel differs when the spectrum is likely to have the GPU to itself
+// (fit_choice). Concurrent callers launch every millisecond or so;
+// contexts that are merely alive (a finished queue, the idle lanes of a
+// Deconvoluter) do not count. a.contexts holds min(count, 2): the choice only asks
+// "alone or not", and the batch arguments are part of the graph keys.
 constexpr int kMaxDevices = 64;
-static std::atomic<int> g_live_ctx[kMaxDevices];
+constexpr long long kActiveNs = 50'000'000;
+struct DeviceActivity {
+    std::mutex mu;
+    std::vector<mdg_ctx*> ctxs;  // contexts that have run a pipeline, until destroyed
+};
+static DeviceActivity g_active[kMaxDevices];
+static long long steady_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+static int active_contexts(mdg_ctx* c) {
+    if (c->device < 0 || c->device >= kMaxDevices) return 2;
+    const long long now = steady_ns();
+    c->last_pipeline_ns.store(now);
+    DeviceActivity& d = g_active[c->device];
+    std::lock_guard<std::mutex> g(d.mu);
+    if (!c->counted) {
+        c->counted = true;
+        d.ctxs.push_back(c);
+    }
+    int n = 0;
+    for (mdg_ctx* o : d.ctxs)
+        if (now - o->last_pipeline_ns.load() < kActiveNs) ++n;
+    return std::min(n, 2);
+}
 
 int fill_args(mdg_ctx* c, BatchArgs& a, size_t b, size_t n, const double* x, size_t xs, const double* y,
               size_t ys, const double* sb, const double* ignore, size_t n_ignore, double* out,
@@ -565,11 +593,7 @@ int fill_args(mdg_ctx* c, BatchArgs& a, size_t b, size_t n, const double* x, siz
     a.y_stride = (int64_t)ys;
     a.sb = sb;
     a.n_ignore = (int)n_ignore;
-    if (!c->counted && c->device < kMaxDevices) {
-        c->counted = true;
-        g_live_ctx[c->device].fetch_add(1);
-    }
-    a.contexts = c->counted ? g_live_ctx[c->device].load() : 2;
+    a.contexts = active_contexts(c);
     a.ignore = nullptr;
     if (n_ignore > 0) {
         const size_t cnt = 2 * n_ignore;
@@ -801,7 +825,11 @@ int mdg_ctx_destroy(mdg_ctx* c) {
         if (c->hsmall) (void)hipHostFree(c->hsmall);
         if (c->own) (void)hipStreamDestroy(c->own);
     }
-    if (c->counted) g_live_ctx[c->device].fetch_sub(1);
+    if (c->counted) {
+        DeviceActivity& d = g_active[c->device];
+        std::lock_guard<std::mutex> g(d.mu);
+        d.ctxs.erase(std::remove(d.ctxs.begin(), d.ctxs.end(), c), d.ctxs.end());
+    }
     delete c;
     return MDG_OK;
 }

@@ -29,7 +29,7 @@ struct BatchArgs {
     int32_t* out_count;
     double* out_mse;
     int32_t* out_status;
-    int contexts;         // engine contexts alive on the device (kernel choice only)
+    int contexts;         // engine contexts with a pipeline in the last 50 ms on the device, max 2 (kernel choice only)
 };
 
 // Context-owned device workspace (sized for the worst case of the batch shape).
