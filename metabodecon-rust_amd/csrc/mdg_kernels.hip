@@ -3215,19 +3215,40 @@ __global__ void k_mse_exact_res(BatchArgs a, Workspace w, double* res, int64_t r
     }
 }
 
-// k_mse_exact_fold: one wave per spectrum folds each region's squared residuals left
-// to right from -0.0 (`.sum::<f64>()`), adds the region sums in region order (the
+// k_mse_exact_fold: one workgroup per spectrum folds each region's squared residuals
+// left to right from -0.0 (`.sum::<f64>()`), adds the region sums in region order (the
 // outer `.sum::<f64>()`) and divides by the regions' total length; it overwrites the
-// MSE k_mse_local wrote (its status stays).
-__global__ __launch_bounds__(64) void k_mse_exact_fold(BatchArgs a, Workspace w, const double* res,
-                                                       int64_t res_row) {
+// MSE k_mse_local wrote (its status stays). The squared residuals are >= +0, so a
+// region of 64 or more terms takes k_select's windowed fold (every add the
+// reference's, in its order; §2): one wave alone folded the ~91k terms of a
+// 131072-point spectrum in ~300 us.
+constexpr int kExactFoldBS = 1024;
+__global__ __launch_bounds__(kExactFoldBS) void k_mse_exact_fold(BatchArgs a, Workspace w, const double* res,
+                                                                 int64_t res_row) {
+    __shared__ WinLds wl;
+    __shared__ double part_sh;
     const int s = blockIdx.x;
     if (w.status[s] || w.mse_panic[s]) return;
     const int nig = w.n_ig[s];
     const int64_t* cum = w.ig_cum + (size_t)s * (w.ig_cap + 2);
     const double* r = res + (size_t)s * res_row;
     double total = -0.0;
-    for (int k = 0; k <= nig; ++k) total += dpp_fold(-0.0, r + cum[k], (int)(cum[k + 1] - cum[k]));
+    for (int k = 0; k <= nig; ++k) {
+        const int n = (int)(cum[k + 1] - cum[k]);
+        double part;
+        if (n >= 4 * kWinSeg) {
+            part = window_fold<kExactFoldBS>(-0.0, wl, r + cum[k], n, 60);  // barriers inside
+        } else {
+            if (threadIdx.x < 64) {
+                const double v = dpp_fold(-0.0, r + cum[k], n);
+                if (threadIdx.x == 0) part_sh = v;
+            }
+            __syncthreads();
+            part = part_sh;
+            __syncthreads();
+        }
+        total += part;
+    }
     if (threadIdx.x == 0) a.out_mse[s] = total / (double)cum[nig + 1];
 }
 
@@ -3541,11 +3562,12 @@ void launch_mse_exact(const double* sup, const double* y, int64_t n, const Works
 }
 void launch_mse_exact_batch(const BatchArgs& a, const Workspace& w, double* res, int64_t res_row,
                             hipStream_t st) {
-    // enough 256-thread workgroups for 4 points per thread at 131072 points, fewer per
-    // spectrum for larger batches (the grid-stride loop covers the rest)
-    const int parts = std::max(1, std::min<int>(cdiv(res_row, 1024), std::max(1, 16384 / a.B)));
+    // one point per thread (every SIMD gets waves even for one spectrum: each thread's
+    // in-order superposition is a dependent chain), fewer workgroups per spectrum for
+    // larger batches (the grid-stride loop covers the rest)
+    const int parts = std::max(1, std::min<int>(cdiv(res_row, 256), std::max(1, 65536 / a.B)));
     launch_k(k_mse_exact_res, dim3(parts * a.B), dim3(256), 0, st, a, w, res, res_row);
-    launch_k(k_mse_exact_fold, dim3(a.B), dim3(64), 0, st, a, w, (const double*)res, res_row);
+    launch_k(k_mse_exact_fold, dim3(a.B), dim3(kExactFoldBS), 0, st, a, w, (const double*)res, res_row);
 }
 void launch_superposition_vec(const double* x, int64_t n, const double* params, int P,
                               double* out, int* flag, hipStream_t st) {
