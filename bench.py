@@ -218,18 +218,24 @@ def hbm_pipeline(tag, batch, iterations, value, n):
     launches per pipeline, / the batch size), and the rate it implies at `value`
     spectra/s -- the BASELINE metric's "achieved HBM GB/s" for the mode that
     produces `value`. None when no summary is committed."""
-    launches = {"k_queue_gather": 1, "k_smooth_chain<3, false>": 1, "k_flags": 1, "k_peaks": 1,
-                "k_select<1024>": 1, "k_fit_sup": iterations, "k_fit_update": iterations,
-                "k_mse_local": 1, "k_queue_scatter": 1}
+    launches = {"k_queue_gather": 1, "k_smooth_chain<3, false>": 1, "k_flags": 1,
+                "k_peaks<256, 1024>": 1, "k_select<1024>": 1, "k_fit_sup": iterations,
+                "k_fit_update": iterations, "k_mse_local<4>": 1, "k_queue_scatter": 1}
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{tag}.json")),
                        reverse=True):
         try:
             kern = json.load(open(path))["kernels"]
-            # matched by base name: template arguments differ between rounds
-            # (k_peaks -> k_peaks<256, 1024>)
-            by_base = {k.split("<")[0].strip(): v for k, v in kern.items()}
-            per = {k: by_base[k.split("<")[0].strip()]["hbm_bytes_per_launch"] * m / batch
-                   for k, m in launches.items()}
+
+            def entry(k):
+                # the exact kernel, else (a summary from before a kernel's template
+                # arguments changed: k_peaks -> k_peaks<256, 1024>) the largest of the
+                # same base name, which is the batch's
+                if k in kern:
+                    return kern[k]
+                base = k.split("<")[0].strip()
+                return max((v for n, v in kern.items() if n.split("<")[0].strip() == base),
+                           key=lambda v: v["hbm_bytes_per_launch"])
+            per = {k: entry(k)["hbm_bytes_per_launch"] * m / batch for k, m in launches.items()}
         except (OSError, KeyError, ValueError):
             continue
         total = sum(per.values())

@@ -45,9 +45,9 @@ for step in "$@"; do
     forcedist) run forcedist 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
         --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 1 --force-dist --steps 4 --warmup 1 --no-cpu-baseline ;;
     prof) run prof_all 1200 bash tools/prof_all.sh
-      f=$(ls gpurun_out/prof_q256/*/*/run_kernel_trace.csv 2>/dev/null | head -1)
-      [ -n "$f" ] && run alone_q256 60 python tools/alone_kernels.py "$f" --out gpurun_out/bench_alone_q256.json \
-          --command "rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu-baseline --no-configs --steps 6 --warmup 2 --verify 0" ;;
+      f=$(find gpurun_out/prof_q256 -name run_kernel_trace.csv | head -1)
+      if [ -n "$f" ]; then run alone_q256 60 python tools/alone_kernels.py "$f" --out gpurun_out/bench_alone_q256.json \
+          --command "rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu-baseline --no-configs --steps 6 --warmup 2 --verify 0"; fi ;;
     c4)
       cfgs=()
       for q in 4 32; do for l in 1 2 3 4 8 16; do
@@ -77,7 +77,7 @@ for step in "$@"; do
           run trace_$tag 180 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/$tag -o run -- python3 tools/blood_trace.py $b
         fi
         f=$(find gpurun_out/$tag -name run_kernel_trace.csv | head -1)
-        [ -n "$f" ] && run timeline_$tag 60 python tools/blood_trace.py --summary "$f"
+        if [ -n "$f" ]; then run timeline_$tag 60 python tools/blood_trace.py --summary "$f"; fi
       done ;;
     ab_r4)
       # round 4 small-batch defaults (twf1 fit, 4-point MSE tiles from B = 8) against the
