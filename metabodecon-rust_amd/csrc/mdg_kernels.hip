@@ -1714,22 +1714,43 @@ __device__ __forceinline__ void two_sum(double a, double b, double& s, double& e
 
 // dpp_fold for one window segment (a few hundred terms): groups of 16 terms are
 // loaded 8 groups at a time, the next 8 in flight while the current 8 are folded
-// (dpp_fold's own steady loop starts at 24 groups; below that it waits on every load)
+// (dpp_fold's own steady loop starts at 24 groups; below that it waits on every load).
+// The count is made wave-uniform (a call passes it in a VGPR), so the group loops are
+// scalar branches, and only the last partial batch clamps its addresses: the
+// per-group exec-mask branches and per-load clamps of the first version cost ~40% of
+// stage B (18.4k cycles per fold on blood_01's 5116 SFR scores).
 __device__ __noinline__ double seg_fold(double acc, const double* __restrict__ t, int n) {
+    n = __builtin_amdgcn_readfirstlane(n);
     const int sub = threadIdx.x & 15;
     const double one = 1.0;
     const int G = n / 16;
-    double cur[8], nxt[8];
+    const double* tp = t + sub;
+    int g = 0;
+    if (G >= 8) {
+        double cur[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) cur[u] = t[min(16 * u + sub, max(n - 1, 0))];
-    for (int g0 = 0; g0 < G; g0 += 8) {
+        for (int u = 0; u < 8; ++u) cur[u] = tp[16 * u];
+        for (; g + 16 <= G; g += 8) {
+            double nxt[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) nxt[u] = t[min(16 * (g0 + 8 + u) + sub, max(n - 1, 0))];
+            for (int u = 0; u < 8; ++u) nxt[u] = tp[16 * (g + 8 + u)];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) fold16(acc, cur[u], one);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) cur[u] = nxt[u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) fold16(acc, cur[u], one);
+        g += 8;
+    }
+    {  // the last < 8 groups: their loads issued together
+        double tl[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u)
-            if (g0 + u < G) fold16(acc, cur[u], one);
+            if (g + u < G) tl[u] = tp[16 * (g + u)];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) cur[u] = nxt[u];
+        for (int u = 0; u < 8; ++u)
+            if (g + u < G) fold16(acc, tl[u], one);
     }
     const int r = n - 16 * G;
     if (r > 0) {
@@ -1925,6 +1946,7 @@ __device__ __forceinline__ void fit_init_pair(const BatchArgs& a, const Workspac
 constexpr int kSfrLds = 12288;         // 96 KB
 constexpr int kSelLds = 4096;          // 3 ints each: 48 KB of the same buffer
 constexpr int kSelCountDirect = 16;    // centers per thread counted directly (P <= 16384)
+constexpr int kSelPerThread = 16;      // candidates per thread compacted from registers
 static_assert(3 * kSelLds * sizeof(int) <= kSfrLds * sizeof(double), "selection fits the SFR buffer");
 template <int BS>
 __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double threshold) {
@@ -2066,6 +2088,45 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
     const int per = (len + BS - 1) / BS;
     const int q0 = left + threadIdx.x * per;
     const int q1 = min(right, q0 + per);
+    if (per <= kSelPerThread) {
+        // up to kSelPerThread candidates per thread (len <= 16384): their scores
+        // loaded together, the keep flags a bit mask; each kept candidate's borders,
+        // then its stencil points, loaded two candidates at a time, and the fit's
+        // initial state (k_fit_init's work) written by the thread that kept it -- no
+        // sequential per-candidate loads, no LDS hand-off to a separate loop
+        unsigned km = 0;
+        {
+            double sc[kSelPerThread];
+#pragma unroll
+            for (int u = 0; u < kSelPerThread; ++u) sc[u] = scores[min(q0 + u, P - 1)];
+#pragma unroll
+            for (int u = 0; u < kSelPerThread; ++u)
+                km |= (unsigned)(q0 + u < q1 && sc[u] >= thr) << u;
+        }
+        int total;
+        int out = block_exclusive_scan<BS>(__builtin_popcount(km), lds_i, &total);
+        if (threadIdx.x == 0) {
+            w.sel_count[s] = total;
+            if (total == 0) w.status[s] = MDG_EMPTY_SIGNAL_REGION;
+        }
+        KSTAMP(14);
+        while (km) {
+            const int u1 = __builtin_ctz(km);
+            km &= km - 1;
+            const int u2 = km ? __builtin_ctz(km) : u1;
+            if (km) km &= km - 1;
+            const int qa = q0 + u1, qb = q0 + u2;
+            const int la = pl[qa], ca = pc[qa], ra = pr[qa];
+            const int lb = pl[qb], cb = pc[qb], rb = pr[qb];
+            const int pa = out, pb = u2 != u1 ? out + 1 : out;
+            w.sel_l[base + pa] = la; w.sel_c[base + pa] = ca; w.sel_r[base + pa] = ra;
+            w.sel_l[base + pb] = lb; w.sel_c[base + pb] = cb; w.sel_r[base + pb] = rb;
+            fit_init_pair(a, w, s, base, pa, la, ca, ra, pb, lb, cb, rb);
+            out = pb + 1;
+        }
+        KSTAMP(18);
+        return;
+    }
     int keep = 0;
     for (int q = q0; q < q1; ++q) keep += scores[q] >= thr;
     int total;
