@@ -1978,12 +1978,13 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
     const int step = (P + BS - 1) / BS;
     long long cnt0, cnt1;
     if (step <= kSelCountDirect) {
-        const int i0 = threadIdx.x * step;
+        // thread t counts centers t, t + BS, ...: each load instruction is coalesced
         long long v = 0;
 #pragma unroll
         for (int u = 0; u < kSelCountDirect; ++u) {
-            const int64_t c = pc[min(i0 + u, P - 1)];
-            if (u < step && i0 + u < P) v += ((long long)(c <= sbi0) << 32) | (long long)(c <= sbi1);
+            const int i = (int)threadIdx.x + BS * u;
+            const int64_t c = pc[min(i, P - 1)];
+            if (i < P) v += ((long long)(c <= sbi0) << 32) | (long long)(c <= sbi1);
         }
         const long long k01 = block_sum_ll<BS>(v, lds_l);
         cnt0 = k01 >> 32;
@@ -2089,40 +2090,63 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
     const int q0 = left + threadIdx.x * per;
     const int q1 = min(right, q0 + per);
     if (per <= kSelPerThread) {
-        // up to kSelPerThread candidates per thread (len <= 16384): their scores
-        // loaded together, the keep flags a bit mask; each kept candidate's borders,
-        // then its stencil points, loaded two candidates at a time, and the fit's
-        // initial state (k_fit_init's work) written by the thread that kept it -- no
-        // sequential per-candidate loads, no LDS hand-off to a separate loop
-        unsigned km = 0;
-        {
-            double sc[kSelPerThread];
+        // up to kSelPerThread candidates per thread (len <= 16384), owned wave by
+        // wave: wave v holds the contiguous range [left + 64·per·v, +64·per), lane l
+        // its candidates 64u + l (u < per), so every score load is coalesced and the
+        // order within the wave is (u, lane). The keep flags of round u are a ballot;
+        // a kept candidate's position is its wave's offset (a scan over the waves),
+        // the kept ones of the wave's earlier rounds and its lanes below it in round u
+        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+        const int wbase = left + 64 * per * wv;
+        double sc[kSelPerThread];  // the scores stay in VGPRs; the ballots are redone
 #pragma unroll
-            for (int u = 0; u < kSelPerThread; ++u) sc[u] = scores[min(q0 + u, P - 1)];
+        for (int u = 0; u < kSelPerThread; ++u) sc[u] = scores[min(wbase + 64 * u + lane, P - 1)];
+        auto kept = [&](int u) { return u < per && wbase + 64 * u + lane < right && sc[u] >= thr; };
+        int wcount = 0;
 #pragma unroll
-            for (int u = 0; u < kSelPerThread; ++u)
-                km |= (unsigned)(q0 + u < q1 && sc[u] >= thr) << u;
-        }
+        for (int u = 0; u < kSelPerThread; ++u) wcount += __popcll(__ballot(kept(u)));
         int total;
-        int out = block_exclusive_scan<BS>(__builtin_popcount(km), lds_i, &total);
+        const int woff = block_exclusive_scan<BS>(lane == 0 ? wcount : 0, lds_i, &total);
+        const int wstart = __shfl(woff, 0, 64);  // lane 0's exclusive prefix: the wave's offset
+        int o = wstart;
+#pragma unroll
+        for (int u = 0; u < kSelPerThread; ++u) {
+            const uint64_t bu = __ballot(kept(u));
+            if (bu >> lane & 1) {
+                const int q = wbase + 64 * u + lane;
+                const int pos = o + __builtin_amdgcn_mbcnt_hi((unsigned)(bu >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((unsigned)bu, 0u));
+                const int l = pl[q], c = pc[q], r = pr[q];
+                w.sel_l[base + pos] = l;
+                w.sel_c[base + pos] = c;
+                w.sel_r[base + pos] = r;
+                if (pos < kSelLds) {
+                    sel_lds[3 * pos] = l;
+                    sel_lds[3 * pos + 1] = c;
+                    sel_lds[3 * pos + 2] = r;
+                }
+            }
+            o += __popcll(bu);
+        }
         if (threadIdx.x == 0) {
             w.sel_count[s] = total;
             if (total == 0) w.status[s] = MDG_EMPTY_SIGNAL_REGION;
         }
         KSTAMP(14);
-        while (km) {
-            const int u1 = __builtin_ctz(km);
-            km &= km - 1;
-            const int u2 = km ? __builtin_ctz(km) : u1;
-            if (km) km &= km - 1;
-            const int qa = q0 + u1, qb = q0 + u2;
-            const int la = pl[qa], ca = pc[qa], ra = pr[qa];
-            const int lb = pl[qb], cb = pc[qb], rb = pr[qb];
-            const int pa = out, pb = u2 != u1 ? out + 1 : out;
-            w.sel_l[base + pa] = la; w.sel_c[base + pa] = ca; w.sel_r[base + pa] = ra;
-            w.sel_l[base + pb] = lb; w.sel_c[base + pb] = cb; w.sel_r[base + pb] = rb;
-            fit_init_pair(a, w, s, base, pa, la, ca, ra, pb, lb, cb, rb);
-            out = pb + 1;
+        const bool in_lds = total <= kSelLds;
+        if (in_lds) lds_barrier();
+        else __syncthreads();
+        for (int p = threadIdx.x; p < total; p += 2 * BS) {
+            const int p2 = p + BS < total ? p + BS : p;
+            int l1, c1, r1, l2, c2, r2;
+            if (in_lds) {
+                l1 = sel_lds[3 * p]; c1 = sel_lds[3 * p + 1]; r1 = sel_lds[3 * p + 2];
+                l2 = sel_lds[3 * p2]; c2 = sel_lds[3 * p2 + 1]; r2 = sel_lds[3 * p2 + 2];
+            } else {
+                l1 = w.sel_l[base + p]; c1 = w.sel_c[base + p]; r1 = w.sel_r[base + p];
+                l2 = w.sel_l[base + p2]; c2 = w.sel_c[base + p2]; r2 = w.sel_r[base + p2];
+            }
+            fit_init_pair(a, w, s, base, p, l1, c1, r1, p2, l2, c2, r2);
         }
         KSTAMP(18);
         return;

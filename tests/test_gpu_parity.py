@@ -525,6 +525,29 @@ def test_peak_chunkings(ctx, mode, monkeypatch):
         assert np.array_equal(out[s, : counts[s]], o.params), s
 
 
+def test_selection_many_signal_peaks(ctx):
+    """k_select compacts up to 16 candidates per thread from registers (16384 signal-
+    region peaks); a pure-noise spectrum with a wide signal region has ~27k, so its
+    workgroup takes the general loop. One batch with a blood spectrum (the register
+    path) beside it: both against the oracle, bit for bit."""
+    n = 131072
+    rng = np.random.default_rng(11)
+    x = np.linspace(14.8, -5.2, n)
+    noise = rng.normal(size=n) * 100 + 1000
+    st = oracle.default_settings()
+    bx, by, bsb, bst, _ = load_case("blood_05")
+    assert bx.size == n
+    for rows, sbs in (([noise], [(14.5, -4.9)]), ([noise, by], [(14.5, -4.9), bsb])):
+        ys = np.stack(rows)
+        status, counts, out, mse = gpu_batch(ctx, x if len(rows) == 1 else np.stack([x, bx]), ys, sbs, st)
+        for k, (yy, sb) in enumerate(zip(rows, sbs)):
+            xx = x if k == 0 else bx
+            o = oracle.deconvolute(xx, yy, sb, st)
+            assert status[k] == o.status == 0
+            assert np.array_equal(out[k, : counts[k]], o.params), k
+            assert abs(mse[k] - o.mse) <= MSE_RTOL * abs(o.mse), k
+
+
 def _force_fit(monkeypatch, path):
     kernel, _, g = path.partition(":")
     monkeypatch.setenv("MDG_FITSUP", kernel)
