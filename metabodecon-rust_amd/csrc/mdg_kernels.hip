@@ -1945,7 +1945,10 @@ __device__ __forceinline__ void fit_init_pair(const BatchArgs& a, const Workspac
 // through the workspace), reused afterwards for the selected peaks (up to kSelLds)
 constexpr int kSfrLds = 12288;         // 96 KB
 constexpr int kSelLds = 4096;          // 3 ints each: 48 KB of the same buffer
-constexpr int kSelCountDirect = 16;    // centers per thread counted directly (P <= 16384)
+// centers per thread counted directly: 1, i.e. only P <= 1024 (blood_01, P = 16100,
+// stamps at B = 1: the two-level search 7.2-8.1k cycles, 16 direct loads per thread
+// 11.2k strided and 12.1k coalesced)
+constexpr int kSelCountDirect = 1;
 constexpr int kSelPerThread = 16;      // candidates per thread compacted from registers
 static_assert(3 * kSelLds * sizeof(int) <= kSfrLds * sizeof(double), "selection fits the SFR buffer");
 template <int BS>
@@ -2108,15 +2111,23 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
         int total;
         const int woff = block_exclusive_scan<BS>(lane == 0 ? wcount : 0, lds_i, &total);
         const int wstart = __shfl(woff, 0, 64);  // lane 0's exclusive prefix: the wave's offset
+        // the kept candidates' borders, every load issued before the first is used
+        int lv[kSelPerThread], cv[kSelPerThread], rv[kSelPerThread];
+#pragma unroll
+        for (int u = 0; u < kSelPerThread; ++u) {
+            const int q = min(wbase + 64 * u + lane, P - 1);
+            lv[u] = kept(u) ? pl[q] : 0;
+            cv[u] = kept(u) ? pc[q] : 0;
+            rv[u] = kept(u) ? pr[q] : 0;
+        }
         int o = wstart;
 #pragma unroll
         for (int u = 0; u < kSelPerThread; ++u) {
             const uint64_t bu = __ballot(kept(u));
             if (bu >> lane & 1) {
-                const int q = wbase + 64 * u + lane;
                 const int pos = o + __builtin_amdgcn_mbcnt_hi((unsigned)(bu >> 32),
                                                                __builtin_amdgcn_mbcnt_lo((unsigned)bu, 0u));
-                const int l = pl[q], c = pc[q], r = pr[q];
+                const int l = lv[u], c = cv[u], r = rv[u];
                 w.sel_l[base + pos] = l;
                 w.sel_c[base + pos] = c;
                 w.sel_r[base + pos] = r;
