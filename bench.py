@@ -1175,6 +1175,30 @@ def dry_run(args, world, rank):
         dist.destroy_process_group()
 
 
+def child_configs(want) -> dict:
+    """configs[4] (default environment and 32 hardware queues) and configs[0], each in
+    a fresh child process (bench.py --c4-only / --c0-only), as a user's process runs
+    them -- started before this process touches the GPU: idle contexts and streams of
+    the headline, alive in a parent, slowed the children's small, latency-bound calls
+    (configs[0]: 1121 against 1193 spectra/s in two runs of the same build)."""
+    out = {}
+    runs = []
+    if "4" in want:
+        runs += [("configs[4]", "--c4-only", {}), ("configs[4]_hw_queues_32", "--c4-only",
+                                                   {"GPU_MAX_HW_QUEUES": "32"})]
+    if "0" in want:
+        runs.append(("configs[0]", "--c0-only", {}))
+    for key, flag, extra in runs:
+        p = subprocess.run([sys.executable, os.path.abspath(__file__), flag],
+                           env=dict(os.environ, **extra), capture_output=True, text=True, timeout=300)
+        try:
+            out[key] = json.loads(p.stdout.strip().splitlines()[-1])
+            out[key]["process"] = f"child (bench.py {flag}, before the parent initialises the GPU)"
+        except (ValueError, IndexError):
+            out[key] = {"error": p.stderr[-500:]}
+    return out
+
+
 def main():
     args = parse()
     # before anything initialises HIP (torch is imported below, and ranks inherit
@@ -1192,6 +1216,9 @@ def main():
         sys.exit(2)
     if args.dry_run:
         return dry_run(args, world, rank)
+    pre = {}
+    if world == 1 and rank == 0 and not (args.c0_only or args.c4_only or args.no_configs or args.force_dist):
+        pre = child_configs({c.strip() for c in args.configs.split(",") if c.strip()})
 
     import torch
     import torch.distributed as dist
@@ -1224,7 +1251,7 @@ def main():
         h = headline(args, nat, torch, dist, dev, rank, world)
         line = stream_line(args, h, world, nat)
     value = line["value"]
-    finish(args, line, value, nat, torch, dist, dev, rank, world, local)
+    finish(args, line, value, nat, torch, dist, dev, rank, world, local, pre)
 
 
 def queue_line(args, h, world, nat):
@@ -1329,7 +1356,7 @@ def stream_line(args, h, world, nat):
     return line
 
 
-def finish(args, line, value, nat, torch, dist, dev, rank, world, local):
+def finish(args, line, value, nat, torch, dist, dev, rank, world, local, pre=None):
     if (world > 1 or args.force_dist) and not args.no_configs:
         threads, _, _ = host_threads(args)
         dc = dist_configs(args, nat, torch, dist, dev, rank, world, threads)
@@ -1342,39 +1369,23 @@ def finish(args, line, value, nat, torch, dist, dev, rank, world, local):
         # configs[4] first: measured after configs[0] and configs[2] (their contexts'
         # streams created before the 16 lanes') its sets took 5.5 instead of 3.9 ms
         # (tools/c4_order.sh), the others are single-stream and order-insensitive
+        # configs[4] and configs[0] in child processes, as a fresh user process runs
+        # them: in this one the headline's contexts and torch's streams hold hardware
+        # queues (HIP's default 4) and the small calls' streams share them.
+        # Normally measured before this process touched the GPU (child_configs).
+        kids = dict(pre) if pre else child_configs(want & {"0", "4"})
         if "4" in want:
             import metabodecon as md
-            # measured in a child process, as a fresh user process runs it: in this
-            # one the headline's contexts and torch's streams already hold hardware
-            # queues (HIP's default 4), and the lanes' streams then share them
-            # (7.5-9.8k in-process against 10.3-11.1k alone); once with
-            # the default environment, once with 32 hardware queues
             blood_set = md.Spectrum.read_bruker_set(BLOOD, 10, 10, (-2.2, 11.8))
-            for key, extra in (("configs[4]", {}), ("configs[4]_hw_queues_32",
-                                                    {"GPU_MAX_HW_QUEUES": "32"})):
-                p = subprocess.run([sys.executable, os.path.abspath(__file__), "--c4-only"],
-                                   env=dict(os.environ, **extra), capture_output=True, text=True,
-                                   timeout=300)
-                try:
-                    configs[key] = json.loads(p.stdout.strip().splitlines()[-1])
-                    configs[key]["process"] = "child (bench.py --c4-only)"
-                except (ValueError, IndexError):
-                    configs[key] = {"error": p.stderr[-500:]}
+            for key in ("configs[4]", "configs[4]_hw_queues_32"):
+                configs[key] = kids.get(key, {"error": "not measured"})
         if "1h" in want:
             configs["configs[1]_host"] = host_rows_config(args, nat, torch, dev, host_threads(args)[0])
         if "0" in want:
             import metabodecon as md
-            # in a child process too: here the headline's queue lanes and the other
-            # configs' contexts keep idle streams on HIP's hardware queues, and a
-            # single-spectrum call, a chain of dependent launches, waits on them
-            # (0.89 against 0.84 ms per call, round 4)
-            p = subprocess.run([sys.executable, os.path.abspath(__file__), "--c0-only"],
-                               capture_output=True, text=True, timeout=300)
-            try:
-                configs["configs[0]"] = json.loads(p.stdout.strip().splitlines()[-1])
-                configs["configs[0]"]["process"] = "child (bench.py --c0-only)"
-            except (ValueError, IndexError):
-                configs["configs[0]"] = {"error": p.stderr[-500:]}
+            # a single-spectrum call is a chain of dependent launches: in this process
+            # it waits on the other contexts' idle streams (0.89 against 0.84 ms)
+            configs["configs[0]"] = kids.get("configs[0]", {"error": "not measured"})
             blood_sp = md.Spectrum.read_bruker(os.path.join(BLOOD, "blood_01"), 10, 10, (-2.2, 11.8))
             configs["optimize_settings"] = optimize_gpu(args, nat, torch, dev, blood_sp)
         if "2" in want:
@@ -1414,7 +1425,7 @@ def finish(args, line, value, nat, torch, dist, dev, rank, world, local):
                              ("configs[2]", ("synthetic", "value")),
                              ("configs[3]", ("synthetic_65536", "value")),
                              ("configs[4]", ("blood_set", "value"))):
-                if key in configs and ref[0] in cb:
+                if key in configs and "value" in configs[key] and ref[0] in cb:
                     configs[key]["speedup_vs_cpu"] = configs[key]["value"] / cb[ref[0]][ref[1]]
     if rank == 0:
         # the driver keeps only the tail of stdout: the parity and roofline summary go last
