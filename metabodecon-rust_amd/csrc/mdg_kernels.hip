@@ -1335,11 +1335,13 @@ __global__ __launch_bounds__(BS) void k_peaks(BatchArgs a, Workspace w, int dete
     __shared__ int lds_i[BS / 64 + 1];
     __shared__ long long lds_l[BS / 64 + 1];
     if (w.status[s]) return;  // uniform per spectrum: no chunk waits for a returned one
+    KSTAMP(0);
     const int nch = (w.W + WORDS - 1) / WORDS;
     unsigned long long* slot = (unsigned long long*)w.peak_cnt + (size_t)s * peak_slots(w.W);
     const int wd = chunk * WORDS + threadIdx.x;
     int bordered = 0, kept = 0;
     if ((int)threadIdx.x < WORDS && wd < w.W) kept = word_peaks<false>(a, w, s, wd, detector_only, &bordered, 0);
+    KSTAMP(1);
     int total;
     const int o = block_exclusive_scan<BS>(kept, lds_i, &total);
     const long long b_tot = block_sum_ll<BS>(bordered, lds_l);
@@ -1380,14 +1382,17 @@ __global__ __launch_bounds__(BS) void k_peaks(BatchArgs a, Workspace w, int dete
         return;
     }
     if (chunk == 0 && threadIdx.x == 0) w.det_count[s] = (int32_t)k_all;
+    KSTAMP(2);
     const size_t b0 = (size_t)s * w.capD + before;
     if (kept) word_peaks<true>(a, w, s, wd, detector_only, &bordered, b0 + o);
     if (detector_only || !score) return;
+    KSTAMP(3);
     // k_scores' work for this chunk's peaks, spread evenly over the block
     __syncthreads();  // the peaks above, written by other threads of the block
     const double* __restrict__ sm = w.smooth_ptr + (size_t)s * w.smooth_stride;
     for (int p = threadIdx.x; p < total; p += BS)
         w.scores[b0 + p] = score_peak(sm, a.N, w.det_l[b0 + p], w.det_c[b0 + p], w.det_r[b0 + p]);
+    KSTAMP(4);
 }
 
 // ----------------------------------------------------------------------------------
@@ -3045,6 +3050,7 @@ __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int
         if (part == 0) mse_panic_out(a, s);
         return;
     }
+    KSTAMP(30);
     const int P = w.sel_count[s];
     const size_t pbase = (size_t)s * w.capD;
     const double* __restrict__ prmv = final_params(w, s, pbase);
@@ -3066,6 +3072,7 @@ __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int
     int kept_n;
     (void)block_exclusive_scan<BS>(cnt, lds_i, &kept_n);
     const bool fast = w.x_ok[s] && !__syncthreads_or(uns);
+    KSTAMP(31);
     double acc = 0.0;
     for (int64_t v0 = (int64_t)part * TP; v0 < total; v0 += (int64_t)nparts * TP) {
         double xv[NPT], yv[NPT], sup[NPT];
@@ -3176,6 +3183,7 @@ __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int
                 nnear += all;
                 __syncthreads();
             }
+            KSTAMP(32);
             // sum the coefficients over the block, PH at a time: 16 threads per
             // coefficient, 16 values each, then a butterfly over the 16 lanes
 #pragma unroll
@@ -3194,6 +3202,7 @@ __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int
                 }
                 __syncthreads();
             }
+            KSTAMP(33);
             if (nnear > near_cap) {
 #pragma unroll
                 for (int i = 0; i < NPT; ++i) sup[i] = sup_retained_direct<true>(xv[i], prm, P);
@@ -3232,6 +3241,7 @@ __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int
         }
         __syncthreads();  // LDS reuse by the next tile
     }
+    KSTAMP(34);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
     if (lane == 0) wacc[wv] = acc;
@@ -3242,6 +3252,7 @@ __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int
         for (int k = 0; k < NW; ++k) tot += wacc[k];
     }
     mse_publish_fold<BS>(a, w, s, part, nparts, tot, kept_n, red);
+    KSTAMP(35);
 }
 
 __device__ __forceinline__ void mse_panic_out(const BatchArgs& a, int s) {

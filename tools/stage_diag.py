@@ -41,7 +41,7 @@ for _ in range(3):
     torch.cuda.synchronize()
 d = diag[STAMPS:].cpu().tolist()
 groups = {"select": range(10, 19), "peaks": range(0, 5), "fit_dpp": range(20, 24),
-          "mse": range(30, 34), "window_mean": [45, 46, 40, 41, 42], "window_var": [55, 56, 50, 51, 52]}
+          "mse": range(30, 36), "window_mean": [45, 46, 40, 41, 42], "window_var": [55, 56, 50, 51, 52]}
 for name, r in groups.items():
     v = [d[k] for k in r]
     if not any(v):
