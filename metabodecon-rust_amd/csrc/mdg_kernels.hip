@@ -1236,12 +1236,13 @@ __device__ __forceinline__ bool in_ignore(int v, const int64_t* pairs, int n) {
     return k >= 0 && v < pairs[2 * k + 1];
 }
 
-// The peaks of one mask word (64 points), in centre order: borders by bit scans,
-// the detector-only and ignore-region filters. Counts the bordered peaks; returns
-// the kept ones, writing them at out.. when WRITE.
+// The peaks of one mask word (64 points) whose centre bits are in sel, in centre
+// order: borders by bit scans, the detector-only and ignore-region filters. Counts
+// the bordered peaks; returns the kept ones, writing them at out.. when WRITE.
 template <bool WRITE>
-__device__ __forceinline__ int word_peaks(const BatchArgs& a, const Workspace& w, int s, int wd,
-                                          int detector_only, int* bordered, size_t out) {
+__device__ __forceinline__ int word_peaks(const BatchArgs& a, const Workspace& w, int s, int wd, uint64_t sel,
+                                          int detector_only, int* bordered, size_t out,
+                                          int* pk = nullptr, int pcap = 0, int po = 0) {
     const int N = a.N, W = w.W;
     const uint64_t* mc = w.masks + (size_t)s * 3 * W;
     const uint64_t* mr = mc + W;
@@ -1251,7 +1252,7 @@ __device__ __forceinline__ int word_peaks(const BatchArgs& a, const Workspace& w
     const int64_t sbi0 = w.sbi[2 * s], sbi1 = w.sbi[2 * s + 1];
     // the word and its neighbours' border masks in one round trip; a border farther
     // than the neighbouring word falls back to the scans over memory
-    uint64_t bits = mc[wd];
+    uint64_t bits = mc[wd] & sel;
     const uint64_t r0 = mr[wd], r1 = wd + 1 < W ? mr[wd + 1] : 0;
     const uint64_t l0 = ml[wd], l1 = wd > 0 ? ml[wd - 1] : 0;
     const int lim_r = N - 3, lim_l = 2;
@@ -1284,6 +1285,11 @@ __device__ __forceinline__ int word_peaks(const BatchArgs& a, const Workspace& w
             w.det_l[out + kept] = l;
             w.det_c[out + kept] = c;
             w.det_r[out + kept] = r;
+            if (pk && po + kept < pcap) {  // the chunk's copy for its scoring (LDS)
+                pk[po + kept] = l;
+                pk[pcap + po + kept] = c;
+                pk[2 * pcap + po + kept] = r;
+            }
         }
         ++kept;
     }
@@ -1292,16 +1298,18 @@ __device__ __forceinline__ int word_peaks(const BatchArgs& a, const Workspace& w
 
 // ScorerMinimumSum::score_peak (scorer.rs:65-75): min(sum |D[l..=c]|, sum
 // |D[c..=r]|) with D[k] = (y[k-1] - 2 y[k]) + y[k+1] of the smoothed row, both
-// sums left folds in k order. The values of a chunk of 8 ticks are loaded
-// together (clamped addresses): one memory latency per 8 ticks, not per tick.
+// sums left folds in k order. The values of a chunk of 16 ticks are loaded
+// together (clamped addresses): one memory latency per 16 ticks, not per tick
+// (p99 of a blood spectrum's peak widths is 12 ticks, its widest 63).
 __device__ __forceinline__ double score_peak(const double* __restrict__ sm, int N, int l, int c, int r) {
+    constexpr int CH = 16;
     double left = -0.0, right = -0.0;
-    for (int k0 = l; k0 <= r; k0 += 8) {
-        double y[10];  // y[k0-1 .. k0+8]
+    for (int k0 = l; k0 <= r; k0 += CH) {
+        double y[CH + 2];  // y[k0-1 .. k0+CH]
 #pragma unroll
-        for (int u = 0; u < 10; ++u) y[u] = sm[min(max(k0 - 1 + u, 0), N - 1)];
+        for (int u = 0; u < CH + 2; ++u) y[u] = sm[min(max(k0 - 1 + u, 0), N - 1)];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < CH; ++u) {
             const int k = k0 + u;
             if (k <= r) {
                 const double d = fabs((y[u] - 2.0 * y[u + 1]) + y[u + 2]);
@@ -1313,12 +1321,28 @@ __device__ __forceinline__ double score_peak(const double* __restrict__ sm, int 
     return fmin(left, right);
 }
 
-// K3 per chunk of WORDS mask words (one word per thread, many workgroups per
-// spectrum: a single-workgroup version took 46-53 us at N = 131072). Large batches
-// take chunks of 256 words on 1024 threads; small ones chunks of 64 words on 256
-// threads, four times the workgroups per spectrum (a B = 1 launch is otherwise 8
-// workgroups on 8 CUs, each scoring ~2000 peaks). The slots are laid out for the
-// finer chunking (kPkSlotWords, mdg_common.hpp) whichever is launched.
+// score_peak over a staged copy of the row: ys[i] = sm[i + lo], l - 1 .. r + 1 inside
+// it; the same operations in the same order
+__device__ __forceinline__ double score_peak_lds(const double* ys, int lo, int l, int c, int r) {
+    double left = -0.0, right = -0.0;
+    double ym = ys[l - 1 - lo], y0 = ys[l - lo];
+    for (int k = l; k <= r; ++k) {
+        const double yp = ys[k + 1 - lo];
+        const double d = fabs((ym - 2.0 * y0) + yp);
+        if (k <= c) left += d;
+        if (k >= c) right += d;
+        ym = y0;
+        y0 = yp;
+    }
+    return fmin(left, right);
+}
+
+// K3 per chunk of WORDS mask words (many workgroups per spectrum: a
+// single-workgroup version took 46-53 us at N = 131072). Large batches take chunks
+// of 256 words on 1024 threads; small ones chunks of 64 words on 256 threads, four
+// times the workgroups per spectrum (a B = 1 launch is otherwise 8 workgroups on 8
+// CUs, each scoring ~2000 peaks). The slots are laid out for the finer chunking
+// (kPkSlotWords, mdg_common.hpp) whichever is launched.
 // K3 in one pass (decoupled look-back): every chunk counts its peaks, publishes
 // {bordered, kept} in its slot of w.peak_cnt (cleared by k_flags), then reads the
 // slots of all chunks of its spectrum -- they publish before they wait, so one
@@ -1326,21 +1350,47 @@ __device__ __forceinline__ double score_peak(const double* __restrict__ sm, int 
 // chunks before it. Replaces k_peaks_count + k_peaks_write (one launch and one
 // word scan fewer).
 constexpr unsigned long long kPkValid = 1ull << 62;
-// BS threads per chunk: the first WORDS own one mask word each; all of them score
-// the chunk's peaks afterwards (four times the threads for that part)
+// BS = 4 WORDS threads per chunk: four per mask word; all of them score the chunk's
+// peaks afterwards
 template <int WORDS, int BS>
 __global__ __launch_bounds__(BS) void k_peaks(BatchArgs a, Workspace w, int detector_only, int score) {
-    static_assert(WORDS % kPkSlotWords == 0 && WORDS <= BS, "chunk shape");
+    static_assert(WORDS % kPkSlotWords == 0 && BS == 4 * WORDS, "chunk shape");
     const int s = blockIdx.y, chunk = blockIdx.x;
     __shared__ int lds_i[BS / 64 + 1];
     __shared__ long long lds_l[BS / 64 + 1];
+    // fine chunks (small batches, latency-bound) stage their stretch of the smoothed
+    // row, MARG ticks either side, and their peaks in LDS for the scoring: its loads
+    // then overlap the word pass instead of following the peak writes (round 4:
+    // 12k of a B = 1 launch's 36k cycles were the scoring's two memory round trips)
+    constexpr bool STAGE = WORDS == 64;
+    constexpr int SPAN = WORDS * 64, MARG = 64, SN = STAGE ? SPAN + 2 * MARG : 1;
+    constexpr int PCAP = STAGE ? SPAN / 2 : 1;  // centres are strict minima: <= SPAN / 2
+    constexpr int PER = STAGE ? (SN + BS - 1) / BS : 1;
+    __shared__ double ys[SN];
+    __shared__ int pk[3 * PCAP];
     if (w.status[s]) return;  // uniform per spectrum: no chunk waits for a returned one
     KSTAMP(0);
+    const double* __restrict__ sm = w.smooth_ptr + (size_t)s * w.smooth_stride;
+    const int lo = chunk * SPAN - MARG;
+    double stv[PER];
+    if constexpr (STAGE) {
+#pragma unroll
+        for (int u = 0; u < PER; ++u) stv[u] = sm[min(max(lo + u * BS + (int)threadIdx.x, 0), a.N - 1)];
+    }
     const int nch = (w.W + WORDS - 1) / WORDS;
     unsigned long long* slot = (unsigned long long*)w.peak_cnt + (size_t)s * peak_slots(w.W);
-    const int wd = chunk * WORDS + threadIdx.x;
+    // four threads per mask word, each the peaks centred in 16 of its bits: thread
+    // order is centre order, and the serial per-peak work a thread does is a
+    // quarter of a word's (round 4: one thread per word, 4.5 us of a B = 1 launch)
+    const int wd = chunk * WORDS + (threadIdx.x >> 2);
+    const uint64_t sel = 0xffffull << (16 * (threadIdx.x & 3));
     int bordered = 0, kept = 0;
-    if ((int)threadIdx.x < WORDS && wd < w.W) kept = word_peaks<false>(a, w, s, wd, detector_only, &bordered, 0);
+    if (wd < w.W) kept = word_peaks<false>(a, w, s, wd, sel, detector_only, &bordered, 0);
+    if constexpr (STAGE) {
+#pragma unroll
+        for (int u = 0; u < PER; ++u)
+            if (u * BS + (int)threadIdx.x < SN) ys[u * BS + threadIdx.x] = stv[u];
+    }
     KSTAMP(1);
     int total;
     const int o = block_exclusive_scan<BS>(kept, lds_i, &total);
@@ -1384,14 +1434,21 @@ __global__ __launch_bounds__(BS) void k_peaks(BatchArgs a, Workspace w, int dete
     if (chunk == 0 && threadIdx.x == 0) w.det_count[s] = (int32_t)k_all;
     KSTAMP(2);
     const size_t b0 = (size_t)s * w.capD + before;
-    if (kept) word_peaks<true>(a, w, s, wd, detector_only, &bordered, b0 + o);
+    if (kept) word_peaks<true>(a, w, s, wd, sel, detector_only, &bordered, b0 + o, STAGE ? pk : nullptr, PCAP, o);
     if (detector_only || !score) return;
     KSTAMP(3);
     // k_scores' work for this chunk's peaks, spread evenly over the block
     __syncthreads();  // the peaks above, written by other threads of the block
-    const double* __restrict__ sm = w.smooth_ptr + (size_t)s * w.smooth_stride;
-    for (int p = threadIdx.x; p < total; p += BS)
-        w.scores[b0 + p] = score_peak(sm, a.N, w.det_l[b0 + p], w.det_c[b0 + p], w.det_r[b0 + p]);
+    if (STAGE && total <= PCAP) {
+        for (int p = threadIdx.x; p < total; p += BS) {
+            const int l = pk[p], c = pk[PCAP + p], r = pk[2 * PCAP + p];
+            w.scores[b0 + p] = l - 1 >= lo && r + 1 < lo + SN ? score_peak_lds(ys, lo, l, c, r)
+                                                               : score_peak(sm, a.N, l, c, r);
+        }
+    } else {
+        for (int p = threadIdx.x; p < total; p += BS)
+            w.scores[b0 + p] = score_peak(sm, a.N, w.det_l[b0 + p], w.det_c[b0 + p], w.det_r[b0 + p]);
+    }
     KSTAMP(4);
 }
 
@@ -3525,10 +3582,12 @@ void launch_flags(const BatchArgs& a, const Workspace& w, hipStream_t st) {
 }
 const char* launch_peaks(const BatchArgs& a, const Workspace& w, int detector_only, hipStream_t st) {
     // k_peaks scores the peaks it writes (scorer.rs:65-75) for the selector. Fine
-    // chunks while the batch gives fewer than 64 workgroups of 256-word chunks
-    // (B <= 7 at N = 131072); MDG_PEAKS = fine | coarse forces one (tests)
+    // (staged) chunks up to 512 workgroups of 64-word chunks (B <= 16 at N = 131072:
+    // blood, 13.2 / 12.9 / 15.4 / 17.5 us at B = 1 / 4 / 8 / 16 against the coarse
+    // chunks' 21.3 / 21.9 / 22.9 / 23.1; synthetic B = 64: 59.8 against 52.6, B = 256:
+    // 230 against 216); MDG_PEAKS = fine | coarse forces one (tests)
     const char* force = std::getenv("MDG_PEAKS");
-    const bool fine = force ? std::string(force) == "fine" : (size_t)cdiv(w.W, 256) * a.B < 64;
+    const bool fine = force ? std::string(force) == "fine" : (size_t)cdiv(w.W, 64) * a.B <= 512;
     if (fine) {
         launch_k(k_peaks<64, 256>, dim3(cdiv(w.W, 64), a.B), dim3(256), 0, st, a, w, detector_only, 1);
         return "k_flags+k_peaks<64>";

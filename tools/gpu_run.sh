@@ -17,6 +17,8 @@
 #                tools/ubench/fit_diag over term-fold shapes (build fit_diag first)
 #   twfdiag      the batch-wide tile-list fit (k_fit_sup_twf) against the (G, B) grids
 #   timeline     rocprofv3 kernel timelines of one blood call at B = 1 and 16
+#   peaksdiag    k_peaks fine against coarse chunks at B = 1, 4, 8, 16 (kernel traces)
+#   synth:<B>    kernel stats of a synthetic device batch of B (tools/synth_batch.py)
 #   c0diag       configs[0]: host/device breakdown (tools/c0_breakdown.py) and the phase
 #                stamps of one pipeline (tools/stage_diag.py; the diag library first:
 #                make -C metabodecon-rust_amd diag && cp .../build/libmdgpu_diag.so tools/ubench/)
@@ -54,6 +56,11 @@ for step in "$@"; do
         [ $l -ge $q ] || cfgs+=("q${q}_l$l GPU_MAX_HW_QUEUES=$q MDGPU_LANES=$l --c4-only")
       done; done
       run c4 1200 bash tools/ab.sh c4 "${cfgs[@]}" ;;
+    c4lanes)
+      # configs[4]: one lane (one batch of 16) against two (8 + 8), three rounds
+      ROUNDS=3 run c4lanes 1200 bash tools/ab.sh c4lanes "q4_l1 GPU_MAX_HW_QUEUES=4 MDGPU_LANES=1 --c4-only" \
+        "q4_l2 GPU_MAX_HW_QUEUES=4 MDGPU_LANES=2 --c4-only" "q32_l1 GPU_MAX_HW_QUEUES=32 MDGPU_LANES=1 --c4-only" \
+        "q32_l2 GPU_MAX_HW_QUEUES=32 MDGPU_LANES=2 --c4-only" ;;
     fitdiag)
       run pmc_fit 600 bash tools/pmc_fit.sh 16 16 992 tw7,tf,plain
       run fit_shapes_b16 120 tools/ubench/fit_diag 16 992 twf,twf1,tw7,s63.1.7@98,s63.2.7@16,s63.2.7@48,s63.1.7@16,s60.1.15@16,s60.1.15@50,s60.2.6@16,s63.2.3@16,s48.1.6@62,s63.1.9@98
@@ -112,6 +119,26 @@ for step in "$@"; do
         f=$(find gpurun_out/${tag}_b1 -name run_kernel_trace.csv | head -1)
         python tools/blood_trace.py --summary "$f" | grep -E "mse|select|total" | tee -a $log
       done ;;
+    peaksdiag|peaksbig)
+      # k_peaks' fine (staged) and coarse chunkings at small batches
+      [ "$step" = peaksdiag ] && for B in 1 4 8 16; do for m in fine coarse; do
+        tag=peaks_${m}_b$B
+        MDG_PEAKS=$m timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/$tag -o run -- python3 tools/blood_trace.py $B > gpurun_out/run/$tag.log 2>&1 || { echo "STOP $tag"; exit 3; }
+        f=$(find gpurun_out/$tag -name run_kernel_trace.csv | head -1)
+        echo "== $tag $(python tools/blood_trace.py --summary "$f" | grep -E "peaks")" | tee -a $log
+      done; done
+      for B in 64 256; do for m in fine coarse; do
+        tag=peaks_${m}_s$B
+        MDG_PEAKS=$m timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$tag -o run -- python3 tools/synth_batch.py $B 3 > gpurun_out/run/$tag.log 2>&1 || { echo "STOP $tag"; exit 3; }
+        f=$(find gpurun_out/$tag -name run_kernel_stats.csv | head -1)
+        echo "== $tag $(grep k_peaks "$f" | cut -c1-200)" | tee -a $log
+      done; done ;;
+    synth:*)
+      # per-kernel stats of three pipelines of one synthetic device batch of B
+      B=${step#synth:}; tag=synth_b$B
+      timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$tag -o run -- python3 tools/synth_batch.py $B 3 > gpurun_out/run/$tag.log 2>&1 || { echo "STOP $tag"; exit 3; }
+      f=$(find gpurun_out/$tag -name run_kernel_stats.csv | head -1)
+      cut -d, -f1-4 "$f" | tee -a $log ;;
     c0diag)
       run c0_breakdown 300 python tools/c0_breakdown.py 200
       run stage_diag_b1 120 python tools/stage_diag.py 1
