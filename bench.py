@@ -941,9 +941,10 @@ def bruker_set(args, nat, torch, dev):
                      len(spectra), "read_s": read_s, "kept_peaks": counts,
                      "verified": f"{ok}/{len(res)} (goldens)", "roofline": roof,
                      "path": "Spectrum.read_bruker_set + Deconvoluter.par_deconvolute_spectra "
-                             "(the set cut into Deconvoluter.LANES chunks, one batched pipeline "
-                             "per lane context, concurrently), host buffers (PCIe inside the "
-                             "timed region)"}
+                             "(sets of up to Deconvoluter.ONE_LANE_UPTO spectra one batched "
+                             "pipeline, larger ones cut into Deconvoluter.LANES chunks on lane "
+                             "contexts, concurrently), host buffers (PCIe inside the timed region: "
+                             "the pipeline reads the page-locked compact rows itself)"}
 
 
 # ------------------------------------------------------------------ multi-rank configs
@@ -1235,7 +1236,8 @@ def main():
     if args.c4_only:
         _, c4 = bruker_set(args, nat, torch, dev)
         c4["hw_queues"] = os.environ.get("GPU_MAX_HW_QUEUES", "unset (HIP default 4)")
-        c4["lanes"] = __import__("metabodecon").Deconvoluter.LANES
+        D = __import__("metabodecon").Deconvoluter
+        c4["lanes"] = 1 if 16 <= D.ONE_LANE_UPTO else D.LANES
         print(json.dumps(c4), flush=True)
         return
 

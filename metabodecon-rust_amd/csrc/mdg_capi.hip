@@ -91,6 +91,11 @@ struct mdg_ctx {
     // staging for the host-pointer API
     Buffer st_x, st_y, st_sb, st_out, st_cnt, st_mse, st_status, st_L, st_sup, st_flag;
     Buffer st_raw, st_desc;  // mdg_deconvolute_rows_i32: int32 rows and their descriptors
+    // mdg_deconvolute_rows_i32 with page-locked rows: the chain launch decodes them
+    // from host memory (BatchArgs::dec_rows); per-chunk flags, the call's generation
+    Buffer dec_flags;
+    int dec_gen = 0;
+    bool dec_next = false;  // set by the upload: the next pipeline decodes the rows
     // page-locked host ring for mdg_deconvolute_rows: the rows are gathered into a
     // slot and sent with one asynchronous DMA per slot (upload_rows)
     void* ring[2] = {nullptr, nullptr};
@@ -198,6 +203,7 @@ struct PinnedPool {
     char* cur = nullptr;                                // bump pointer in the newest slab
     size_t cur_left = 0;
     size_t pinned = 0;                                  // bytes of all slabs
+    bool uva = true;  // every slab's device address is its host address (kernels may read the rows)
 };
 PinnedPool& pinned_pool() {
     static PinnedPool* p = new PinnedPool();  // never destroyed: blocks may be freed at exit
@@ -238,6 +244,8 @@ int pinned_alloc(int device, size_t bytes, void** out) {
         const hipError_t e = hipHostMalloc(&s, slab, hipHostMallocPortable);
         (void)hipSetDevice(prev);
         if (e != hipSuccess) return MDG_ERR_OUT_OF_MEMORY;
+        void* dp = nullptr;
+        if (hipHostGetDevicePointer(&dp, s, 0) != hipSuccess || dp != s) P.uva = false;
         if (P.cur_left) P.free_blocks[P.cur_left].push_back(P.cur);  // the old slab's tail
         P.cur = (char*)s;
         P.cur_left = slab;
@@ -262,11 +270,12 @@ int pinned_free(void* p) {
     return MDG_OK;
 }
 
-// every [rows[i], rows[i] + bytes) inside one live page-locked block
-bool pinned_rows(const void* const* rows, size_t b, size_t bytes) {
+// every [rows[i], rows[i] + bytes) inside one live page-locked block (and, with
+// device_readable, the blocks readable by kernels at their host addresses)
+bool pinned_rows(const void* const* rows, size_t b, size_t bytes, bool device_readable = false) {
     PinnedPool& P = pinned_pool();
     std::lock_guard<std::mutex> g(P.mu);
-    if (P.live.empty()) return false;
+    if (P.live.empty() || (device_readable && !P.uva)) return false;
     for (size_t i = 0; i < b; ++i) {
         const uintptr_t a = (uintptr_t)rows[i];
         auto it = P.live.upper_bound(a);
@@ -472,6 +481,23 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     const char* prep_env = std::getenv("MDG_PREP");
     const bool fused_prep = ma && !panic_shape && !skip_smooth && !(prep_env && std::string(prep_env) == "separate") &&
                             reps("prep") == 1 && smooth_uses_chain(a, w, sm_it, sm_ws);
+    if (a.dec_rows) {
+        // rows still in host memory (mdg_deconvolute_rows_i32): the chain launch
+        // decodes them while it smooths (flags of this call's generation), any other
+        // smoother after a decode launch of their own
+        const size_t need = (size_t)a.B * kDecChunks * 4;
+        if (c->dec_flags.bytes < need || c->dec_gen >= INT32_MAX - 1) {
+            if ((rc = ensure(c->dec_flags, need))) return rc;
+            HIPCHK(hipMemsetAsync(c->dec_flags.p, 0, c->dec_flags.bytes, st));
+            c->dec_gen = 0;
+        }
+        a.dec_gen = ++c->dec_gen;
+        w.dec_flags = (int32_t*)c->dec_flags.p;
+        if (!fused_prep) {
+            StageTimer t(c, ST_PREP);
+            launch_decode_rows_zc(a, st);
+        }
+    }
     if (!fused_prep) {
         StageTimer t(c, ST_PREP);
         for (int r = reps("prep"); r > 0; --r) launch_prep(a, w, st);
@@ -1191,7 +1217,7 @@ static int batch_host(mdg_ctx* c, size_t b, size_t n, bool shared_x, Upload uplo
     int rc;
     if ((rc = ensure(c->st_x, xrows * n * 8))) return rc;
     if ((rc = ensure(c->st_y, b * n * 8))) return rc;
-    if ((rc = ensure(c->st_sb, b * 48))) return rc;  // [sb: 2b doubles][descriptors: 4b]
+    if ((rc = ensure(c->st_sb, b * 56))) return rc;  // [sb: 2b doubles][descriptors: 4b][row table: b]
     if ((rc = ensure(c->st_out, std::max<size_t>(1, b * cap) * 24))) return rc;
     // the per-spectrum results in one device row, [mse: 8 b][counts: 4 b][statuses:
     // 4 b] like the host scratch below, so they come back in one copy
@@ -1206,10 +1232,10 @@ static int batch_host(mdg_ctx* c, size_t b, size_t n, bool shared_x, Upload uplo
     // (above 64 MiB of guessed rows, every spectrum's rows are copied on their own)
     size_t guess = std::min(cap, c->rows_guess);
     if (b * guess * 24 > ((size_t)64 << 20)) guess = 0;
-    // page-locked scratch: [sb: 16 b][the upload's own descriptors: 32 b
-    // (mdg_deconvolute_rows_i32)][mse: 8 b][counts: 4 b][statuses: 4 b][the guessed
-    // result rows: 24 guess b]
-    const size_t hs_need = b * 64 + b * guess * 24;
+    // page-locked scratch: [sb: 16 b][the upload's own descriptors: 32 b and row
+    // table: 8 b (mdg_deconvolute_rows_i32)][mse: 8 b][counts: 4 b][statuses: 4 b]
+    // [the guessed result rows: 24 guess b]
+    const size_t hs_need = b * 72 + b * guess * 24;
     if (c->hsmall_busy) {
         HIPCHK(hipStreamSynchronize(st));
         c->hsmall_busy = false;
@@ -1225,10 +1251,10 @@ static int batch_host(mdg_ctx* c, size_t b, size_t n, bool shared_x, Upload uplo
         c->hsmall_bytes = want;
     }
     double* h_sb = (double*)c->hsmall;
-    double* h_mse = h_sb + 6 * b;
+    double* h_mse = h_sb + 7 * b;
     int32_t* h_cnt = (int32_t*)(h_mse + b);
     int32_t* h_st = h_cnt + b;
-    mdg_lorentzian* h_rows = (mdg_lorentzian*)(h_sb + 8 * b);
+    mdg_lorentzian* h_rows = (mdg_lorentzian*)(h_sb + 9 * b);
     c->hsmall_busy = true;
     // From here on DMAs may read the caller's page-locked rows (upload_rows sends
     // mdg_host_alloc rows without copying them): a failure must not return while they
@@ -1240,6 +1266,7 @@ static int batch_host(mdg_ctx* c, size_t b, size_t n, bool shared_x, Upload uplo
     };
     std::memcpy(h_sb, sb, b * 16);
     bool sent_sb = false;
+    c->dec_next = false;
     if ((rc = upload(dx, dy, st, &sent_sb))) return fail(rc);
     hipError_t he = hipSuccess;
     if (!sent_sb) he = hipMemcpyAsync(c->st_sb.p, h_sb, b * 16, hipMemcpyHostToDevice, st);
@@ -1248,6 +1275,11 @@ static int batch_host(mdg_ctx* c, size_t b, size_t n, bool shared_x, Upload uplo
     if ((rc = fill_args(c, a, b, n, dx, shared_x ? 0 : n, dy, n, (const double*)c->st_sb.p, ignore,
                         n_ignore, (double*)c->st_out.p, cap, d_cnt, d_mse, d_st)))
         return fail(rc);
+    if (c->dec_next) {  // the rows are decoded by the pipeline (run_pipeline)
+        a.dec_rows = (const int32_t* const*)((const double*)c->st_sb.p + 6 * b);
+        a.dec_desc = (const double*)c->st_sb.p + 2 * b;
+        c->dec_next = false;
+    }
     if ((rc = run_pipeline(c, a, s))) return fail(rc);
     // Only the rows the spectra filled travel back (cap is usually N/2 + 2 rows, 1.5
     // MiB per 131072-point spectrum, against ~24 KiB of Lorentzians), and their count
@@ -1357,11 +1389,15 @@ int mdg_deconvolute_rows_i32(mdg_ctx* c, size_t b, size_t n, const double* axes,
         if (axes[3 * i + 2] == 0.0 || !std::isfinite(y_scale[i])) return MDG_INVALID_ARGUMENT;
         shared = shared && std::memcmp(axes + 3 * i, axes, 3 * sizeof(double)) == 0;
     }
+    // rows in mdg_host_alloc memory are decoded by the pipeline straight from host
+    // memory, the chain smoother starting on the first chunks while the rest are
+    // read (chain_decode; MDG_DEC_OVERLAP=0: DMA and decode first, as other rows)
+    const char* ov = std::getenv("MDG_DEC_OVERLAP");
+    const bool zc = !(ov && ov[0] == '0') && pinned_rows((const void* const*)y_rows, b, n * 4, true);
     auto upload = [&](double* dx, double* dy, hipStream_t st, bool* sent_sb) -> int {
         int rc;
-        if ((rc = ensure(c->st_raw, b * n * 4))) return rc;
-        if ((rc = upload_rows(c, st, (char*)c->st_raw.p, (const void* const*)y_rows, b, n * 4))) return rc;
-        // batch_host's scratch holds [sb: 2b][descriptors: 4b] doubles: one copy sends both
+        // batch_host's scratch holds [sb: 2b][descriptors: 4b][row table: b] doubles:
+        // one copy sends them all
         double* h = (double*)c->hsmall + 2 * b;
         for (size_t i = 0; i < b; ++i) {
             h[4 * i] = axes[3 * i];
@@ -1369,6 +1405,16 @@ int mdg_deconvolute_rows_i32(mdg_ctx* c, size_t b, size_t n, const double* axes,
             h[4 * i + 2] = axes[3 * i + 2];
             h[4 * i + 3] = y_scale[i];
         }
+        if (zc) {
+            const int32_t** tab = (const int32_t**)(h + 4 * b);
+            for (size_t i = 0; i < b; ++i) tab[i] = y_rows[i];
+            HIPCHK(hipMemcpyAsync(c->st_sb.p, c->hsmall, b * 56, hipMemcpyHostToDevice, st));
+            *sent_sb = true;
+            c->dec_next = true;
+            return MDG_OK;
+        }
+        if ((rc = ensure(c->st_raw, b * n * 4))) return rc;
+        if ((rc = upload_rows(c, st, (char*)c->st_raw.p, (const void* const*)y_rows, b, n * 4))) return rc;
         HIPCHK(hipMemcpyAsync(c->st_sb.p, c->hsmall, b * 48, hipMemcpyHostToDevice, st));
         *sent_sb = true;
         launch_decode_rows_i32((const int32_t*)c->st_raw.p, (const double*)c->st_sb.p + 2 * b, (int)b,

@@ -297,10 +297,20 @@ __device__ __forceinline__ int find_prev_bit(const uint64_t* __restrict__ m, int
 // indices, MSE-region checks, range flags, counters and status. k_prep runs it for
 // every spectrum; with the chain smoother the pass-0 workgroup of each spectrum
 // runs it instead (one launch fewer), no other kernel of that launch reading it.
+// x_i of a compact row (k_decode_rows_i32's operations): d = {maximum, width, divisor}
+__device__ __forceinline__ double dec_x(const double* d, int64_t i) {
+    return d[0] - ((double)i * d[1]) / d[2];
+}
+
 __device__ __forceinline__ void prep_spectrum(const BatchArgs& a, const Workspace& w, int s) {
+    // rows the chain launch is still decoding (a.dec_rows): the axis's end points from
+    // its descriptor, the values the decoders write
     const double* x = a.x + (size_t)s * a.x_stride;
-    const double x0 = x[0];
-    const double step = x[1] - x[0];
+    const double* xd = a.dec_desc ? a.dec_desc + 4 * (a.x_stride ? s : 0) : nullptr;
+    const double x0 = xd ? dec_x(xd, 0) : x[0];
+    const double x1 = xd ? dec_x(xd, 1) : x[1];
+    const double xl = xd ? dec_x(xd, a.N - 1) : x[a.N - 1];
+    const double step = x1 - x0;
     const double sb0 = a.sb[2 * s], sb1 = a.sb[2 * s + 1];
     const int64_t bi0 = as_index(floor((sb0 - x0) / step));
     const int64_t bi1 = as_index(ceil((sb1 - x0) / step));
@@ -344,7 +354,7 @@ __device__ __forceinline__ void prep_spectrum(const BatchArgs& a, const Workspac
     }
     w.mse_panic[s] = panic;
     // the axis is monotone (Spectrum invariant): its end points bound every x
-    w.x_ok[s] = x_fast_ok(x0) && x_fast_ok(x[a.N - 1]);
+    w.x_ok[s] = x_fast_ok(x0) && x_fast_ok(xl);
     w.unsafe[4 * s] = 0;
     w.unsafe[4 * s + 1] = 0;
     w.unsafe[4 * s + 2] = 0;
@@ -781,6 +791,70 @@ __device__ __forceinline__ void chain_l2_pull(const double* p, int cnt) {
         : "v20", "v21", "v22", "v23", "v24", "v25", "s40", "scc", "memory");
 }
 
+// Rows decoded while the chain smooths them (mdg_deconvolute_rows_i32 with
+// page-locked rows): the chain launch's first ndec workgroups read the int32 rows
+// straight from host memory and write y_i = raw_i * scale (k_decode_rows_i32's
+// operation) chunk by chunk, kDecChunks chunks per row, chunk-major over the batch
+// (the first chunks of every row first), each chunk published
+// (Workspace::dec_flags = dec_gen) the way a chain pass publishes its output
+// blocks: agent-scope stores, vmcnt(0), then the flag; pass 0's feeder polls the
+// flags. The x rows follow (the chain does not read them; prep_spectrum takes the
+// axis from its descriptor). Decoders wait for nothing, so they always finish;
+// the chain waits for them within its spin limits.
+__device__ __forceinline__ int dec_block_chunk(int nIB) { return (nIB + kDecChunks - 1) / kDecChunks; }
+__device__ __forceinline__ void chain_decode(const BatchArgs& a, const Workspace& w, int d, int ndec) {
+    const int N = a.N, B = a.B, NT = blockDim.x, tid = threadIdx.x;
+    const int pts = dec_block_chunk((N + kChainCB - 1) / kChainCB) * kChainCB;  // a multiple of 4
+    constexpr int U = 3;
+    for (int t = d; t < kDecChunks * B; t += ndec) {
+        const int c = t / B, s = t - c * B;
+        const int lo = c * pts, hi = min(N, lo + pts);
+        const int32_t* __restrict__ r = a.dec_rows[s];
+        const double sc = a.dec_desc[4 * s + 3];
+        double* yr = const_cast<double*>(a.y) + (size_t)s * a.y_stride;
+        // 16-byte host reads where the row allows them (lo is a multiple of 4)
+        const bool v4 = ((uintptr_t)r & 15) == 0;
+        const int n4 = v4 && hi > lo ? (hi - lo) >> 2 : 0;
+        for (int b4 = 0; b4 < n4; b4 += U * NT) {
+            int4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {  // all host reads in flight together
+                const int q = b4 + u * NT + tid;
+                v[u] = q < n4 ? ((const int4*)(r + lo))[q] : make_int4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int q = b4 + u * NT + tid;
+                if (q < n4) {
+                    double* o = yr + lo + 4 * q;
+                    __hip_atomic_store(o, (double)v[u].x * sc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(o + 1, (double)v[u].y * sc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(o + 2, (double)v[u].z * sc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(o + 3, (double)v[u].w * sc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+        }
+        for (int i = lo + 4 * n4 + tid; i < hi; i += NT)  // the rest (unaligned rows, the row's tail)
+            __hip_atomic_store(yr + i, (double)r[i] * sc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        // the whole of wave 0 publishes (a wave-uniform branch and value)
+        if (tid < 64)
+            __hip_atomic_store(w.dec_flags + (size_t)s * kDecChunks + c, a.dec_gen, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // x rows (read only by later launches): one row when the axis is shared
+    const int xrows = a.x_stride ? B : 1;
+    double* xr0 = const_cast<double*>(a.x);
+    for (int t = d; t < kDecChunks * xrows; t += ndec) {
+        const int c = t / xrows, s = t % xrows;
+        const int lo = c * pts, hi = min(N, lo + pts);
+        const double* xd = a.dec_desc + 4 * s;
+        double* xr = xr0 + (size_t)s * a.x_stride;
+        for (int i = lo + tid; i < hi; i += NT) xr[i] = dec_x(xd, i);
+    }
+}
+
 // EXCL: each wave claims the whole register file of its SIMD (256 arch + 256 acc
 // VGPRs), so a chain workgroup owns its CU outright. Small batches only (the
 // launcher requires B * passes <= kChainExclMax): with one workgroup per CU every
@@ -790,14 +864,19 @@ __device__ __forceinline__ void chain_l2_pull(const double* p, int cnt) {
 // k_fit_sup_tf launch lasts as long as its slowest workgroup).
 template <int WS, bool EXCL>
 __global__ __launch_bounds__(64 * (2 + kChainScalers)) void k_smooth_chain(BatchArgs a, Workspace w, int P,
-                                                                            int fused_prep) {
+                                                                            int fused_prep, int ndec) {
     if constexpr (EXCL) {
         asm volatile("v_mov_b32 v255, 0" ::: "v255");
         asm volatile("v_accvgpr_write_b32 a255, 0" ::: "a255");
     }
+    // the first ndec workgroups (a multiple of 8) decode the rows (chain_decode)
+    if ((int)blockIdx.x < ndec) {
+        chain_decode(a, w, blockIdx.x, ndec);
+        return;
+    }
     // workgroup id -> (spectrum, pass): the P passes of a spectrum share id % 8
     // (the XCD of round-robin dispatch), so their hand-offs stay in one L2
-    const int id = blockIdx.x;
+    const int id = blockIdx.x - ndec;
     const int x8 = id & 7, j8 = id >> 3;
     const int p = j8 % P, s = (j8 / P) * 8 + x8;
     if (s >= a.B) return;
@@ -915,7 +994,8 @@ __global__ __launch_bounds__(64 * (2 + kChainScalers)) void k_smooth_chain(Batch
         // scalar cache (kChainPrefetch blocks ahead of the chain) and publishes them
         int pf = 0;     // next input block to touch
         int ready = 0;  // in_ready published
-        int up = p == 0 ? nIB : 0;
+        // pass 0 of rows this launch decodes: the decoded chunks (dec_flags)
+        int up = p == 0 && ndec == 0 ? nIB : 0;
         int l2 = 0;  // next input block pulled into L2
         unsigned idle = 0;
         bool ok = true;
@@ -943,6 +1023,16 @@ __global__ __launch_bounds__(64 * (2 + kChainScalers)) void k_smooth_chain(Batch
             if (p > 0 && up < min(nIB, rd + kChainL2Ahead))
                 up = __hip_atomic_load(const_cast<int32_t*>(up_flag), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
+            if (p == 0 && ndec > 0 && up < min(nIB, rd + kChainL2Ahead)) {
+                // lane c reads chunk c's flag; the decoded prefix is the run of set
+                // flags from chunk 0 (kDecChunks == 64: one per lane)
+                static_assert(kDecChunks == 64, "one flag per feeder lane");
+                const int32_t f = __hip_atomic_load(w.dec_flags + (size_t)s * kDecChunks + lane, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+                const uint64_t nm = ~__ballot(f == a.dec_gen);
+                const int chunks = nm ? __builtin_ctzll(nm) : kDecChunks;
+                up = min(nIB, chunks * dec_block_chunk(nIB));
+            }
             // pull published full input blocks into L2 (16 per wait), so the
             // scalar-cache touches below hit L2 instead of HBM / the MALL
             // (every pass: without it, 11.7 / 12.3 / 12.5 cycles per tick, passes 0..2)
@@ -3512,12 +3602,16 @@ static const char* launch_chain(const BatchArgs& a, const Workspace& w, int iter
     const unsigned grid = 8u * (unsigned)iters * cdiv(a.B, 8);
     const char* excl_env = std::getenv("MDG_CHAIN_EXCL");  // 0 = never (measurements)
     const bool excl = (int)grid <= kChainExclMax && !(excl_env && excl_env[0] == '0');
+    // rows still in host memory (a.dec_rows; the pipeline fuses the prep then): 32
+    // decoders up to 4 spectra, 64 beyond (chain_decode; a multiple of 8 keeps the
+    // chain workgroups' XCD mapping)
+    const int ndec = a.dec_rows && fused_prep ? (a.B <= 4 ? 32 : 64) : 0;
     if (excl) {
-        launch_k((k_smooth_chain<WS, true>), dim3(grid), dim3(64 * (2 + kChainScalers)), 0, st,
-                           a, w, iters, fused_prep);
+        launch_k((k_smooth_chain<WS, true>), dim3(grid + ndec), dim3(64 * (2 + kChainScalers)), 0, st,
+                           a, w, iters, fused_prep, ndec);
     } else {
-        launch_k((k_smooth_chain<WS, false>), dim3(grid), dim3(64 * (2 + kChainScalers)), 0, st,
-                           a, w, iters, fused_prep);
+        launch_k((k_smooth_chain<WS, false>), dim3(grid + ndec), dim3(64 * (2 + kChainScalers)), 0, st,
+                           a, w, iters, fused_prep, ndec);
     }
     static const char* names[2][9] = {
         {"", "", "k_smooth_chain<2, false>", "k_smooth_chain<3, false>", "k_smooth_chain<4, false>",
@@ -3836,6 +3930,37 @@ void launch_decode_rows_i32(const int32_t* raw, const double* desc, int B, int64
     const unsigned gx = std::max(1u, std::min(cdiv(n, 1024), 128u));
     hipLaunchKernelGGL(k_decode_rows_i32, dim3(gx, B), dim3(256), 0, st, raw, desc, n, shared_x,
                        x_rows, y_rows);
+}
+// the same decode from the rows in host memory (BatchArgs::dec_rows), for pipelines
+// whose smoother cannot decode them while it runs (chain_decode)
+__global__ __launch_bounds__(256) void k_decode_rows_zc(BatchArgs a) {
+    const int s = blockIdx.y;
+    const double* d = a.dec_desc + 4 * s;
+    const int32_t* __restrict__ r = a.dec_rows[s];
+    double* yr = const_cast<double*>(a.y) + (size_t)s * a.y_stride;
+    double* xr = const_cast<double*>(a.x) + (size_t)s * a.x_stride;
+    const bool do_x = a.x_stride != 0 || s == 0;
+    constexpr int U = 8;
+    for (int64_t b0 = (int64_t)blockIdx.x * 256 * U; b0 < a.N; b0 += (int64_t)gridDim.x * 256 * U) {
+        int32_t v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {  // host reads in flight together
+            const int64_t i = b0 + u * 256 + threadIdx.x;
+            v[u] = i < a.N ? r[i] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = b0 + u * 256 + threadIdx.x;
+            if (i < a.N) {
+                yr[i] = (double)v[u] * d[3];
+                if (do_x) xr[i] = dec_x(d, i);
+            }
+        }
+    }
+}
+void launch_decode_rows_zc(const BatchArgs& a, hipStream_t st) {
+    const unsigned gx = std::max(1u, std::min(cdiv(a.N, 2048), 64u));
+    hipLaunchKernelGGL(k_decode_rows_zc, dim3(gx, a.B), dim3(256), 0, st, a);
 }
 
 }  // namespace mdg

@@ -30,6 +30,11 @@ struct BatchArgs {
     double* out_mse;
     int32_t* out_status;
     int contexts;         // engine contexts with a pipeline in the last 50 ms on the device, max 2 (kernel choice only)
+    // mdg_deconvolute_rows_i32 with page-locked rows: the pipeline decodes the rows
+    // into y / x itself, reading them from host memory (null: y and x hold them)
+    const int32_t* const* dec_rows;  // B host-mapped int32 rows (device copy of the table)
+    const double* dec_desc;          // B x {maximum, width, divisor, scale}
+    int dec_gen;                     // a decoded chunk's flag value in this call (Workspace::dec_flags)
 };
 
 // Context-owned device workspace (sized for the worst case of the batch shape).
@@ -89,6 +94,7 @@ struct Workspace {
     int32_t* chain_flags;     // B x P x 32: published output blocks of (s, p) (own 128-B line)
     int64_t chain_stride;
     int chain_P;              // passes the chain buffers hold (0 = not allocated)
+    int32_t* dec_flags;       // B x kDecChunks: chunk c of row s decoded when == BatchArgs::dec_gen
     // per-spectrum overrides (optimize_settings batches; null = the batch settings)
     const double* thr_s;      // B noise-score thresholds
     const int32_t* fit_iters_s;  // B fit iteration counts (<= the launched count)
@@ -98,6 +104,9 @@ struct Workspace {
 int64_t chain_stride_for(int N, int ws);
 size_t chain_bytes(int B, int N, int ws, int passes);
 bool chain_supported(int B, int N, int iters, int ws);
+// a.dec_rows decoded into a.y / a.x by a launch of its own (the pipeline does this
+// when the chain smoother cannot decode them while it runs)
+void launch_decode_rows_zc(const BatchArgs& a, hipStream_t st);
 
 // exact-order MSE of spectrum 0 of the last pipeline run over its MSE regions
 // (read on the device from the workspace: signal boundaries and ignore pairs)

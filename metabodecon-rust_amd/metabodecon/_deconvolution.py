@@ -434,6 +434,12 @@ class Deconvoluter:
     LANES = max(1, min(16, int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) - 1,
                        int(os.environ.get("MDGPU_LANES", "2") or 2)))
     CHUNK = 256  # spectra per batched call (the host staging of one call stays bounded)
+    # Sets of up to this many spectra of one length run as one batch on one context
+    # (unless MDGPU_LANES is set): since the pipeline decodes page-locked compact rows
+    # while the smoother runs (round 4), one batch of the 16 blood spectra takes
+    # 13.6-13.7k spectra/s in three rounds against 12.4-13.0k for two lanes of 8
+    # (tools/gpu_run.sh c4lanes, 4 and 32 hardware queues alike).
+    ONE_LANE_UPTO = 0 if os.environ.get("MDGPU_LANES") else 16
 
     def _run_one(self, ctx, sp: Spectrum, n: int, ign):
         """_run_batch for one spectrum with the ctypes arguments cached: the
@@ -555,7 +561,7 @@ class Deconvoluter:
         ign = self._ignore_array()
         from .distributed import shard_range
         for n, idx in by_n.items():
-            lanes_n = min(self.LANES, len(idx))
+            lanes_n = 1 if len(idx) <= self.ONE_LANE_UPTO else min(self.LANES, len(idx))
             k = max(lanes_n, -(-len(idx) // self.CHUNK))
             chunks = [idx[lo:hi] for lo, hi in (shard_range(len(idx), r, k) for r in range(k))]
             if lanes_n <= 1:

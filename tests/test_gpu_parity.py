@@ -182,6 +182,7 @@ def test_concurrent_lanes_and_release(monkeypatch):
     import metabodecon as md
     from metabodecon import _native as nat
     monkeypatch.setattr(md.Deconvoluter, "LANES", 16)
+    monkeypatch.setattr(md.Deconvoluter, "ONE_LANE_UPTO", 0)
     spectra = md.Spectrum.read_bruker_set(os.path.join(GOLDEN, "bruker", "blood"), 10, 10,
                                           (-2.2, 11.8))
     for rnd in range(2):
@@ -202,6 +203,7 @@ def test_chunked_lanes_bit_exact(monkeypatch):
     import metabodecon as md
     monkeypatch.setattr(md.Deconvoluter, "LANES", 2)
     monkeypatch.setattr(md.Deconvoluter, "CHUNK", 3)
+    monkeypatch.setattr(md.Deconvoluter, "ONE_LANE_UPTO", 0)
     spectra = md.Spectrum.read_bruker_set(os.path.join(GOLDEN, "bruker", "blood"), 10, 10,
                                           (-2.2, 11.8))
     decs = md.Deconvoluter().par_deconvolute_spectra(spectra)

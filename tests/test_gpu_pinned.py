@@ -50,6 +50,7 @@ def test_compact_pinned_pageable_and_mixed_rows_match_goldens(lanes, monkeypatch
     batch of 16 (1 lane) and two concurrent lanes of 8."""
     import metabodecon as md
     monkeypatch.setattr(md.Deconvoluter, "LANES", lanes)
+    monkeypatch.setattr(md.Deconvoluter, "ONE_LANE_UPTO", 0)
     read = _blood(md)
     assert all(s._raw is not None and _pinned(s._raw[0]) for s in read)
     _check(md.Deconvoluter().par_deconvolute_spectra(read), range(16))
@@ -119,6 +120,65 @@ def test_compact_rows_decode_bit_exact():
                                                                      s.smooth_window)), k
         assert np.array_equal(c_counts, f_counts) and np.array_equal(c_mse, f_mse)
         assert np.array_equal(c_out, f_out)
+
+
+@pytest.mark.parametrize("env", ["", "MDG_DEC_OVERLAP=0", "MDG_SMOOTH=pipe", "MDG_PREP=separate",
+                                 "MDG_CHAIN_EXCL=0"])
+def test_compact_rows_decode_paths(env, monkeypatch):
+    """Page-locked compact rows are decoded from host memory by the pipeline: by the
+    chain launch's decoders while pass 0 smooths the decoded chunks (default), or by
+    a decode launch of their own before any other smoother / a separate prep
+    (MDG_SMOOTH=pipe, MDG_PREP=separate); MDG_DEC_OVERLAP=0 sends them by DMA first.
+    Every path: the smoothed rows equal the oracle's and the results equal
+    mdg_deconvolute_rows' on the reader's f64 rows, at 1, 3 (distinct axes) and 16
+    spectra (two decoders per XCD)."""
+    import metabodecon as md
+    import oracle
+    if env:
+        k, v = env.split("=")
+        monkeypatch.setenv(k, v)
+    read = _blood(md)
+    ctx = nat.context()
+    s = md.Deconvoluter().settings
+    n = len(read[0])
+    cap = n // 2 + 2
+    for group in ([7], [0, 5, 9], list(range(16))):
+        spectra = [read[k] for k in group]
+        b = len(spectra)
+        sb = np.array([sp.signal_boundaries for sp in spectra], dtype=np.float64)
+
+        def run(compact):
+            out = np.zeros((b, cap, 3))
+            counts = np.zeros(b, dtype=np.uintp)
+            mse = np.zeros(b)
+            status = np.zeros(b, dtype=np.intc)
+            tail = (nat.ptr(out), cap, nat.ptr(counts, nat._szp), nat.ptr(mse),
+                    status.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+            if compact:
+                yr = np.array([sp._raw[0].ctypes.data for sp in spectra], dtype=np.uintp)
+                axes = np.array([sp._raw[2] for sp in spectra], dtype=np.float64)
+                scale = np.array([sp._raw[1] for sp in spectra], dtype=np.float64)
+                rc = nat.lib().mdg_deconvolute_rows_i32(
+                    ctx.handle, b, n, nat.ptr(axes), yr.ctypes.data_as(ctypes.POINTER(nat._i32p)),
+                    nat.ptr(scale), nat.ptr(sb), ctypes.byref(s), None, 0, *tail)
+            else:
+                xr = np.array([sp.chemical_shifts.ctypes.data for sp in spectra], dtype=np.uintp)
+                yr = np.array([sp.intensities.ctypes.data for sp in spectra], dtype=np.uintp)
+                rc = nat.lib().mdg_deconvolute_rows(
+                    ctx.handle, b, n, xr.ctypes.data_as(ctypes.POINTER(nat._dp)),
+                    yr.ctypes.data_as(ctypes.POINTER(nat._dp)), nat.ptr(sb), ctypes.byref(s),
+                    None, 0, *tail)
+            assert rc == 0 and not status.any(), (rc, status)
+            return out, counts, mse
+        with ctx.lock:
+            c_out, c_counts, c_mse = run(True)
+            smoothed = [ctx.last_smoothed(k, n) for k in range(b)]
+            f_out, f_counts, f_mse = run(False)
+        for k, sp in enumerate(spectra):
+            assert np.array_equal(smoothed[k], oracle.moving_average(sp.intensities, s.smooth_iterations,
+                                                                     s.smooth_window)), (group, k)
+        assert np.array_equal(c_counts, f_counts) and np.array_equal(c_mse, f_mse), group
+        assert np.array_equal(c_out, f_out), group
 
 
 def test_compact_rows_reject_bad_descriptors():

@@ -139,6 +139,18 @@ for step in "$@"; do
       timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$tag -o run -- python3 tools/synth_batch.py $B 3 > gpurun_out/run/$tag.log 2>&1 || { echo "STOP $tag"; exit 3; }
       f=$(find gpurun_out/$tag -name run_kernel_stats.csv | head -1)
       cut -d, -f1-4 "$f" | tee -a $log ;;
+    decab)
+      # compact rows decoded by the chain launch (default) against DMA + decode first
+      for v in 1 0; do
+        MDG_DEC_OVERLAP=$v run c0_dec$v 300 python tools/c0_breakdown.py 100
+        for b in 1 16; do
+          tag=dec${v}_b$b
+          MDG_DEC_OVERLAP=$v timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/$tag -o run -- python3 tools/blood_trace.py $b > gpurun_out/run/$tag.log 2>&1 || { echo "STOP $tag"; exit 3; }
+          f=$(find gpurun_out/$tag -name run_kernel_trace.csv | head -1)
+          echo "== $tag" | tee -a $log
+          python tools/blood_trace.py --summary "$f" | grep -E "smooth|decode|total" | tee -a $log
+        done
+      done ;;
     c0diag)
       run c0_breakdown 300 python tools/c0_breakdown.py 200
       run stage_diag_b1 120 python tools/stage_diag.py 1
