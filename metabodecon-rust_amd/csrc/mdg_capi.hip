@@ -106,6 +106,7 @@ struct mdg_ctx {
     // page-locked scratch of the host-buffer calls: boundaries in, counts / statuses /
     // MSEs out (pageable small copies each cost a staged, host-blocking transfer)
     void* hsmall = nullptr;
+    void* hsmall_dev = nullptr;  // its device address (null: kernels do not write it)
     size_t hsmall_bytes = 0;
     bool hsmall_busy = false;  // a call that failed midway may still have copies in flight
     size_t rows_guess = 0;     // batch_host: result rows fetched with the records (last count + 1/8)
@@ -1249,6 +1250,8 @@ static int batch_host(mdg_ctx* c, size_t b, size_t n, bool shared_x, Upload uplo
         const size_t want = std::max<size_t>(hs_need, 64 * 64);
         HIPCHK(hipHostMalloc(&c->hsmall, want, hipHostMallocDefault));
         c->hsmall_bytes = want;
+        void* dp = nullptr;
+        c->hsmall_dev = hipHostGetDevicePointer(&dp, c->hsmall, 0) == hipSuccess ? dp : nullptr;
     }
     double* h_sb = (double*)c->hsmall;
     double* h_mse = h_sb + 7 * b;
@@ -1280,6 +1283,21 @@ static int batch_host(mdg_ctx* c, size_t b, size_t n, bool shared_x, Upload uplo
         a.dec_desc = (const double*)c->st_sb.p + 2 * b;
         c->dec_next = false;
     }
+    // the records and the first guess rows of every table are written by the kernels
+    // straight into the page-locked scratch (no copy back, no copy engine round
+    // trip; MDG_HOST_DIRECT=0: device rows and copies, as before round 4)
+    const char* hd = std::getenv("MDG_HOST_DIRECT");
+    const bool direct = c->hsmall_dev && !(hd && hd[0] == '0');
+    if (direct) {
+        auto dev = [&](void* p) { return (char*)c->hsmall_dev + ((char*)p - (char*)c->hsmall); };
+        a.out_mse = (double*)dev(h_mse);
+        a.out_count = (int32_t*)dev(h_cnt);
+        a.out_status = (int32_t*)dev(h_st);
+        if (guess) {
+            a.out_host = (double*)dev(h_rows);
+            a.out_host_rows = (int)guess;
+        }
+    }
     if ((rc = run_pipeline(c, a, s))) return fail(rc);
     // Only the rows the spectra filled travel back (cap is usually N/2 + 2 rows, 1.5
     // MiB per 131072-point spectrum, against ~24 KiB of Lorentzians), and their count
@@ -1288,10 +1306,13 @@ static int batch_host(mdg_ctx* c, size_t b, size_t n, bool shared_x, Upload uplo
     // trip, into the page-locked scratch, and each spectrum's own rows go on to `out`
     // from there (rows at and past counts[i] are never written: the device rows there
     // are stale); a spectrum with more rows than the guess has the rest copied after.
-    he = hipMemcpyAsync(h_mse, d_mse, b * 16, hipMemcpyDeviceToHost, st);
-    if (he == hipSuccess && guess)
-        he = hipMemcpy2DAsync(h_rows, guess * 24, c->st_out.p, cap * 24, guess * 24, b, hipMemcpyDeviceToHost, st);
-    if (he != hipSuccess) return fail(hip_fail(he));
+    if (!direct) {
+        he = hipMemcpyAsync(h_mse, d_mse, b * 16, hipMemcpyDeviceToHost, st);
+        if (he == hipSuccess && guess)
+            he = hipMemcpy2DAsync(h_rows, guess * 24, c->st_out.p, cap * 24, guess * 24, b,
+                                  hipMemcpyDeviceToHost, st);
+        if (he != hipSuccess) return fail(hip_fail(he));
+    }
     he = hipStreamSynchronize(st);
     if (he != hipSuccess) return fail(hip_fail(he));
     c->hsmall_busy = false;

@@ -2917,6 +2917,19 @@ __global__ __launch_bounds__(BS) void k_retain(BatchArgs a, Workspace w) {
     retain_body<BS>(a, w, s, lds_i);
 }
 
+// row o of spectrum s's result table: page-locked host rows first (out_host_rows
+// of them, host-buffer calls), the caller's device rows after them, none past cap
+__device__ __forceinline__ void put_row(const BatchArgs& a, int s, int o, double f, double h, double m) {
+    double* q = o < a.out_host_rows ? a.out_host + 3 * ((size_t)s * a.out_host_rows + o)
+              : o < a.cap           ? a.out + 3 * ((size_t)s * a.cap + o)
+                                    : nullptr;
+    if (q) {
+        q[0] = f;
+        q[1] = h;
+        q[2] = m;
+    }
+}
+
 // ordered compaction of the retained Lorentzians into kept and the caller's rows
 // (k_retain; k_mse_local's first workgroup of each spectrum)
 template <int BS>
@@ -2927,7 +2940,6 @@ __device__ __forceinline__ void retain_body(const BatchArgs& a, const Workspace&
     const int per = (P + BS - 1) / BS;
     const int p0 = threadIdx.x * per, p1 = min(P, p0 + per);
     double* kept = w.kept + 3 * base;
-    double* out = a.out + 3 * (size_t)s * a.cap;
     // up to R parameters per thread stay in registers (one load round): 4096
     // Lorentzians at 1024 threads, 2048 at 256
     constexpr int R = BS >= 1024 ? 4 : 8;
@@ -2954,11 +2966,7 @@ __device__ __forceinline__ void retain_body(const BatchArgs& a, const Workspace&
                 kept[3 * o + 1] = v[u][1];
                 kept[3 * o + 2] = v[u][2];
                 unsafe += !peak_fast_ok(v[u][0], v[u][1], v[u][2]);
-                if (o < a.cap) {
-                    out[3 * o] = v[u][0];
-                    out[3 * o + 1] = v[u][1];
-                    out[3 * o + 2] = v[u][2];
-                }
+                put_row(a, s, o, v[u][0], v[u][1], v[u][2]);
                 ++o;
             }
         }
@@ -2981,11 +2989,7 @@ __device__ __forceinline__ void retain_body(const BatchArgs& a, const Workspace&
             kept[3 * o + 2] = params[3 * p + 2];
             if (!peak_fast_ok(params[3 * p], params[3 * p + 1], params[3 * p + 2]))
                 atomicAdd(&w.unsafe_kept[s], 1);
-            if (o < a.cap) {
-                out[3 * o] = params[3 * p];
-                out[3 * o + 1] = params[3 * p + 1];
-                out[3 * o + 2] = params[3 * p + 2];
-            }
+            put_row(a, s, o, params[3 * p], params[3 * p + 1], params[3 * p + 2]);
             ++o;
         }
     }

@@ -35,6 +35,10 @@ struct BatchArgs {
     const int32_t* const* dec_rows;  // B host-mapped int32 rows (device copy of the table)
     const double* dec_desc;          // B x {maximum, width, divisor, scale}
     int dec_gen;                     // a decoded chunk's flag value in this call (Workspace::dec_flags)
+    // the host-buffer calls: the first out_host_rows rows of every spectrum's table go
+    // straight to page-locked host memory (row s*out_host_rows + k), the rest to out
+    double* out_host;
+    int out_host_rows;               // <= cap; 0 when out_host is null
 };
 
 // Context-owned device workspace (sized for the worst case of the batch shape).
