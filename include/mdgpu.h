@@ -213,8 +213,10 @@ int mdg_deconvolute_rows(mdg_ctx* ctx, size_t b, size_t n, const double* const* 
  *   x_j = axes[3i] - ((double)j * axes[3i+1]) / axes[3i+2]   (maximum, width, SI - 1),
  * evaluated in that operation order, and its intensities y_j = (double)y_rows[i][j] *
  * y_scale[i] (the 1r int32 samples times 2^NC_proc). A quarter of the bytes of
- * mdg_deconvolute_rows cross PCIe (n int32 per spectrum, no axis row); page-locked
- * rows (mdg_host_alloc) go by DMA straight from where they are. */
+ * mdg_deconvolute_rows cross PCIe (n int32 per spectrum, no axis row). Page-locked
+ * rows (mdg_host_alloc) are not copied: the smoother's launch reads them from host
+ * memory and smooths each chunk as soon as it is decoded (MDG_DEC_OVERLAP=0: one
+ * DMA first, as for other rows). The call returns after every read of the rows. */
 int mdg_deconvolute_rows_i32(mdg_ctx* ctx, size_t b, size_t n, const double* axes,
                              const int32_t* const* y_rows, const double* y_scale, const double* sb,
                              const mdg_settings* s, const double* ignore, size_t n_ignore,
