@@ -181,6 +181,70 @@ def test_compact_rows_decode_paths(env, monkeypatch):
         assert np.array_equal(c_out, f_out), group
 
 
+@pytest.mark.parametrize("n,b,off", [(4099, 1, 1), (20001, 5, 3), (131071, 2, 0)])
+def test_compact_rows_decode_odd_shapes(n, b, off):
+    """The in-launch decode on rows that are not 16-byte aligned (an offset of off
+    int32 into a page-locked block: the decoders' scalar path) and lengths that are
+    not a multiple of 4 or of the chunk (the tails), 1-5 spectra (32 and 64
+    decoders): results bit-equal to mdg_deconvolute_rows on the same rows built on
+    the host with the decode's operations."""
+    import metabodecon as md
+    ctx = nat.context()
+    s = md.Deconvoluter().settings
+    rng = np.random.default_rng(n + b)
+    blk = nat.pinned_empty((b * (n + 4) + 4,), np.int32)
+    assert blk is not None
+    rows, xs, ys, axes, scales = [], [], [], [], []
+    for i in range(b):
+        mx, wd, dv = 11.8 + 0.01 * i, 14.0, float(n - 1)
+        x = mx - (np.arange(n, dtype=np.float64) * wd) / dv
+        c = rng.uniform(1.0, 9.0, 40)
+        hw = rng.uniform(0.002, 0.01, 40) ** 2
+        a = rng.uniform(1e5, 1e7, 40) * hw
+        y = (a[:, None] / (hw[:, None] + (x[None, :] - c[:, None]) ** 2)).sum(0) + rng.normal(0, 50, n)
+        scale = 2.0 ** int(rng.integers(-2, 3))
+        raw = np.round(y / scale).astype(np.int32)
+        r = blk[off + i * (n + 4): off + i * (n + 4) + n]
+        r[:] = raw
+        rows.append(r)
+        xs.append(nat.pinned_copy(x))
+        ys.append(nat.pinned_copy(raw.astype(np.float64) * scale))
+        axes.append((mx, wd, dv))
+        scales.append(scale)
+    cap = n // 2 + 2
+    sb = np.array([[11.0, 0.5]] * b, dtype=np.float64)
+
+    def run(compact):
+        out = np.zeros((b, cap, 3))
+        counts = np.zeros(b, dtype=np.uintp)
+        mse = np.zeros(b)
+        status = np.zeros(b, dtype=np.intc)
+        tail = (nat.ptr(out), cap, nat.ptr(counts, nat._szp), nat.ptr(mse),
+                status.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+        if compact:
+            yr = np.array([r.ctypes.data for r in rows], dtype=np.uintp)
+            ax = np.array(axes, dtype=np.float64)
+            sc = np.array(scales, dtype=np.float64)
+            rc = nat.lib().mdg_deconvolute_rows_i32(
+                ctx.handle, b, n, nat.ptr(ax), yr.ctypes.data_as(ctypes.POINTER(nat._i32p)),
+                nat.ptr(sc), nat.ptr(sb), ctypes.byref(s), None, 0, *tail)
+        else:
+            xr = np.array([v.ctypes.data for v in xs], dtype=np.uintp)
+            yr = np.array([v.ctypes.data for v in ys], dtype=np.uintp)
+            rc = nat.lib().mdg_deconvolute_rows(
+                ctx.handle, b, n, xr.ctypes.data_as(ctypes.POINTER(nat._dp)),
+                yr.ctypes.data_as(ctypes.POINTER(nat._dp)), nat.ptr(sb), ctypes.byref(s),
+                None, 0, *tail)
+        return rc, out, counts, mse, status
+    with ctx.lock:
+        c = run(True)
+        f = run(False)
+    assert c[0] == f[0]
+    assert np.array_equal(c[4], f[4]) and np.array_equal(c[2], f[2]) and np.array_equal(c[3], f[3])
+    assert np.array_equal(c[1], f[1])
+    assert c[2].min() > 0  # every spectrum found its peaks
+
+
 def test_compact_rows_reject_bad_descriptors():
     """A zero divisor, a non-finite axis operand or scale, or a null row: invalid
     argument, nothing run."""
