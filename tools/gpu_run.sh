@@ -101,7 +101,7 @@ for step in "$@"; do
     fitb:*)
       # fitb:<B>: the fit kernels' launch durations in one blood call of B spectra
       b=${step#fitb:}
-      for fk in tw7 twf1 twf3s tf plain; do
+      for fk in ${FITB_KERNELS:-tw7 twf1 twf3s tf plain}; do
         tag=fit_b${b}_$fk
         MDG_FITSUP=$fk timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/$tag -o run -- python3 tools/blood_trace.py $b > gpurun_out/run/$tag.log 2>&1 || { echo "STOP $tag"; exit 3; }
         f=$(find gpurun_out/$tag -name run_kernel_trace.csv | head -1)
