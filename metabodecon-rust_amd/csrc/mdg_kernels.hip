@@ -2485,15 +2485,16 @@ __device__ __forceinline__ bool fit_done(const Workspace& w, int s, int it) {
 // win from B = 4 (tools/fit_sweep.sh).
 constexpr int kTfQ = 24, kTfEW = 3;
 constexpr int kTfPad = 2;  // row padding (doubles): 16-byte aligned rows
-constexpr int kTfLds = 2 * kTfQ * (64 * kTfEW + kTfPad);
+template <int Q>
+constexpr int tf_lds() { return 2 * Q * (64 * kTfEW + kTfPad); }
 
 __device__ __forceinline__ const double* params_version(const Workspace& w, size_t base, int v) {
     return ((v & 1) ? w.params_alt : w.params) + 3 * base;
 }
 
-template <bool FAST>
+template <bool FAST, int QT = kTfQ>
 __device__ __forceinline__ void fit_tf_body(const Workspace& w, int s, int P, int it, double* T) {
-    constexpr int Q = kTfQ, EW = kTfEW, J = 64 * EW;
+    constexpr int Q = QT, EW = kTfEW, J = 64 * EW;
     constexpr int RS = J + kTfPad;  // row stride of T (doubles)
     static_assert(Q % 3 == 0 && Q / 3 <= 64, "whole peaks per tile");
     const size_t base = (size_t)s * w.capD;
@@ -2597,14 +2598,15 @@ __device__ __forceinline__ void fit_tf_body(const Workspace& w, int s, int P, in
     DIAG_FLUSH();
 }
 
+template <int Q>
 __global__ __launch_bounds__(64 * (kTfEW + 1)) void k_fit_sup_tf(BatchArgs a, Workspace w, int it) {
-    __shared__ __attribute__((aligned(16))) double T[kTfLds];
+    __shared__ __attribute__((aligned(16))) double T[tf_lds<Q>()];
     const int s = blockIdx.y;
     if (w.status[s] || fit_done(w, s, it)) return;
     const int P = w.sel_count[s];
     if (blockIdx.x == 0 && threadIdx.x == 0) w.unsafe[4 * s + (it + 2) % 3] = 0;
-    if (w.x_ok[s] && w.unsafe[4 * s + it % 3] == 0) fit_tf_body<true>(w, s, P, it, T);
-    else fit_tf_body<false>(w, s, P, it, T);
+    if (w.x_ok[s] && w.unsafe[4 * s + it % 3] == 0) fit_tf_body<true, Q>(w, s, P, it, T);
+    else fit_tf_body<false, Q>(w, s, P, it, T);
 }
 
 // K6h  term-fold fit, wide tiles ("tw"): Q = 63 points (21 peaks) per workgroup
@@ -3702,24 +3704,26 @@ const char* launch_select(const BatchArgs& a, const Workspace& w, int detector_o
     launch_k(k_select<1024>, dim3(a.B), dim3(1024), 0, st, a, w, threshold);
     return "k_select<1024>";
 }
-// Fit kernel choice by batch size. B <= 4: the 24-point term fold
-// over one workgroup per tile ("tf"); B <= 24: the 63-point term fold over one
+// Fit kernel choice by batch size. B = 1: the term fold over 12-point
+// tiles ("tf12": blood, ten launches 95.4 against 100.7 us; equal at B = 2, worse at
+// 4); B <= 4: the 24-point term fold over one workgroup per tile ("tf"); B <= 24: the 63-point term fold over one
 // batch-wide tile list on two workgroups per CU ("twf1"; blood set, ten launches:
 // 373 us at B = 16 against 403 for the (98, B) grid "tw7", 270 / 268 at B = 8, 204
 // against tf's 185 at B = 4); beyond, one point per lane with the update separate
 // ("plain": 79 / 57 us per spectrum at B = 32 / 256). When other engine contexts on
 // the device have run pipelines, B = 1 keeps "tw7": "tf"'s lead alone is gone as
 // soon as a second context has been used, and 18 concurrent B = 1 pipelines run
-// 6.6k spectra/s with "tf" against 7.8-8.1k with "tw7". MDG_FITSUP = tf | tw7 |
+// 6.6k spectra/s with "tf" against 7.8-8.1k with "tw7". MDG_FITSUP = tf | tf12 | tw7 |
 // tw3s | twf | twf1 | twf3s | plain forces one (all bit-identical; tests,
 // measurements); any other value is ignored.
 static std::string fit_choice(const BatchArgs& a) {
     if (const char* force = std::getenv("MDG_FITSUP")) {
         const std::string f(force);
-        if (f == "tf" || f == "tw7" || f == "tw3s" || f == "twf" || f == "twf1" || f == "twf3s" || f == "plain")
+        if (f == "tf" || f == "tf12" || f == "tw7" || f == "tw3s" || f == "twf" || f == "twf1" || f == "twf3s" ||
+            f == "plain")
             return f;
     }
-    if (a.B == 1 && a.contexts > 1) return "tw7";
+    if (a.B == 1) return a.contexts > 1 ? "tw7" : "tf12";
     return a.B <= 4 ? "tf" : a.B <= 24 ? "twf1" : "plain";
 }
 bool fit_sup_fused(const BatchArgs& a) { return fit_choice(a) != "plain"; }
@@ -3769,10 +3773,16 @@ const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int i
         launch_k(k_fit_sup_twf<SH>, dim3(g), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
         return "k_fit_sup_twf<63, 1, 7>";
     }
+    if (f == "tf12") {
+        // 12-point tiles: twice the workgroups, half the evaluation per workgroup
+        const int g = tg ? std::max(1, std::atoi(tg)) : (3 * 2048 + 11) / 12;
+        launch_k(k_fit_sup_tf<12>, dim3(g, a.B), dim3(64 * (kTfEW + 1)), 0, st, a, w, it);
+        return "k_fit_sup_tf<12>";
+    }
     if (f == "tf" || f == "twf" || f == "twf1" || f == "twf3s") {
         // 24 points per workgroup: one workgroup per tile of a 2048-peak spectrum (256)
         const int g = tg ? std::max(1, std::atoi(tg)) : (3 * 2048 + 23) / 24;
-        launch_k(k_fit_sup_tf, dim3(g, a.B), dim3(64 * (kTfEW + 1)), 0, st, a, w, it);
+        launch_k(k_fit_sup_tf<kTfQ>, dim3(g, a.B), dim3(64 * (kTfEW + 1)), 0, st, a, w, it);
         return "k_fit_sup_tf";
     }
     // gx 256-thread workgroups per spectrum (24: one point per thread at P = 2048)

@@ -501,7 +501,7 @@ def test_chain_smoother_repeated_launches(ctx, monkeypatch):
 
 # the library's fit kernels (fit_choice, mdg_kernels.hip); "twf*" are the batch-wide
 # tile lists, "tw3s"/"twf3s" single-buffered; ":G" = G workgroups (many tiles each)
-FIT_KERNELS = ["tf", "tw7", "tw3s", "twf", "twf1", "twf3s", "twf:5", "twf3s:7", "plain"]
+FIT_KERNELS = ["tf", "tf12", "tw7", "tw3s", "twf", "twf1", "twf3s", "twf:5", "twf3s:7", "plain"]
 
 
 @pytest.mark.parametrize("mode", ["fine", "coarse"])
