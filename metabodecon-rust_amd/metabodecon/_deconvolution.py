@@ -424,10 +424,9 @@ class Deconvoluter:
     # over, concurrently: a set of one length is cut into contiguous chunks (at least
     # one per lane, at most CHUNK spectra each), dealt round-robin to the lanes, each
     # chunk one batched pipeline; each lane's sequential smoother overlaps the other
-    # lane's fit. Two lanes measured best for the 16 blood spectra under both HIP's
-    # default 4 hardware queues and 32 (tools/c4_lanes.sh: 2.65-2.72 ms per set
-    # against 3.3-4.3 with 3-4 lanes, 3.9 with 16 lanes of one spectrum, 9.3-9.9 with
-    # one batch of 16, whose B > 8 fit leaves the chip mostly idle). HIP maps streams
+    # lane's fit. (Round 3 measured two lanes best for the 16 blood spectra, 2.65-2.72
+    # ms per set against 9.3-9.9 for one batch of 16; since round 4's small-batch fit
+    # and in-launch decode, one batch wins for such sets: ONE_LANE_UPTO.) HIP maps streams
     # round-robin onto GPU_MAX_HW_QUEUES hardware queues and two busy streams on one
     # queue serialise, so the lanes also stay below that count (one queue is left
     # for the caller's own stream). MDGPU_LANES overrides the count.
