@@ -154,6 +154,7 @@ for step in "$@"; do
     hdab)
       # results written by the kernels into page-locked memory (default) against copies
       for v in 1 0 1 0; do MDG_HOST_DIRECT=$v run c0_hd$v 300 python tools/c0_breakdown.py 200; done ;;
+    smallsets) run small_sets 600 python tools/small_sets.py ;;
     c0diag)
       run c0_breakdown 300 python tools/c0_breakdown.py 200
       run stage_diag_b1 120 python tools/stage_diag.py 1
