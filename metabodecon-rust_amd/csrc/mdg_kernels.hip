@@ -3706,7 +3706,7 @@ const char* launch_select(const BatchArgs& a, const Workspace& w, int detector_o
 }
 // Fit kernel choice by batch size. B = 1: the term fold over 12-point
 // tiles ("tf12": blood, ten launches 95.4 against 100.7 us; equal at B = 2, worse at
-// 4); B <= 4: the 24-point term fold over one workgroup per tile ("tf"); B <= 24: the 63-point term fold over one
+// 4; 6-point tiles: 112-113 us); B <= 4: the 24-point term fold over one workgroup per tile ("tf"); B <= 24: the 63-point term fold over one
 // batch-wide tile list on two workgroups per CU ("twf1"; blood set, ten launches:
 // 373 us at B = 16 against 403 for the (98, B) grid "tw7", 270 / 268 at B = 8, 204
 // against tf's 185 at B = 4); beyond, one point per lane with the update separate
