@@ -96,6 +96,10 @@ struct mdg_ctx {
     Buffer dec_flags;
     int dec_gen = 0;
     bool dec_next = false;  // set by the upload: the next pipeline decodes the rows
+    // batch_host: where this call's kernels read [sb][descriptors][row table] (the
+    // page-locked scratch's device address, or st_sb after a copy when small_copy)
+    const double* small_rd = nullptr;
+    bool small_copy = true;
     // page-locked host ring for mdg_deconvolute_rows: the rows are gathered into a
     // slot and sent with one asynchronous DMA per slot (upload_rows)
     void* ring[2] = {nullptr, nullptr};
@@ -1267,27 +1271,30 @@ static int batch_host(mdg_ctx* c, size_t b, size_t n, bool shared_x, Upload uplo
         c->hsmall_busy = false;
         return code;
     };
+    // the kernels read the call's small inputs ([sb][descriptors][row table]) straight
+    // from the page-locked scratch and write the records and the first guess rows of
+    // every table into it (no copy either way, no copy-engine round trip;
+    // MDG_HOST_DIRECT=0: device copies, as before round 4)
+    const char* hd = std::getenv("MDG_HOST_DIRECT");
+    const bool direct = c->hsmall_dev && !(hd && hd[0] == '0');
+    c->small_rd = direct ? (const double*)c->hsmall_dev : (const double*)c->st_sb.p;
+    c->small_copy = !direct;
     std::memcpy(h_sb, sb, b * 16);
     bool sent_sb = false;
     c->dec_next = false;
     if ((rc = upload(dx, dy, st, &sent_sb))) return fail(rc);
     hipError_t he = hipSuccess;
-    if (!sent_sb) he = hipMemcpyAsync(c->st_sb.p, h_sb, b * 16, hipMemcpyHostToDevice, st);
+    if (!sent_sb && !direct) he = hipMemcpyAsync(c->st_sb.p, h_sb, b * 16, hipMemcpyHostToDevice, st);
     if (he != hipSuccess) return fail(hip_fail(he));
     BatchArgs a;
-    if ((rc = fill_args(c, a, b, n, dx, shared_x ? 0 : n, dy, n, (const double*)c->st_sb.p, ignore,
-                        n_ignore, (double*)c->st_out.p, cap, d_cnt, d_mse, d_st)))
+    if ((rc = fill_args(c, a, b, n, dx, shared_x ? 0 : n, dy, n, c->small_rd, ignore, n_ignore,
+                        (double*)c->st_out.p, cap, d_cnt, d_mse, d_st)))
         return fail(rc);
     if (c->dec_next) {  // the rows are decoded by the pipeline (run_pipeline)
-        a.dec_rows = (const int32_t* const*)((const double*)c->st_sb.p + 6 * b);
-        a.dec_desc = (const double*)c->st_sb.p + 2 * b;
+        a.dec_rows = (const int32_t* const*)(c->small_rd + 6 * b);
+        a.dec_desc = c->small_rd + 2 * b;
         c->dec_next = false;
     }
-    // the records and the first guess rows of every table are written by the kernels
-    // straight into the page-locked scratch (no copy back, no copy engine round
-    // trip; MDG_HOST_DIRECT=0: device rows and copies, as before round 4)
-    const char* hd = std::getenv("MDG_HOST_DIRECT");
-    const bool direct = c->hsmall_dev && !(hd && hd[0] == '0');
     // (writing a page-locked caller table in place instead measured no better:
     // configs[4] 13.9-14.1k against 14.0k, configs[0] alike, round 4)
     if (direct) {
@@ -1431,16 +1438,16 @@ int mdg_deconvolute_rows_i32(mdg_ctx* c, size_t b, size_t n, const double* axes,
         if (zc) {
             const int32_t** tab = (const int32_t**)(h + 4 * b);
             for (size_t i = 0; i < b; ++i) tab[i] = y_rows[i];
-            HIPCHK(hipMemcpyAsync(c->st_sb.p, c->hsmall, b * 56, hipMemcpyHostToDevice, st));
+            if (c->small_copy) HIPCHK(hipMemcpyAsync(c->st_sb.p, c->hsmall, b * 56, hipMemcpyHostToDevice, st));
             *sent_sb = true;
             c->dec_next = true;
             return MDG_OK;
         }
         if ((rc = ensure(c->st_raw, b * n * 4))) return rc;
         if ((rc = upload_rows(c, st, (char*)c->st_raw.p, (const void* const*)y_rows, b, n * 4))) return rc;
-        HIPCHK(hipMemcpyAsync(c->st_sb.p, c->hsmall, b * 48, hipMemcpyHostToDevice, st));
+        if (c->small_copy) HIPCHK(hipMemcpyAsync(c->st_sb.p, c->hsmall, b * 48, hipMemcpyHostToDevice, st));
         *sent_sb = true;
-        launch_decode_rows_i32((const int32_t*)c->st_raw.p, (const double*)c->st_sb.p + 2 * b, (int)b,
+        launch_decode_rows_i32((const int32_t*)c->st_raw.p, c->small_rd + 2 * b, (int)b,
                                (int64_t)n, shared ? 1 : 0, dx, dy, st);
         HIPCHK(hipGetLastError());
         return MDG_OK;
