@@ -218,7 +218,8 @@ def hbm_pipeline(tag, batch, iterations, value, n):
     launches per pipeline, / the batch size), and the rate it implies at `value`
     spectra/s -- the BASELINE metric's "achieved HBM GB/s" for the mode that
     produces `value`. None when no summary is committed."""
-    launches = {"k_queue_gather": 1, "k_smooth_chain<3, false>": 1, "k_flags": 1,
+    # (round 5: the queue reads each submission's row in place -- no k_queue_gather)
+    launches = {"k_smooth_chain<3, false>": 1, "k_flags": 1,
                 "k_peaks<256, 1024>": 1, "k_select<1024>": 1, "k_fit_sup": iterations,
                 "k_fit_update": iterations, "k_mse_local<4>": 1, "k_queue_scatter": 1}
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{tag}.json")),
@@ -425,6 +426,10 @@ def headline(args, nat, torch, dist, dev, rank, world):
     if args.exact_mse:
         settings.options = nat.OPTION_EXACT_MSE
     slots = [Slot(nat, torch, dev, B, n, cap) for _ in range(S)]
+    # many contexts run B = 1 pipelines at once: the fit tiling that leaves room for
+    # the others (mdg_ctx_set_latency_mode; one context keeps the latency default)
+    for sl in slots:
+        sl.ctx.set_latency_mode(S == 1)
     R = max(KS, WS, 1)  # distinct spectra (B each), seeds rank*R*B ...
     x, Y = synth_device(nat, slots[0].ctx, torch, R * B, n, args.peaks, rank * R * B, dev,
                         args.hw_scale)
@@ -581,13 +586,13 @@ def headline_queue(args, nat, torch, dist, dev, rank, world):
     q.synchronize()
     torch.cuda.synchronize()
     if dist_on:  # RCCL connections are set up by the first collectives, not in the timing
-        from metabodecon.distributed import gather_tables
+        from metabodecon.distributed import gather_packed
 
         def gather():
             # the (status, count, mse) records and the Lorentzian tables (padded to the
             # largest count of any rank) to rank 0, the caller that receives the
-            # results: distributed.gather_tables, one packed gather over RCCL/xGMI
-            return gather_tables(status, cnt, mse, out, world * KS, dst=0)
+            # results: distributed.gather_packed, one packed gather over RCCL/xGMI
+            return gather_packed(status, cnt, mse, out, world * KS, dst=0)[1]
         gather()
         torch.cuda.synchronize()
     status.fill_(-1)
@@ -704,7 +709,17 @@ def headline_queue(args, nat, torch, dist, dev, rank, world):
                                   14.8 - 20.0 / (n - 1.0), SB)
     roof = roofline_from_stages(lane, prof, work, f"q{B}", n) if prof else None
     if roof:
-        roof["rocprof"] = rocprof_check(roof)
+        rc = rocprof_check(roof)
+        roof["rocprof"] = rc
+        if rc:
+            # scalars beside the live figure (a driver record keeps a roofline's scalar
+            # keys only): the committed rocprof trace's average for the same kernel and
+            # the fraction it gives (hipEvents around each launch in the profiled pass
+            # add their own cost to the live average)
+            roof["frac_rocprof"] = rc["frac"]
+            roof["avg_launch_ms_rocprof"] = rc["avg_launch_ms"]
+            roof["rocprof_launches"] = rc["launches"]
+            roof["rocprof_source"] = rc["source"]
     if roof and qprof.get(roof["stage"], (0, 0))[1]:
         ms, cnt = qprof[roof["stage"]]
         roof["in_queue"] = {
@@ -964,13 +979,13 @@ def dist_configs(args, nat, torch, dist, dev, rank, world, threads):
       distributed.shard_range, each rank's block generated on its own GPU (seeds =
       global indices, so the spectra are the 1-GPU run's) and run as one
       device-resident batch; the timed region ends after the RCCL gather of every
-      rank's tables and records (distributed.gather_tables), reported separately;
+      rank's tables and records (distributed.gather_packed), reported separately;
     - configs[4]: the 16 blood spectra through distributed.par_deconvolute_spectra
       (host buffers: the H2D copies and the gather are inside).
     Results checked after timing: configs[3] the first spectrum of every rank's block
     against the oracle (rank 0), configs[4] all 16 against the goldens."""
     import metabodecon as md
-    from metabodecon.distributed import gather_tables, par_deconvolute_spectra, shard_range
+    from metabodecon.distributed import gather_packed, par_deconvolute_spectra, shard_range
     out = {}
     settings = nat.default_settings()
     lo, hi = shard_range(C3_N, rank, world)
@@ -993,7 +1008,7 @@ def dist_configs(args, nat, torch, dist, dev, rank, world, threads):
         ctx.synchronize()
 
     def gather():
-        g = gather_tables(s3, c3, m3, o3, C3_N, dst=0)
+        g = gather_packed(s3, c3, m3, o3, C3_N, dst=0)[1]
         torch.cuda.synchronize()
         return g
 
@@ -1068,8 +1083,8 @@ def dist_configs(args, nat, torch, dist, dev, rank, world, threads):
         "ms_per_step": 1e3 * statistics.median(ts), "steps": 10, "scaling": "strong",
         "verified": f"{ok}/{len(spectra)} (goldens)" if rank == 0 else None,
         "workload": ("the 16 blood spectra, Spectrum.read_bruker_set + "
-                     "distributed.par_deconvolute_spectra (sharded, host buffers, one packed "
-                     "RCCL gather to rank 0)")}
+                     "distributed.par_deconvolute_spectra (sharded; every rank's block through "
+                     "the single-process host path; one packed RCCL gather to rank 0)")}
     return out
 
 
@@ -1267,6 +1282,16 @@ def queue_line(args, h, world, nat):
                        "Lorentzian evaluation: fit 3 P_sel^2 x iterations, MSE L x P_kept; + 3L) "
                        "x value")}
     pipe["frac"] = pipe["achieved"] / pipe["peak"]
+    hbm = hbm_pipeline(f"q{args.max_batch}", args.max_batch, args.fit_iterations or 10, value, args.n)
+    if roof and hbm:
+        # the whole pipeline's HBM traffic beside the dominant kernel's (scalars: kept
+        # by a driver record): bytes per spectrum moved, their ratio to the
+        # algorithmic bytes, and the rate at `value`
+        roof["traffic_pipeline_bytes_per_spectrum"] = hbm["bytes_per_spectrum"]
+        roof["traffic_pipeline_over_algorithmic"] = hbm["bytes_per_spectrum"] / hbm["algorithmic_bytes_per_spectrum"]
+        roof["hbm_pipeline_gbs"] = hbm["achieved"]
+        roof["hbm_pipeline_frac"] = hbm["frac"]
+        roof["traffic_pipeline_source"] = hbm["source"].split(":")[0]
     if roof and roof.get("stage") == "fit_superposition":
         evals = roof["algorithmic_per_launch"] / FLOPS_PER_EVAL / (roof["avg_launch_ms"] / 1e3)
         roof["issue_roofline"] = {
@@ -1308,8 +1333,7 @@ def queue_line(args, h, world, nat):
         "rccl_gather_ms": h["gather_ms"],
         "roofline": roof,
         "roofline_pipeline": pipe,
-        "hbm_pipeline": hbm_pipeline(f"q{args.max_batch}", args.max_batch,
-                                     args.fit_iterations or 10, value, args.n),
+        "hbm_pipeline": hbm,
         "stages_ms_per_spectrum": h["stages_ms_per_spectrum"],
         "stages_source": (f"separate profiled pass: one batch of {args.max_batch} on lane 0 "
                           "(hipEvents around every stage), per spectrum"),

@@ -168,6 +168,17 @@ int mdg_ctx_reset_stage_times(mdg_ctx* ctx);
  * not run). The string is static. Lets benchmarks label measurements with what the
  * engine actually dispatched. */
 int mdg_ctx_stage_kernel(mdg_ctx* ctx, int stage, const char** name);
+/* Latency mode (default 1): a one-spectrum pipeline of this context expects the GPU to
+ * itself (the reference's deconvolute_spectrum called from one thread,
+ * deconvoluter.rs:530-552) and takes the fit tiling fastest alone; 0 = many contexts
+ * run concurrently (par_ callers spread over contexts, deconvoluter.rs:591-613,
+ * 913-917): the tiling that leaves room for the others. Results are bit-identical
+ * either way; only which shipped kernel runs changes. */
+int mdg_ctx_set_latency_mode(mdg_ctx* ctx, int on);
+/* The engine's MDG_* switches (kernel choices for tests and measurements, all
+ * bit-exact) are read from the environment once, when the context is created; this
+ * reads them again (nothing else on a call's path reads the environment). */
+int mdg_ctx_reload_switches(mdg_ctx* ctx);
 
 /* ---- hot path: host buffers ------------------------------------------------
  * x, y: n chemical shifts / intensities of a validated Spectrum

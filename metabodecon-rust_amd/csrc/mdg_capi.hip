@@ -11,6 +11,7 @@
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
+#include <cstddef>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -51,8 +52,12 @@ struct mdg_ctx {
     int device = 0;
     hipStream_t own = nullptr;
     hipStream_t stream = nullptr;
-    bool counted = false;  // in g_active (has run a pipeline)
-    std::atomic<long long> last_pipeline_ns{0};  // steady clock at its last pipeline
+    // MDG_* switches, read when the context was created (mdg_ctx_reload_switches
+    // re-reads them); the per-call paths read only this copy
+    EngineSwitches sw;
+    // latency mode (mdg_ctx_set_latency_mode): a B = 1 pipeline expects the GPU to
+    // itself and takes the finer fit tiles (fit_choice)
+    int latency = 1;
     std::mutex mu;
     // workspace arena
     Buffer arena;
@@ -216,11 +221,16 @@ PinnedPool& pinned_pool() {
 }
 constexpr size_t kPinnedSlab = 64u << 20;
 
+// The environment, read in these two places only: the engine switches when a
+// context is created (or mdg_ctx_reload_switches), and the pinned-memory cap once per
+// process at its first page-locked allocation.
+size_t env_pinned_max() {
+    const char* e = std::getenv("MDGPU_PINNED_MAX");
+    return e && *e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)8 << 30;
+}
+
 size_t pinned_limit() {
-    static const size_t lim = [] {
-        const char* e = std::getenv("MDGPU_PINNED_MAX");
-        return e && *e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)8 << 30;
-    }();
+    static const size_t lim = env_pinned_max();
     return lim;
 }
 
@@ -439,13 +449,13 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     const int det_only = s->selector == MDG_SELECT_DETECTOR_ONLY;
     // the term-fold fit kernel also updates the stencils; its parameter versions
     // alternate between params and the (then unused) ratio buffer
-    const bool fused = fit_sup_fused(a);
+    const EngineSwitches& sw = c->sw;
+    const bool fused = fit_sup_fused(a, sw);
     w.params_alt = fused ? w.ratio : nullptr;
     w.fit_iters = (int)s->fit_iterations;
-    int gfit = 24;  // k_fit_sup workgroups per spectrum (3 * 2048 / 256)
-    if (const char* e = std::getenv("MDG_GFIT")) gfit = std::max(1, std::atoi(e));  // tuning
+    const int gfit = sw.gfit;  // k_fit_sup workgroups per spectrum (3 * 2048 / 256; MDG_GFIT: tuning)
     const int gupd = std::max(1, std::min(16, 1024 / std::max(1, a.B)));
-    const int nparts = mse_nparts(a);
+    const int nparts = mse_nparts(a, sw);
     // chain smoother buffers: raw sums of every pass, scaled outputs of passes
     // 0..P-2 and one 128-byte progress counter per (spectrum, pass)
     w.thr_s = c->ovr_thr;
@@ -454,9 +464,9 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     w.chain_raw = w.chain_tmp = nullptr;
     w.chain_flags = nullptr;
     if (ma) {
-        const char* force = std::getenv("MDG_SMOOTH");
         const int P = (int)s->smooth_iterations, ws = (int)s->smooth_window;
-        if ((!force || std::string(force) == "chain") && chain_supported(a.B, a.N, P, ws) &&
+        if ((sw.smooth == EngineSwitches::SM_DEFAULT || sw.smooth == EngineSwitches::SM_CHAIN) &&
+            chain_supported(a.B, a.N, P, ws) &&
             ensure_chain(c, chain_bytes(a.B, a.N, ws, P)) == MDG_OK) {
             const int64_t L = chain_stride_for(a.N, ws);
             char* base = (char*)c->chain.p;
@@ -472,10 +482,8 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     // skips those stages (their outputs are stale, results wrong); MDG_DIAG_DUP=prep,
     // smooth,detect,select,retain,mse launches those stages twice (each is idempotent;
     // smooth adds a k_flags), for their marginal cost in stream mode
-    const char* skip = std::getenv("MDG_DIAG_SKIP");
-    const bool skip_smooth = skip && std::strstr(skip, "smooth"), skip_mse = skip && std::strstr(skip, "mse");
-    const char* dup_env = std::getenv("MDG_DIAG_DUP");
-    auto reps = [&](const char* stage) { return dup_env && std::strstr(dup_env, stage) ? 2 : 1; };
+    const bool skip_smooth = std::strstr(sw.diag_skip, "smooth"), skip_mse = std::strstr(sw.diag_skip, "mse");
+    auto reps = [&](const char* stage) { return std::strstr(sw.diag_dup, stage) ? 2 : 1; };
 #else
     constexpr bool skip_smooth = false, skip_mse = false;
     auto reps = [](const char*) { return 1; };
@@ -483,9 +491,8 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     const int sm_it = (int)s->smooth_iterations, sm_ws = (int)s->smooth_window;
     const bool panic_shape = ma && (int64_t)(s->smooth_window / 2) > a.N;
     // the chain smoother does k_prep's work itself (MDG_PREP=separate: not)
-    const char* prep_env = std::getenv("MDG_PREP");
-    const bool fused_prep = ma && !panic_shape && !skip_smooth && !(prep_env && std::string(prep_env) == "separate") &&
-                            reps("prep") == 1 && smooth_uses_chain(a, w, sm_it, sm_ws);
+    const bool fused_prep = ma && !panic_shape && !skip_smooth && !sw.prep_separate && reps("prep") == 1 &&
+                            smooth_uses_chain(a, w, sm_it, sm_ws, sw);
     if (a.dec_rows) {
         // rows still in host memory (mdg_deconvolute_rows_i32): the chain launch
         // decodes them while it smooths (flags of this call's generation), any other
@@ -498,9 +505,13 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
         }
         a.dec_gen = ++c->dec_gen;
         w.dec_flags = (int32_t*)c->dec_flags.p;
-        if (!fused_prep) {
+        // the chain launch's hand-off needs rows of whole 128-byte lines (batch_host
+        // pads them; chain_decode): other rows are decoded by a launch of their own
+        const bool lines_owned = a.y_stride % kDecRowAlign == 0 && ((uintptr_t)a.y & 127) == 0;
+        if (!fused_prep || !lines_owned) {
             StageTimer t(c, ST_PREP);
             launch_decode_rows_zc(a, st);
+            a.dec_rows = nullptr;  // decoded: the smoother reads y (the prep still takes the axis from dec_desc)
         }
     }
     if (!fused_prep) {
@@ -509,8 +520,7 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
         kn[ST_PREP] = "k_prep";
     }
 #ifdef MDG_DIAG
-    if (const char* e = std::getenv("MDG_DIAG_PAD"))
-        for (int k = std::atoi(e); k > 0; --k) launch_diag_nop(a, w, st);
+    for (int k = sw.diag_pad; k > 0; --k) launch_diag_nop(a, w, sw, st);
 #endif
     if (ma) {
         if (panic_shape) {
@@ -521,17 +531,17 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
         } else if (!skip_smooth) {
             StageTimer t(c, ST_SMOOTH);
             if (reps("smooth") == 2) {  // k_flags resets the chain's progress counters
-                launch_smooth(a, w, sm_it, sm_ws, st, fused_prep ? 1 : 0);
+                launch_smooth(a, w, sm_it, sm_ws, sw, st, fused_prep ? 1 : 0);
                 launch_flags(a, w, st);
             }
-            kn[ST_SMOOTH] = launch_smooth(a, w, sm_it, sm_ws, st, fused_prep ? 1 : 0);
+            kn[ST_SMOOTH] = launch_smooth(a, w, sm_it, sm_ws, sw, st, fused_prep ? 1 : 0);
         }
     }
     {
         StageTimer t(c, ST_DETECT);
         for (int r = reps("detect"); r > 0; --r) {
             launch_flags(a, w, st);
-            kn[ST_DETECT] = launch_peaks(a, w, det_only, st);
+            kn[ST_DETECT] = launch_peaks(a, w, det_only, sw, st);
         }
     }
     {
@@ -541,7 +551,7 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     for (uint32_t it = 0; it < s->fit_iterations; ++it) {
         {
             StageTimer t(c, ST_FIT_SUP);
-            kn[ST_FIT_SUP] = launch_fit_sup(a, w, gfit, (int)it, st);
+            kn[ST_FIT_SUP] = launch_fit_sup(a, w, gfit, (int)it, sw, st);
         }
         if (!fused) {
             StageTimer t(c, ST_FIT_UPDATE);
@@ -558,7 +568,7 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     }
     if (!skip_mse) {
         StageTimer t(c, ST_MSE);
-        for (int r = reps("mse"); r > 0; --r) kn[ST_MSE] = launch_mse(a, w, nparts, st);
+        for (int r = reps("mse"); r > 0; --r) kn[ST_MSE] = launch_mse(a, w, nparts, sw, st);
     }
     if (!skip_mse && (s->options & MDG_OPTION_EXACT_MSE)) {
         // the reference's summation order (deconvoluter.rs:828-862), over the retained
@@ -578,40 +588,6 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
 // uploaded only when the regions differ from the ones it holds (the usual caller
 // passes the same Deconvoluter's regions every call): no host-to-device copy, and
 // no pageable-copy stall, in a stream of calls.
-// Engine contexts per device that ran a pipeline in the last kActiveNs: the B = 1
-// fit kernel differs when the spectrum is likely to have the GPU to itself
-// (fit_choice). Concurrent callers launch every millisecond or so;
-// contexts that are merely alive (a finished queue, the idle lanes of a
-// Deconvoluter) do not count. a.contexts holds min(count, 2): the choice only asks
-// "alone or not", and the batch arguments are part of the graph keys.
-constexpr int kMaxDevices = 64;
-constexpr long long kActiveNs = 50'000'000;
-struct DeviceActivity {
-    std::mutex mu;
-    std::vector<mdg_ctx*> ctxs;  // contexts that have run a pipeline, until destroyed
-};
-static DeviceActivity g_active[kMaxDevices];
-static long long steady_ns() {
-    return std::chrono::duration_cast<std::chrono::nanoseconds>(
-               std::chrono::steady_clock::now().time_since_epoch())
-        .count();
-}
-static int active_contexts(mdg_ctx* c) {
-    if (c->device < 0 || c->device >= kMaxDevices) return 2;
-    const long long now = steady_ns();
-    c->last_pipeline_ns.store(now);
-    DeviceActivity& d = g_active[c->device];
-    std::lock_guard<std::mutex> g(d.mu);
-    if (!c->counted) {
-        c->counted = true;
-        d.ctxs.push_back(c);
-    }
-    int n = 0;
-    for (mdg_ctx* o : d.ctxs)
-        if (now - o->last_pipeline_ns.load() < kActiveNs) ++n;
-    return std::min(n, 2);
-}
-
 int fill_args(mdg_ctx* c, BatchArgs& a, size_t b, size_t n, const double* x, size_t xs, const double* y,
               size_t ys, const double* sb, const double* ignore, size_t n_ignore, double* out,
               size_t cap, int32_t* cnt, double* mse, int32_t* status) {
@@ -623,8 +599,9 @@ int fill_args(mdg_ctx* c, BatchArgs& a, size_t b, size_t n, const double* x, siz
     a.y = y;
     a.y_stride = (int64_t)ys;
     a.sb = sb;
+    a.sb_step = 2;
     a.n_ignore = (int)n_ignore;
-    a.contexts = active_contexts(c);
+    a.latency = c->latency;
     a.ignore = nullptr;
     if (n_ignore > 0) {
         const size_t cnt = 2 * n_ignore;
@@ -811,6 +788,61 @@ int mdg_host_alloc(int device, size_t bytes, void** out) {
 
 int mdg_host_free(void* p) { return pinned_free(p); }
 
+}  // extern "C"
+
+EngineSwitches mdg::read_engine_switches() {
+    EngineSwitches w;
+    auto str = [](const char* name) -> std::string {
+        const char* v = std::getenv(name);
+        return v ? std::string(v) : std::string();
+    };
+    auto num = [&](const char* name, int dflt) {
+        const std::string v = str(name);
+        return v.empty() ? dflt : std::atoi(v.c_str());
+    };
+    auto copy = [](char* dst, size_t cap, const std::string& v) {
+        std::memset(dst, 0, cap);
+        std::strncpy(dst, v.c_str(), cap - 1);
+    };
+    const std::string sm = str("MDG_SMOOTH");
+    w.smooth = sm.empty() ? EngineSwitches::SM_DEFAULT
+               : sm == "chain" ? EngineSwitches::SM_CHAIN
+               : sm == "pipe"  ? EngineSwitches::SM_PIPE
+               : sm == "generic" ? EngineSwitches::SM_GENERIC
+                                 : EngineSwitches::SM_OTHER;
+    w.chain_excl = str("MDG_CHAIN_EXCL").substr(0, 1) != "0";
+    const std::string pk = str("MDG_PEAKS");
+    w.peaks = pk.empty() ? 0 : pk == "fine" ? 1 : 2;
+    const std::string f = str("MDG_FITSUP");
+    copy(w.fitsup, sizeof(w.fitsup), "");
+    if (f == "tf" || f == "tf12" || f == "tw7" || f == "tw3s" || f == "twf" || f == "twf1" || f == "twf3s" ||
+        f == "plain")
+        copy(w.fitsup, sizeof(w.fitsup), f);
+    w.tw_g = std::max(0, num("MDG_TW_G", 0));
+    if (!str("MDG_TW_G").empty()) w.tw_g = std::max(1, w.tw_g);
+    w.gfit = std::max(1, num("MDG_GFIT", 24));
+    w.mse_npt = str("MDG_MSE_NPT").empty() ? 0 : (num("MDG_MSE_NPT", 2) == 4 ? 4 : 2);
+    w.mse_parts = str("MDG_MSE_PARTS").empty() ? 0 : std::max(1, num("MDG_MSE_PARTS", 1));
+    w.mse_nearcap = str("MDG_MSE_NEARCAP").empty() ? -1 : std::max(0, num("MDG_MSE_NEARCAP", 0));
+    w.prep_separate = str("MDG_PREP") == "separate";
+    w.graphs = str("MDG_GRAPHS") == "1";
+    w.host_direct = str("MDG_HOST_DIRECT").substr(0, 1) != "0";
+    w.dec_overlap = str("MDG_DEC_OVERLAP").substr(0, 1) != "0";
+#ifdef MDG_DIAG
+    copy(w.diag_skip, sizeof(w.diag_skip), str("MDG_DIAG_SKIP"));
+    copy(w.diag_dup, sizeof(w.diag_dup), str("MDG_DIAG_DUP"));
+    w.diag_pad = std::max(0, num("MDG_DIAG_PAD", 0));
+    w.diag_pad_small = !str("MDG_DIAG_PAD_SMALL").empty();
+    w.diag_pad_wgs = std::max(0, num("MDG_DIAG_PAD_WGS", 0));
+#else
+    copy(w.diag_skip, sizeof(w.diag_skip), "");
+    copy(w.diag_dup, sizeof(w.diag_dup), "");
+#endif
+    return w;
+}
+
+extern "C" {
+
 int mdg_ctx_create(int device, mdg_ctx** out) {
     if (!out) return MDG_INVALID_ARGUMENT;
     *out = nullptr;
@@ -827,6 +859,7 @@ int mdg_ctx_create(int device, mdg_ctx** out) {
         return hip_fail(e);
     }
     c->stream = c->own;
+    c->sw = read_engine_switches();
     *out = c;
     return MDG_OK;
 }
@@ -855,11 +888,6 @@ int mdg_ctx_destroy(mdg_ctx* c) {
         }
         if (c->hsmall) (void)hipHostFree(c->hsmall);
         if (c->own) (void)hipStreamDestroy(c->own);
-    }
-    if (c->counted) {
-        DeviceActivity& d = g_active[c->device];
-        std::lock_guard<std::mutex> g(d.mu);
-        d.ctxs.erase(std::remove(d.ctxs.begin(), d.ctxs.end(), c), d.ctxs.end());
     }
     delete c;
     return MDG_OK;
@@ -935,6 +963,21 @@ int mdg_ctx_stage_kernel(mdg_ctx* c, int stage, const char** name) {
     return MDG_OK;
 }
 
+int mdg_ctx_set_latency_mode(mdg_ctx* c, int on) {
+    if (!c || (on != 0 && on != 1)) return MDG_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> g(c->mu);
+    c->latency = on;
+    return MDG_OK;
+}
+
+int mdg_ctx_reload_switches(mdg_ctx* c) {
+    if (!c) return MDG_INVALID_ARGUMENT;
+    const EngineSwitches w = read_engine_switches();
+    std::lock_guard<std::mutex> g(c->mu);
+    c->sw = w;
+    return MDG_OK;
+}
+
 int mdg_ctx_last_peaks(mdg_ctx* c, size_t spectrum, int which, int32_t* left, int32_t* center,
                        int32_t* right, size_t cap, size_t* count) {
     if (!c || !count || (which != 0 && which != 1)) return MDG_INVALID_ARGUMENT;
@@ -973,6 +1016,7 @@ int mdg_ctx_last_smoothed(mdg_ctx* c, size_t spectrum, double* out, size_t n) {
 // graph's key; a replay with other addresses rewrites them in the graph's nodes
 void clear_io(BatchArgs& a) {
     a.x = a.y = a.sb = nullptr;
+    a.y_rows = nullptr;
     a.out = nullptr;
     a.out_count = nullptr;
     a.out_mse = nullptr;
@@ -980,7 +1024,7 @@ void clear_io(BatchArgs& a) {
 }
 
 bool same_io(const BatchArgs& p, const BatchArgs& q) {
-    return p.x == q.x && p.y == q.y && p.sb == q.sb && p.out == q.out && p.out_count == q.out_count &&
+    return p.x == q.x && p.y == q.y && p.y_rows == q.y_rows && p.sb == q.sb && p.out == q.out && p.out_count == q.out_count &&
            p.out_mse == q.out_mse && p.out_status == q.out_status;
 }
 
@@ -1019,9 +1063,8 @@ int repoint_graph(mdg_ctx::CachedGraph& ge, const BatchArgs& a) {
 // 7740-7766 launched directly, one spectrum alone 0.97-0.98 ms against 0.95
 // (DESIGN.md §8); the host saves ≈10 µs per call.
 int run_pipeline_graphed(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
-    const char* env = std::getenv("MDG_GRAPHS");
     const bool ma = s->smoother == MDG_SMOOTH_MOVING_AVERAGE;
-    if (!(env && std::string(env) == "1") || c->profile_mask ||
+    if (!c->sw.graphs || c->profile_mask ||
         (ma && (int64_t)(s->smooth_window / 2) > a.N))
         return run_pipeline(c, a, s);
     // size every buffer first: the capture must not allocate, and the key needs the
@@ -1029,7 +1072,7 @@ int run_pipeline_graphed(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     int rc = ensure_workspace(c, a.B, a.N, a.n_ignore);
     if (rc) return rc;
     if (ma && chain_supported(a.B, a.N, (int)s->smooth_iterations, (int)s->smooth_window) &&
-        !(std::getenv("MDG_SMOOTH") && std::string(std::getenv("MDG_SMOOTH")) != "chain"))
+        (c->sw.smooth == EngineSwitches::SM_DEFAULT || c->sw.smooth == EngineSwitches::SM_CHAIN))
         (void)ensure_chain(c, chain_bytes(a.B, a.N, (int)s->smooth_window, (int)s->smooth_iterations));
     if ((s->options & MDG_OPTION_EXACT_MSE) && (rc = ensure_exact(c, a.B, a.N))) return rc;
     if (c->graphs_gen != c->ws_gen) {  // buffers moved since these graphs were captured
@@ -1038,18 +1081,14 @@ int run_pipeline_graphed(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     }
     BatchArgs ka = a;
     clear_io(ka);
-    // the kernel-choice overrides (tests, diagnostics) select other kernels, so
-    // they are part of the key too
-    std::string envs;
-    for (const char* e : {"MDG_SMOOTH", "MDG_CHAIN_EXCL", "MDG_FITSUP", "MDG_GFIT", "MDG_TW_G", "MDG_PEAKS", "MDG_MSE_NEARCAP", "MDG_MSE_NPT", "MDG_MSE_PARTS",
-                          "MDG_DIAG_SKIP", "MDG_DIAG_DUP", "MDG_DIAG_PAD", "MDG_DIAG_PAD_SMALL", "MDG_PREP"}) {
-        const char* v = std::getenv(e);
-        envs += v ? v : "\x01";
-        envs += '\0';
-    }
+    // the kernel-choice switches (tests, diagnostics) select other kernels, so they
+    // are part of the key too (the struct is value-initialised: padding included)
     std::vector<unsigned char> key(sizeof(BatchArgs) + sizeof(mdg_settings) + 2 * sizeof(void*) +
                                    sizeof(size_t));
-    key.insert(key.end(), envs.begin(), envs.end());
+    {
+        const unsigned char* sp = (const unsigned char*)&c->sw;
+        key.insert(key.end(), sp, sp + sizeof(EngineSwitches));
+    }
     unsigned char* k = key.data();
     std::memcpy(k, &ka, sizeof(BatchArgs));
     k += sizeof(BatchArgs);
@@ -1221,7 +1260,12 @@ static int batch_host(mdg_ctx* c, size_t b, size_t n, bool shared_x, Upload uplo
     const size_t xrows = shared_x ? 1 : b;
     int rc;
     if ((rc = ensure(c->st_x, xrows * n * 8))) return rc;
-    if ((rc = ensure(c->st_y, b * n * 8))) return rc;
+    // y rows the chain launch decodes while it smooths them (dec_next) are padded to
+    // whole 128-byte lines (kDecRowAlign doubles): every line then belongs to one
+    // decode chunk of one row (chain_decode), so no consumer can pull a line whose
+    // bytes another decoder has yet to publish
+    const size_t n_pad = (n + kDecRowAlign - 1) / kDecRowAlign * kDecRowAlign;
+    if ((rc = ensure(c->st_y, b * n_pad * 8))) return rc;
     if ((rc = ensure(c->st_sb, b * 56))) return rc;  // [sb: 2b doubles][descriptors: 4b][row table: b]
     if ((rc = ensure(c->st_out, std::max<size_t>(1, b * cap) * 24))) return rc;
     // the per-spectrum results in one device row, [mse: 8 b][counts: 4 b][statuses:
@@ -1275,8 +1319,7 @@ static int batch_host(mdg_ctx* c, size_t b, size_t n, bool shared_x, Upload uplo
     // from the page-locked scratch and write the records and the first guess rows of
     // every table into it (no copy either way, no copy-engine round trip;
     // MDG_HOST_DIRECT=0: device copies, as before round 4)
-    const char* hd = std::getenv("MDG_HOST_DIRECT");
-    const bool direct = c->hsmall_dev && !(hd && hd[0] == '0');
+    const bool direct = c->hsmall_dev && c->sw.host_direct;
     c->small_rd = direct ? (const double*)c->hsmall_dev : (const double*)c->st_sb.p;
     c->small_copy = !direct;
     std::memcpy(h_sb, sb, b * 16);
@@ -1287,8 +1330,8 @@ static int batch_host(mdg_ctx* c, size_t b, size_t n, bool shared_x, Upload uplo
     if (!sent_sb && !direct) he = hipMemcpyAsync(c->st_sb.p, h_sb, b * 16, hipMemcpyHostToDevice, st);
     if (he != hipSuccess) return fail(hip_fail(he));
     BatchArgs a;
-    if ((rc = fill_args(c, a, b, n, dx, shared_x ? 0 : n, dy, n, c->small_rd, ignore, n_ignore,
-                        (double*)c->st_out.p, cap, d_cnt, d_mse, d_st)))
+    if ((rc = fill_args(c, a, b, n, dx, shared_x ? 0 : n, dy, c->dec_next ? n_pad : n, c->small_rd, ignore,
+                        n_ignore, (double*)c->st_out.p, cap, d_cnt, d_mse, d_st)))
         return fail(rc);
     if (c->dec_next) {  // the rows are decoded by the pipeline (run_pipeline)
         a.dec_rows = (const int32_t* const*)(c->small_rd + 6 * b);
@@ -1422,8 +1465,7 @@ int mdg_deconvolute_rows_i32(mdg_ctx* c, size_t b, size_t n, const double* axes,
     // rows in mdg_host_alloc memory are decoded by the pipeline straight from host
     // memory, the chain smoother starting on the first chunks while the rest are
     // read (chain_decode; MDG_DEC_OVERLAP=0: DMA and decode first, as other rows)
-    const char* ov = std::getenv("MDG_DEC_OVERLAP");
-    const bool zc = !(ov && ov[0] == '0') && pinned_rows((const void* const*)y_rows, b, n * 4, true);
+    const bool zc = c->sw.dec_overlap && pinned_rows((const void* const*)y_rows, b, n * 4, true);
     auto upload = [&](double* dx, double* dy, hipStream_t st, bool* sent_sb) -> int {
         int rc;
         // batch_host's scratch holds [sb: 2b][descriptors: 4b][row table: b] doubles:
@@ -1799,12 +1841,30 @@ int queue_launch(mdg_queue* q) {
     bool shared = true;
     for (const QueueItem& it : q->open) shared = shared && it.x == x0;
     const QueueItem* items = (const QueueItem*)L.table.p;
-    launch_queue_gather(items, B, (int64_t)n, shared ? 0 : 1, (double*)L.x.p, (double*)L.y.p, (double*)L.sb.p, st);
+    // Each submission's intensity row is read where it lies, through the submission
+    // table itself (BatchArgs::y_rows: row s = items[s].y; the signal boundaries
+    // items[s].sb0 / sb1 likewise): no gather copy of 1 MiB per spectrum. The
+    // identity smoother hands y to detection as the smoothed rows (one strided
+    // base), and distinct axes need their rows side by side: those batches are
+    // gathered as before.
+    const bool in_place = shared && q->s.smoother == MDG_SMOOTH_MOVING_AVERAGE;
+    if (!in_place)
+        launch_queue_gather(items, B, (int64_t)n, shared ? 0 : 1, (double*)L.x.p, (double*)L.y.p, (double*)L.sb.p,
+                            st);
     BatchArgs a;
     int rc = fill_args(c, a, B, n, shared ? x0 : (const double*)L.x.p, shared ? 0 : n, (const double*)L.y.p, n,
                        (const double*)L.sb.p, q->ignore.empty() ? nullptr : q->ignore.data(), q->ignore.size() / 2,
                        (double*)L.out.p, cap, (int32_t*)L.cnt.p, (double*)L.mse.p, (int32_t*)L.st.p);
     if (rc) return rc;
+    if (in_place) {
+        static_assert(sizeof(QueueItem) % 8 == 0 && offsetof(QueueItem, y) % 8 == 0 &&
+                          offsetof(QueueItem, sb1) == offsetof(QueueItem, sb0) + 8,
+                      "the submission table is read as rows of 8-byte words");
+        a.y_rows = (const double* const*)((const char*)items + offsetof(QueueItem, y));
+        a.rows_step = (int)(sizeof(QueueItem) / sizeof(void*));
+        a.sb = (const double*)((const char*)items + offsetof(QueueItem, sb0));
+        a.sb_step = (int)(sizeof(QueueItem) / sizeof(double));
+    }
     if ((rc = run_pipeline(c, a, &q->s))) return rc;
     launch_queue_scatter(items, B, (const double*)L.out.p, (int64_t)cap, (const int32_t*)L.cnt.p,
                          (const double*)L.mse.p, (const int32_t*)L.st.p, st);

@@ -23,6 +23,7 @@ constexpr double kCheckPrecision = 1.0e+3 * 2.220446049250313080847e-16;
 constexpr double kEpsilon = 2.220446049250313080847e-16;  // f64::EPSILON
 constexpr int kIgnoreRow = 64;  // ignore-region pairs per spectrum row, grown in steps of this
 constexpr int kPkSlotWords = 64;   // k_peaks: mask words per look-back slot (the finest chunk)
+constexpr int kDecRowAlign = 16;  // doubles: decoded staging rows start on 128-byte lines (chain_decode)
 constexpr int kDecChunks = 64;     // chunks per row the chain launch's decoders publish (Workspace::dec_flags)
 constexpr int kMseMaxParts = 2048;  // MSE partial sums per spectrum (workspace rows)
 

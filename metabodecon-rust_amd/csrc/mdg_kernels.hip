@@ -311,7 +311,7 @@ __device__ __forceinline__ void prep_spectrum(const BatchArgs& a, const Workspac
     const double x1 = xd ? dec_x(xd, 1) : x[1];
     const double xl = xd ? dec_x(xd, a.N - 1) : x[a.N - 1];
     const double step = x1 - x0;
-    const double sb0 = a.sb[2 * s], sb1 = a.sb[2 * s + 1];
+    const double sb0 = a.sb[(size_t)s * a.sb_step], sb1 = a.sb[(size_t)s * a.sb_step + 1];
     const int64_t bi0 = as_index(floor((sb0 - x0) / step));
     const int64_t bi1 = as_index(ceil((sb1 - x0) / step));
     w.sbi[2 * s] = bi0;
@@ -545,7 +545,7 @@ __global__ __launch_bounds__(64) void k_smooth_pipe(BatchArgs a, Workspace w, in
     const bool valid = g < spw && s < a.B;
     const bool ok = valid && w.status[valid ? s : 0] == 0;
     const int N = a.N;
-    const double* yrow = a.y + (size_t)(valid ? s : 0) * a.y_stride;
+    const double* yrow = y_row(a, valid ? s : 0);
     double* orow = w.smooth + (size_t)(valid ? s : 0) * N;
     const bool feeder = p == 0;
     const bool writer = ok && p == P - 1;
@@ -792,7 +792,9 @@ __device__ __forceinline__ void chain_l2_pull(const double* p, int cnt) {
 }
 
 // Rows decoded while the chain smooths them (mdg_deconvolute_rows_i32 with
-// page-locked rows): the chain launch's first ndec workgroups read the int32 rows
+// page-locked rows; y rows padded to whole 128-byte lines, kDecRowAlign, and a chunk
+// is a whole number of 96-double blocks, 768 bytes, so every line belongs to one
+// chunk of one row and one decoder): the chain launch's first ndec workgroups read the int32 rows
 // straight from host memory and write y_i = raw_i * scale (k_decode_rows_i32's
 // operation) chunk by chunk, kDecChunks chunks per row, chunk-major over the batch
 // (the first chunks of every row first), each chunk published
@@ -895,7 +897,7 @@ __global__ __launch_bounds__(64 * (2 + kChainScalers)) void k_smooth_chain(Batch
     const int nIB = (N + CB - 1) / CB;      // input blocks
     const int nOB = nIB;                    // output blocks
     const int64_t L = w.chain_stride;
-    const double* in = p == 0 ? a.y + (size_t)s * a.y_stride
+    const double* in = p == 0 ? y_row(a, s)
                               : w.chain_tmp + ((size_t)(p - 1) * a.B + s) * L;
     double* out = p == P - 1 ? w.smooth + (size_t)s * N : w.chain_tmp + ((size_t)p * a.B + s) * L;
     double* raw = w.chain_raw + ((size_t)p * a.B + s) * L;
@@ -1031,7 +1033,21 @@ __global__ __launch_bounds__(64 * (2 + kChainScalers)) void k_smooth_chain(Batch
                                                     __HIP_MEMORY_SCOPE_AGENT);
                 const uint64_t nm = ~__ballot(f == a.dec_gen);
                 const int chunks = nm ? __builtin_ctzll(nm) : kDecChunks;
-                up = min(nIB, chunks * dec_block_chunk(nIB));
+                const int nu = min(nIB, chunks * dec_block_chunk(nIB));
+                if (nu > up) {
+                    // consumer side of the decoders' hand-off (MI355X_MICROARCH.md,
+                    // inter-workgroup visibility: one relaxed poll, one agent-scope
+                    // acquire, its wait, then the loads): this CU's L1 is invalidated
+                    // before the pulls, the touches and -- through in_ready, set after
+                    // the wait -- the chain's loads of the new chunks. The rows are of
+                    // whole 128-byte lines per chunk (kDecRowAlign; the host checks it),
+                    // so no line read here holds bytes of a chunk not yet published,
+                    // and the scalar cache (invalidated at this workgroup's start) only
+                    // ever receives lines of published chunks.
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    up = nu;
+                }
             }
             // pull published full input blocks into L2 (16 per wait), so the
             // scalar-cache touches below hit L2 instead of HBM / the MALL
@@ -1242,7 +1258,7 @@ __global__ void k_smooth(BatchArgs a, Workspace w, int iters, int ws) {
     if (s >= a.B) return;
     if (w.status[s]) return;
     const int N = a.N;
-    const double* src = a.y + (size_t)s * a.y_stride;
+    const double* src = y_row(a, s);
     double* out = w.smooth + (size_t)s * N;
     double* tmp0 = w.tmp0 + (size_t)s * N;
     double* tmp1 = w.tmp1 + (size_t)s * N;
@@ -2418,7 +2434,7 @@ __device__ __forceinline__ void solve(const Stencil& q, double* out3) {
 __device__ __forceinline__ void fit_init_peak(const BatchArgs& a, const Workspace& w, int s, size_t base,
                                               int p, int l, int c, int r) {
     const double* x = a.x + (size_t)s * a.x_stride;
-    const double* y = a.y + (size_t)s * a.y_stride;
+    const double* y = y_row(a, s);
     Stencil q{x[l], x[c], x[r], y[l], y[c], y[r]};
     double* rx = w.rx + 3 * base + 3 * (size_t)p;
     double* ry = w.ry + 3 * base + 3 * (size_t)p;
@@ -2437,7 +2453,7 @@ __device__ __forceinline__ void fit_init_pair(const BatchArgs& a, const Workspac
                                               int p1, int l1, int c1, int r1, int p2, int l2, int c2,
                                               int r2) {
     const double* x = a.x + (size_t)s * a.x_stride;
-    const double* y = a.y + (size_t)s * a.y_stride;
+    const double* y = y_row(a, s);
     const double xa[6] = {x[l1], x[c1], x[r1], x[l2], x[c2], x[r2]};
     const double ya[6] = {y[l1], y[c1], y[r1], y[l2], y[c2], y[r2]};
 #pragma unroll
@@ -3209,7 +3225,7 @@ __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int
     const double* __restrict__ prmv = final_params(w, s, pbase);
     const const_f64_ptr prm = (const_f64_ptr)prmv;
     const double* x = a.x + (size_t)s * a.x_stride;
-    const double* y = a.y + (size_t)s * a.y_stride;
+    const double* y = y_row(a, s);
     const int nig = w.n_ig[s];
     const int64_t total = mse_len(w, s);
     // every workgroup counts the retained Lorentzians (the last one reports the
@@ -3463,7 +3479,7 @@ __global__ void k_mse_exact_res(BatchArgs a, Workspace w, double* res, int64_t r
     const int P = w.kept_count[s];
     const double* __restrict__ kept = w.kept + 3 * (size_t)s * w.capD;
     const double* x = a.x + (size_t)s * a.x_stride;
-    const double* y = a.y + (size_t)s * a.y_stride;
+    const double* y = y_row(a, s);
     const int nig = w.n_ig[s];
     const int64_t total = mse_len(w, s);
     const bool fast = w.x_ok[s] && w.unsafe_kept[s] == 0;
@@ -3583,12 +3599,12 @@ __global__ void k_diag_nop(BatchArgs a, Workspace w) {
 __global__ void k_diag_nop_small(int32_t* p, int b) {
     if (b < 0) p[0] = 0;
 }
-void launch_diag_nop(const BatchArgs& a, const Workspace& w, hipStream_t st) {
-    if (std::getenv("MDG_DIAG_PAD_SMALL")) hipLaunchKernelGGL(k_diag_nop_small, dim3(1), dim3(64), 0, st, w.status, a.B);
+void launch_diag_nop(const BatchArgs& a, const Workspace& w, const EngineSwitches& sw, hipStream_t st) {
+    if (sw.diag_pad_small) hipLaunchKernelGGL(k_diag_nop_small, dim3(1), dim3(64), 0, st, w.status, a.B);
     else {
         // MDG_DIAG_PAD_WGS: workgroups of the no-op (the cost of workgroup dispatch)
-        const char* g = std::getenv("MDG_DIAG_PAD_WGS");
-        launch_k(k_diag_nop, dim3(g ? std::max(1, std::atoi(g)) : 1), dim3(g ? 256 : 64), 0, st, a, w);
+        const int g = sw.diag_pad_wgs;
+        launch_k(k_diag_nop, dim3(g ? std::max(1, g) : 1), dim3(g ? 256 : 64), 0, st, a, w);
     }
 }
 #endif
@@ -3603,11 +3619,10 @@ static const char* launch_pipe(const BatchArgs& a, const Workspace& w, int iters
 }
 
 template <int WS>
-static const char* launch_chain(const BatchArgs& a, const Workspace& w, int iters, hipStream_t st,
-                                int fused_prep) {
+static const char* launch_chain(const BatchArgs& a, const Workspace& w, int iters, const EngineSwitches& sw,
+                                hipStream_t st, int fused_prep) {
     const unsigned grid = 8u * (unsigned)iters * cdiv(a.B, 8);
-    const char* excl_env = std::getenv("MDG_CHAIN_EXCL");  // 0 = never (measurements)
-    const bool excl = (int)grid <= kChainExclMax && !(excl_env && excl_env[0] == '0');
+    const bool excl = (int)grid <= kChainExclMax && sw.chain_excl;  // MDG_CHAIN_EXCL=0: never (measurements)
     // rows still in host memory (a.dec_rows; the pipeline fuses the prep then): 32
     // decoders up to 4 spectra, 64 beyond (chain_decode; a multiple of 8 keeps the
     // chain workgroups' XCD mapping)
@@ -3630,28 +3645,26 @@ static const char* launch_chain(const BatchArgs& a, const Workspace& w, int iter
 }
 // chain kernel (one CU per pass) for windows <= 8 and batches <= 512 (B * iters
 // <= 2048) when its buffers are set up and MDG_SMOOTH does not force another
-bool smooth_uses_chain(const BatchArgs& a, const Workspace& w, int iters, int ws) {
-    const char* force = std::getenv("MDG_SMOOTH");
-    const bool chain = force ? std::string(force) == "chain" : true;
+bool smooth_uses_chain(const BatchArgs& a, const Workspace& w, int iters, int ws, const EngineSwitches& sw) {
+    const bool chain = sw.smooth == EngineSwitches::SM_DEFAULT || sw.smooth == EngineSwitches::SM_CHAIN;
     return chain && w.chain_P >= iters && chain_supported(a.B, a.N, iters, ws);
 }
-const char* launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int ws, hipStream_t st,
-                          int fused_prep) {
+const char* launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int ws, const EngineSwitches& sw,
+                          hipStream_t st, int fused_prep) {
     // the chain kernel; then lane-pipelined (window fits the register FIFO); the
     // one-lane-per-spectrum kernel otherwise.
     // MDG_SMOOTH = chain | pipe | generic forces one (tests); an
     // unsupported shape falls through. fused_prep (chain only): the chain kernel
     // runs k_prep's work itself.
-    const char* force = std::getenv("MDG_SMOOTH");
-    if (smooth_uses_chain(a, w, iters, ws)) {
+    if (smooth_uses_chain(a, w, iters, ws, sw)) {
         switch (ws) {
-            case 2: return launch_chain<2>(a, w, iters, st, fused_prep);
-            case 3: return launch_chain<3>(a, w, iters, st, fused_prep);
-            case 4: return launch_chain<4>(a, w, iters, st, fused_prep);
-            case 5: return launch_chain<5>(a, w, iters, st, fused_prep);
-            case 6: return launch_chain<6>(a, w, iters, st, fused_prep);
-            case 7: return launch_chain<7>(a, w, iters, st, fused_prep);
-            case 8: return launch_chain<8>(a, w, iters, st, fused_prep);
+            case 2: return launch_chain<2>(a, w, iters, sw, st, fused_prep);
+            case 3: return launch_chain<3>(a, w, iters, sw, st, fused_prep);
+            case 4: return launch_chain<4>(a, w, iters, sw, st, fused_prep);
+            case 5: return launch_chain<5>(a, w, iters, sw, st, fused_prep);
+            case 6: return launch_chain<6>(a, w, iters, sw, st, fused_prep);
+            case 7: return launch_chain<7>(a, w, iters, sw, st, fused_prep);
+            case 8: return launch_chain<8>(a, w, iters, sw, st, fused_prep);
             default: break;
         }
     }
@@ -3659,7 +3672,7 @@ const char* launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int
     // 131072 points, B = 1024: 4.8 ms; configs[3], 4096 x 65536: 2.7 ms; round 2's
     // wave-per-pass kernel took 9.9 and 17.0); windows outside its
     // register FIFO the one-lane-per-spectrum kernel
-    const bool pipe = !force || std::string(force) == "pipe";
+    const bool pipe = sw.smooth == EngineSwitches::SM_DEFAULT || sw.smooth == EngineSwitches::SM_PIPE;
     if (pipe && iters >= 1 && iters <= 32 && a.N > ws + 1) {
         switch (ws) {
             case 2: return launch_pipe<2>(a, w, iters, st);
@@ -3680,14 +3693,14 @@ const char* launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int
 void launch_flags(const BatchArgs& a, const Workspace& w, hipStream_t st) {
     launch_k(k_flags, dim3(cdiv(a.N, 256), a.B), dim3(256), 0, st, a, w);
 }
-const char* launch_peaks(const BatchArgs& a, const Workspace& w, int detector_only, hipStream_t st) {
+const char* launch_peaks(const BatchArgs& a, const Workspace& w, int detector_only, const EngineSwitches& sw,
+                         hipStream_t st) {
     // k_peaks scores the peaks it writes (scorer.rs:65-75) for the selector. Fine
     // (staged) chunks up to 512 workgroups of 64-word chunks (B <= 16 at N = 131072:
     // blood, 13.2 / 12.9 / 15.4 / 17.5 us at B = 1 / 4 / 8 / 16 against the coarse
     // chunks' 21.3 / 21.9 / 22.9 / 23.1; synthetic B = 64: 59.8 against 52.6, B = 256:
     // 230 against 216); MDG_PEAKS = fine | coarse forces one (tests)
-    const char* force = std::getenv("MDG_PEAKS");
-    const bool fine = force ? std::string(force) == "fine" : (size_t)cdiv(w.W, 64) * a.B <= 512;
+    const bool fine = sw.peaks ? sw.peaks == 1 : (size_t)cdiv(w.W, 64) * a.B <= 512;
     if (fine) {
         launch_k(k_peaks<64, 256>, dim3(cdiv(w.W, 64), a.B), dim3(256), 0, st, a, w, detector_only, 1);
         return "k_flags+k_peaks<64>";
@@ -3711,38 +3724,37 @@ const char* launch_select(const BatchArgs& a, const Workspace& w, int detector_o
 // 373 us at B = 16 against 403 for the (98, B) grid "tw7", 270 / 268 at B = 8, 204
 // against tf's 185 at B = 4); beyond, one point per lane with the update separate
 // ("plain": 79 / 57 us per spectrum at B = 32 / 256). When other engine contexts on
-// the device have run pipelines, B = 1 keeps "tw7": "tf"'s lead alone is gone as
-// soon as a second context has been used, and 18 concurrent B = 1 pipelines run
-// 6.6k spectra/s with "tf" against 7.8-8.1k with "tw7". MDG_FITSUP = tf | tf12 | tw7 |
-// tw3s | twf | twf1 | twf3s | plain forces one (all bit-identical; tests,
-// measurements); any other value is ignored.
-static std::string fit_choice(const BatchArgs& a) {
-    if (const char* force = std::getenv("MDG_FITSUP")) {
-        const std::string f(force);
-        if (f == "tf" || f == "tf12" || f == "tw7" || f == "tw3s" || f == "twf" || f == "twf1" || f == "twf3s" ||
-            f == "plain")
-            return f;
-    }
-    if (a.B == 1) return a.contexts > 1 ? "tw7" : "tf12";
+// the device run pipelines concurrently, B = 1 keeps "tw7": "tf"'s lead alone is gone
+// as soon as a second context runs, and 18 concurrent B = 1 pipelines run 6.6k
+// spectra/s with "tf" against 7.8-8.1k with "tw7". Which of the two a context takes
+// is its latency mode (mdg_ctx_set_latency_mode: on by default -- one spectrum at a
+// time with the GPU to itself; callers running many contexts at once turn it off).
+// MDG_FITSUP = tf | tf12 | tw7 | tw3s | twf | twf1 | twf3s | plain forces one (all
+// bit-identical; tests, measurements; read into the context's switches, where any
+// other value is ignored).
+static std::string fit_choice(const BatchArgs& a, const EngineSwitches& sw) {
+    if (sw.fitsup[0]) return sw.fitsup;
+    if (a.B == 1) return a.latency ? "tf12" : "tw7";
     return a.B <= 4 ? "tf" : a.B <= 24 ? "twf1" : "plain";
 }
-bool fit_sup_fused(const BatchArgs& a) { return fit_choice(a) != "plain"; }
-const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st) {
-    const std::string f = fit_choice(a);
+bool fit_sup_fused(const BatchArgs& a, const EngineSwitches& sw) { return fit_choice(a, sw) != "plain"; }
+const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int it, const EngineSwitches& sw,
+                           hipStream_t st) {
+    const std::string f = fit_choice(a, sw);
     // MDG_TW_G (tuning): workgroups per spectrum; tiles beyond them grid-stride
-    const char* tg = std::getenv("MDG_TW_G");
+    const int tg = sw.tw_g;
     if (f == "tw7") {
         // 7 evaluator waves: 1 peak block x 7 point subsets, 63 points per workgroup:
         // one workgroup per tile of a 2048-peak spectrum (98)
         using SH = TwShape<63, 1, 7>;
-        const int g = tg ? std::max(1, std::atoi(tg)) : (3 * 2048 + 62) / 63;
+        const int g = tg ? tg : (3 * 2048 + 62) / 63;
         launch_k(k_fit_sup_tw<SH>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
         return "k_fit_sup_tw<63, 1, 7>";
     }
     if (f == "tw3s") {
         // single-buffered 63-point tiles, 3 evaluator waves: four workgroups per CU
         using SH = TwShape<63, 1, 3, true>;
-        const int g = tg ? std::max(1, std::atoi(tg)) : (3 * 2048 + 62) / 63;
+        const int g = tg ? tg : (3 * 2048 + 62) / 63;
         launch_k(k_fit_sup_tw<SH>, dim3(g, a.B), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
         return "k_fit_sup_tw<63, 1, 3, SB>";
     }
@@ -3758,30 +3770,30 @@ const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int i
         }
         if (f == "twf3s") {
             using SH = TwShape<63, 1, 3, true>;
-            const int g = tg ? std::max(1, std::atoi(tg)) : 4 * cus;
+            const int g = tg ? tg : 4 * cus;
             launch_k(k_fit_sup_twf<SH>, dim3(g), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
             return "k_fit_sup_twf<63, 1, 3, SB>";
         }
         if (f == "twf") {
             using SH = TwShape<63, 2, 7>;
-            const int g = tg ? std::max(1, std::atoi(tg)) : cus;
+            const int g = tg ? tg : cus;
             launch_k(k_fit_sup_twf<SH>, dim3(g), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
             return "k_fit_sup_twf<63, 2, 7>";
         }
         using SH = TwShape<63, 1, 7>;
-        const int g = tg ? std::max(1, std::atoi(tg)) : 2 * cus;
+        const int g = tg ? tg : 2 * cus;
         launch_k(k_fit_sup_twf<SH>, dim3(g), dim3(64 * (SH::EW + 1)), 0, st, a, w, it);
         return "k_fit_sup_twf<63, 1, 7>";
     }
     if (f == "tf12") {
         // 12-point tiles: twice the workgroups, half the evaluation per workgroup
-        const int g = tg ? std::max(1, std::atoi(tg)) : (3 * 2048 + 11) / 12;
+        const int g = tg ? tg : (3 * 2048 + 11) / 12;
         launch_k(k_fit_sup_tf<12>, dim3(g, a.B), dim3(64 * (kTfEW + 1)), 0, st, a, w, it);
         return "k_fit_sup_tf<12>";
     }
     if (f == "tf" || f == "twf" || f == "twf1" || f == "twf3s") {
         // 24 points per workgroup: one workgroup per tile of a 2048-peak spectrum (256)
-        const int g = tg ? std::max(1, std::atoi(tg)) : (3 * 2048 + 23) / 24;
+        const int g = tg ? tg : (3 * 2048 + 23) / 24;
         launch_k(k_fit_sup_tf<kTfQ>, dim3(g, a.B), dim3(64 * (kTfEW + 1)), 0, st, a, w, it);
         return "k_fit_sup_tf";
     }
@@ -3807,22 +3819,22 @@ constexpr int kLocNPT = 2;
 // launch; the headline queue, B = 256: 3.6 against 3.8 us per spectrum, 15.76-15.78k
 // against 15.67-15.68k spectra/s; B = 1: 24 against 18 -- a single spectrum wants the
 // finer tiles)
-static int mse_npt(const BatchArgs& a) {
-    if (const char* e = std::getenv("MDG_MSE_NPT")) return std::atoi(e) == 4 ? 4 : kLocNPT;
+static int mse_npt(const BatchArgs& a, const EngineSwitches& sw) {
+    if (sw.mse_npt) return sw.mse_npt == 4 ? 4 : kLocNPT;
     return a.B >= 8 ? 4 : kLocNPT;
 }
-int mse_nparts(const BatchArgs& a) {
-    if (const char* e = std::getenv("MDG_MSE_PARTS")) return std::max(1, std::min(kMseMaxParts, std::atoi(e)));
-    const int tp = kLocTP * mse_npt(a);
+int mse_nparts(const BatchArgs& a, const EngineSwitches& sw) {
+    if (sw.mse_parts) return std::max(1, std::min(kMseMaxParts, sw.mse_parts));
+    const int tp = kLocTP * mse_npt(a, sw);
     return std::max(1, std::min({kMseMaxParts, (a.N + tp - 1) / tp, std::max(1, 8192 / a.B)}));
 }
-const char* launch_mse(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st) {
+const char* launch_mse(const BatchArgs& a, const Workspace& w, int nparts, const EngineSwitches& sw,
+                       hipStream_t st) {
     // MDG_MSE_NEARCAP (tests): a smaller near-list capacity, to exercise the kernel's
     // own direct fallback for crowded tiles
-    int cap = kLocNear;
-    if (const char* e = std::getenv("MDG_MSE_NEARCAP")) cap = std::max(0, std::min(kLocNear, std::atoi(e)));
+    const int cap = sw.mse_nearcap >= 0 ? std::min(kLocNear, sw.mse_nearcap) : kLocNear;
     // nparts tile workgroups per spectrum plus its retain workgroup
-    if (mse_npt(a) == 4) {
+    if (mse_npt(a, sw) == 4) {
         launch_k(k_mse_local<4>, dim3((nparts + 1) * a.B), dim3(256), 0, st, a, w, nparts, cap);
         return "k_mse_local<4>";
     }

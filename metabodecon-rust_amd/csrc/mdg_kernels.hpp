@@ -19,9 +19,14 @@ struct BatchArgs {
     int N;                // points per spectrum
     const double* x;      // row s at x + s*x_stride (x_stride 0: shared axis)
     int64_t x_stride;
-    const double* y;      // row s at y + s*y_stride
+    const double* y;      // row s at y + s*y_stride (y_rows null)
     int64_t y_stride;
-    const double* sb;     // 2B signal boundaries (ppm, ordered as Spectrum stores them)
+    // rows read in place through a table of row pointers (the spectrum queue: each
+    // submission's own row, no gather copy): row s at y_rows[s * rows_step]
+    const double* const* y_rows;
+    int rows_step;        // pointers between consecutive rows' entries of y_rows
+    int sb_step;          // doubles between consecutive spectra's signal-boundary pairs
+    const double* sb;     // signal boundaries of spectrum s at sb[s*sb_step], sb[s*sb_step+1] (ppm, ordered as Spectrum stores them)
     int n_ignore;         // merged ignore regions (ppm), shared by the batch
     const double* ignore; // 2 * n_ignore doubles in device memory (null when none)
     double* out;          // B x cap x {sfhw, hw2, maxp}
@@ -29,7 +34,7 @@ struct BatchArgs {
     int32_t* out_count;
     double* out_mse;
     int32_t* out_status;
-    int contexts;         // engine contexts with a pipeline in the last 50 ms on the device, max 2 (kernel choice only)
+    int latency;          // the context's latency mode (mdg_ctx_set_latency_mode; kernel choice only)
     // mdg_deconvolute_rows_i32 with page-locked rows: the pipeline decodes the rows
     // into y / x itself, reading them from host memory (null: y and x hold them)
     const int32_t* const* dec_rows;  // B host-mapped int32 rows (device copy of the table)
@@ -104,6 +109,42 @@ struct Workspace {
     const int32_t* fit_iters_s;  // B fit iteration counts (<= the launched count)
 };
 
+// row s of a batch's intensities (BatchArgs::y_rows or the strided rows)
+__device__ __host__ inline const double* y_row(const BatchArgs& a, int s) {
+    return a.y_rows ? a.y_rows[(size_t)s * a.rows_step] : a.y + (size_t)s * a.y_stride;
+}
+
+// Engine switches: the MDG_* environment variables that choose among the shipped,
+// bit-exact kernels (tests, measurements). Read once per context, when it is created
+// (mdg_ctx_create) or on an explicit mdg_ctx_reload_switches -- never on a call's
+// path (a getenv there races a concurrent setenv, costs time every call, and makes a
+// context's behaviour depend on when the variable was read).
+// (ints and char arrays only: no padding, the bytes are part of the graph keys)
+struct EngineSwitches {
+    enum { SM_DEFAULT = 0, SM_CHAIN, SM_PIPE, SM_GENERIC, SM_OTHER };
+    int smooth = SM_DEFAULT;     // MDG_SMOOTH = chain | pipe | generic (other values: the generic kernel)
+    int chain_excl = 1;          // MDG_CHAIN_EXCL=0: never whole-CU chain workgroups
+    int peaks = 0;               // MDG_PEAKS: 0 by batch size, 1 fine, 2 coarse (any other value)
+    char fitsup[8] = {};         // MDG_FITSUP: a shipped fit kernel's name ("": by batch size)
+    int tw_g = 0;                // MDG_TW_G: term-fold workgroups (0: the kernel's default)
+    int gfit = 24;               // MDG_GFIT: k_fit_sup workgroups per spectrum
+    int mse_npt = 0;             // MDG_MSE_NPT = 2 | 4 (0: by batch size)
+    int mse_parts = 0;           // MDG_MSE_PARTS (0: by shape)
+    int mse_nearcap = -1;        // MDG_MSE_NEARCAP (-1: kLocNear)
+    int prep_separate = 0;      // MDG_PREP=separate
+    int graphs = 0;              // MDG_GRAPHS=1
+    int host_direct = 1;         // MDG_HOST_DIRECT=0: device copies of the small inputs / results
+    int dec_overlap = 1;         // MDG_DEC_OVERLAP=0: compact rows by DMA + decode launch
+    // diagnostic builds only (make diag)
+    char diag_skip[32] = {};
+    char diag_dup[64] = {};
+    int diag_pad = 0;
+    int diag_pad_small = 0;
+    int diag_pad_wgs = 0;
+};
+// the switches as the environment holds them now
+EngineSwitches read_engine_switches();
+
 // Bytes of the k_smooth_chain buffers for (B, N, passes) and their row stride.
 int64_t chain_stride_for(int N, int ws);
 size_t chain_bytes(int B, int N, int ws, int passes);
@@ -142,24 +183,27 @@ inline void launch_k(void (*k)(BatchArgs, Workspace, P...), dim3 g, dim3 b, size
 
 void launch_prep(const BatchArgs& a, const Workspace& w, hipStream_t st);
 #ifdef MDG_DIAG
-void launch_diag_nop(const BatchArgs& a, const Workspace& w, hipStream_t st);
+void launch_diag_nop(const BatchArgs& a, const Workspace& w, const EngineSwitches& sw, hipStream_t st);
 #endif
-bool smooth_uses_chain(const BatchArgs& a, const Workspace& w, int iters, int ws);
-const char* launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int ws, hipStream_t st,
-                          int fused_prep = 0);
+bool smooth_uses_chain(const BatchArgs& a, const Workspace& w, int iters, int ws, const EngineSwitches& sw);
+const char* launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int ws, const EngineSwitches& sw,
+                          hipStream_t st, int fused_prep = 0);
 void launch_flags(const BatchArgs& a, const Workspace& w, hipStream_t st);
-const char* launch_peaks(const BatchArgs& a, const Workspace& w, int detector_only, hipStream_t st);
+const char* launch_peaks(const BatchArgs& a, const Workspace& w, int detector_only, const EngineSwitches& sw,
+                         hipStream_t st);
 const char* launch_select(const BatchArgs& a, const Workspace& w, int detector_only,
                           double threshold, hipStream_t st);
 // returns true when the launched kernel also did the stencil update (no k_fit_update)
-bool fit_sup_fused(const BatchArgs& a);
-const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st);
+bool fit_sup_fused(const BatchArgs& a, const EngineSwitches& sw);
+const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int it, const EngineSwitches& sw,
+                           hipStream_t st);
 void launch_fit_update(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st);
 void launch_retain(const BatchArgs& a, const Workspace& w, hipStream_t st);
 // MSE tiles per spectrum for launch_mse (<= kMseMaxParts)
-int mse_nparts(const BatchArgs& a);
+int mse_nparts(const BatchArgs& a, const EngineSwitches& sw);
 // k_mse_local: the MSE and the retained Lorentzians (out rows, counts, statuses)
-const char* launch_mse(const BatchArgs& a, const Workspace& w, int nparts, hipStream_t st);
+const char* launch_mse(const BatchArgs& a, const Workspace& w, int nparts, const EngineSwitches& sw,
+                       hipStream_t st);
 // exact-order MSE of every spectrum of the batch (MDG_OPTION_EXACT_MSE), after
 // launch_mse: squared residuals into res (B rows of res_row >= N doubles), then the
 // reference's left folds; overwrites out_mse

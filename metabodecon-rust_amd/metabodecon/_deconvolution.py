@@ -585,93 +585,6 @@ class Deconvoluter:
                         results[i] = r
         return results
 
-    def _run_device(self, spectra: list[Spectrum]):
-        """Device-resident variant of ``_run`` for the multi-GPU path: the block's
-        inputs go to HBM once, ``mdg_deconvolute_batch_device`` runs one batched
-        pipeline per distinct length on this process's GPU, and the results stay
-        in HBM as torch tensors for the RCCL gather:
-        (status int32[b], counts int32[b], mse f64[b], tables f64[b, cap, 3]),
-        with cap = the largest count of the block (>= 1)."""
-        import torch
-        dev_index = nat.default_device() if self.device is None else self.device
-        dev = torch.device("cuda", dev_index)
-        b_all = len(spectra)
-        by_n: dict[int, list[int]] = {}
-        for i, sp in enumerate(spectra):
-            if not isinstance(sp, Spectrum):
-                raise TypeError("expected metabodecon.Spectrum")
-            by_n.setdefault(len(sp), []).append(i)
-        ign = self._ignore_array()
-        ctx = nat.context(dev_index)
-        status = torch.zeros(b_all, dtype=torch.int32, device=dev)
-        counts = torch.zeros(b_all, dtype=torch.int32, device=dev)
-        mse = torch.zeros(b_all, dtype=torch.float64, device=dev)
-        parts = []
-        parts_keep = []  # device inputs read by enqueued work (torch must not reuse them)
-        for n, idx in by_n.items():
-            b = len(idx)
-            raws = [spectra[i]._raw for i in idx]
-            with ctx.lock:
-                if all(r is not None for r in raws):
-                    # Bruker rows in their compact form (int32 samples, the axis
-                    # formula): a quarter of the bytes over PCIe, decoded on the
-                    # device bit for bit (mdg_decode_rows_i32_device)
-                    hr = ctx.pinned_rows("raw", ((b * n + 1) // 2,))  # b x n int32
-                    nr = hr.numpy().view(np.int32)[: b * n].reshape(b, n)
-                    for r, raw in enumerate(raws):
-                        nr[r] = raw[0]
-                    desc = torch.tensor([[*r[2], r[1]] for r in raws], dtype=torch.float64)
-                    d_raw = hr.to(dev, non_blocking=True)
-                    d_desc = desc.to(dev)
-                    x = torch.empty((b, n), dtype=torch.float64, device=dev)
-                    y = torch.empty((b, n), dtype=torch.float64, device=dev)
-                    torch.cuda.current_stream(dev).synchronize()  # the buffers are reused
-                    rc = nat.lib().mdg_decode_rows_i32_device(
-                        ctx.handle, b, n, d_raw.data_ptr(), d_desc.data_ptr(), x.data_ptr(),
-                        y.data_ptr())
-                    if rc:
-                        raise exc.UnexpectedError(f"GPU engine failure: {nat.strerror(rc)}")
-                    # the pipeline below runs on the same context stream, after it;
-                    # the device rows stay referenced until the context synchronises
-                    parts_keep += [d_raw, d_desc]
-                else:
-                    # host rows gathered into the context's page-locked buffers, then
-                    # one asynchronous DMA each (not a pageable copy of fresh arrays)
-                    hx = ctx.pinned_rows("x", (b, n))
-                    hy = ctx.pinned_rows("y", (b, n))
-                    nx, ny = hx.numpy(), hy.numpy()
-                    for r, i in enumerate(idx):
-                        nx[r] = spectra[i].chemical_shifts
-                        ny[r] = spectra[i].intensities
-                    x = hx.to(dev, non_blocking=True)
-                    y = hy.to(dev, non_blocking=True)
-                    torch.cuda.current_stream(dev).synchronize()  # the buffers are reused
-            sb = torch.tensor([spectra[i].signal_boundaries for i in idx], dtype=torch.float64,
-                              device=dev)
-            cap = n // 2 + 2
-            out = torch.empty((b, cap, 3), dtype=torch.float64, device=dev)
-            cnt = torch.zeros(b, dtype=torch.int32, device=dev)
-            m = torch.zeros(b, dtype=torch.float64, device=dev)
-            st = torch.zeros(b, dtype=torch.int32, device=dev)
-            torch.cuda.synchronize(dev)  # inputs written on torch's stream
-            with ctx.lock:
-                rc = nat.lib().mdg_deconvolute_batch_device(
-                    ctx.handle, b, n, x.data_ptr(), n, y.data_ptr(), n, sb.data_ptr(),
-                    ctypes.byref(self._s), nat.ptr(ign) if ign.size else None, ign.size // 2,
-                    out.data_ptr(), cap, cnt.data_ptr(), m.data_ptr(), st.data_ptr())
-                if rc:
-                    raise exc.UnexpectedError(f"GPU engine failure: {nat.strerror(rc)}")
-                ctx.synchronize()
-            ii = torch.tensor(idx, dtype=torch.int64, device=dev)
-            status[ii], counts[ii], mse[ii] = st, cnt, m
-            parts.append((ii, out))
-        width = max(1, int(counts.max().item())) if b_all else 1
-        tables = torch.zeros((b_all, width, 3), dtype=torch.float64, device=dev)
-        for ii, out in parts:
-            w = min(width, out.shape[1])
-            tables[ii, :w] = out[:, :w]
-        return status, counts, mse, tables
-
     def _collect(self, results) -> list[Deconvolution]:
         out = []
         snap = self._s.copy()  # one snapshot of the settings for the call's results

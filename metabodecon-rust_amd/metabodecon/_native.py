@@ -54,7 +54,7 @@ EXPORTS = [
     "mdg_queue_create", "mdg_queue_submit", "mdg_queue_flush", "mdg_queue_set_flush_us",
     "mdg_queue_synchronize",
     "mdg_queue_lane", "mdg_queue_stats", "mdg_queue_destroy", "mdg_queue_fail_next_launch",
-    "mdg_jcampdx_decode",
+    "mdg_jcampdx_decode", "mdg_ctx_set_latency_mode", "mdg_ctx_reload_switches",
 ]
 
 
@@ -236,6 +236,8 @@ def _declare(L):
     L.mdg_ctx_stage_times.argtypes = [_vp, _dp, _u64p, ctypes.c_int]
     L.mdg_ctx_reset_stage_times.argtypes = [_vp]
     L.mdg_ctx_stage_kernel.argtypes = [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p)]
+    L.mdg_ctx_set_latency_mode.argtypes = [_vp, ctypes.c_int]
+    L.mdg_ctx_reload_switches.argtypes = [_vp]
     L.mdg_deconvolute.argtypes = [_vp, _dp, _dp, _sz, ctypes.c_double, ctypes.c_double, sp, _dp,
                                   _sz, _dp, _sz, _szp, _dp]
     L.mdg_deconvolute_batch.argtypes = [_vp, _sz, _sz, _dp, _sz, _dp, _sz, _dp, sp, _dp, _sz,
@@ -362,6 +364,7 @@ class Context:
         self.device = device
         self.lock = threading.Lock()
         self._host: dict = {}  # host_rows / pinned_rows buffers
+        _live.add(self)
 
     def host_rows(self, name: str, shape: tuple, dtype=np.float64) -> np.ndarray:
         """A C-contiguous host array of `shape` for this context's host-buffer calls
@@ -383,20 +386,6 @@ class Context:
             self._host[name] = buf
         return buf[:need].view(dt).reshape(shape)
 
-    def pinned_rows(self, name: str, shape: tuple):
-        """A page-locked torch f64 CPU tensor of `shape` kept across calls (grown
-        geometrically), for host rows that torch sends to the device
-        (`Deconvoluter._run_device`): an asynchronous DMA instead of a pageable
-        copy from freshly stacked arrays."""
-        import torch
-        need = int(np.prod(shape)) * 8
-        buf = self._host.get("pinned:" + name)
-        if buf is None or buf.numel() < need:
-            size = max(need, 2 * buf.numel() if buf is not None else 0)
-            buf = torch.empty(size, dtype=torch.uint8, pin_memory=True)
-            self._host["pinned:" + name] = buf
-        return buf[:need].view(torch.float64).view(shape)
-
     def close(self):
         if getattr(self, "handle", None):
             lib().mdg_ctx_destroy(self.handle)
@@ -407,6 +396,20 @@ class Context:
             self.close()
         except Exception:
             pass
+
+    def set_latency_mode(self, on: bool):
+        """mdg_ctx_set_latency_mode: a one-spectrum pipeline of this context expects
+        the GPU to itself (True, the engine's default) or shares it with other
+        contexts running concurrently (False). Bit-identical results either way."""
+        st = lib().mdg_ctx_set_latency_mode(self.handle, 1 if on else 0)
+        if st:
+            raise RuntimeError(strerror(st))
+
+    def reload_switches(self):
+        """Re-read the MDG_* engine switches from the environment (the engine reads
+        them once, when the context is created)."""
+        if getattr(self, "handle", None):
+            lib().mdg_ctx_reload_switches(self.handle)
 
     def set_stream(self, stream_ptr: int | None):
         lib().mdg_ctx_set_stream(self.handle, _vp(stream_ptr or 0))
@@ -506,6 +509,13 @@ class SpectrumQueue:
             raise RuntimeError(f"mdg_queue_create failed: {strerror(st)}")
         self.handle, self.device, self.n = h, device, n
         self.max_batch, self.lanes = max_batch, lanes
+        _live.add(self)
+
+    def reload_switches(self):
+        """Re-read the MDG_* engine switches on every lane context."""
+        if getattr(self, "handle", None):
+            for k in range(self.lanes):
+                self.lane(k).reload_switches()
 
     def submit(self, x_ptr: int, y_ptr: int, sb, out_ptr: int, cap: int, count_ptr: int,
                mse_ptr: int, status_ptr: int) -> None:
@@ -563,6 +573,16 @@ class SpectrumQueue:
 
 _ctx: dict[int, Context] = {}
 _ctx_lock = threading.Lock()
+# every live Context / SpectrumQueue, for reload_switches
+_live: "weakref.WeakSet" = weakref.WeakSet()
+
+
+def reload_switches() -> None:
+    """Re-read the MDG_* engine switches (tests, measurements) on every live context
+    and queue of this process: the engine reads the environment only when a context
+    is created, never on a call's path."""
+    for obj in list(_live):
+        obj.reload_switches()
 
 
 def device_count() -> int:
@@ -608,7 +628,9 @@ def lane_contexts(device: int | None, n: int) -> list[Context]:
     with _ctx_lock:
         lanes = _lanes.setdefault(device, [])
         while len(lanes) < n:
-            lanes.append(Context(device))
+            c = Context(device)
+            c.set_latency_mode(False)  # lanes run concurrently: no B = 1 pipeline has the GPU to itself
+            lanes.append(c)
         return lanes[:n]
 
 

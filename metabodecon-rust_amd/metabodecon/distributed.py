@@ -5,22 +5,31 @@ so a batch is sharded into contiguous blocks, one per rank, with no data-path
 collective. The only exchange is the gather of the results: per spectrum its
 (status, count, mse) record and its Lorentzian table, padded to the largest count,
 packed into one buffer per rank and sent in ONE gather to the collecting rank
-(``gather_packed``; an all-gather only when every rank asks for the results),
-after a two-element all_reduce that agrees on the width and on the first failure
-(RCCL over xGMI with the ``nccl`` backend, ``gloo`` on CPU for tests). The gather
-buffers are kept across calls.
+(an all-gather only when every rank asks for the results), after a two-element
+all_reduce that agrees on the width and on the first failure (RCCL over xGMI with
+the ``nccl`` backend, ``gloo`` on CPU for tests). The gather buffers are kept
+across calls.
 
-On the GPU path every rank runs its block on its own device (LOCAL_RANK, see
-``_native.default_device``) through ``Deconvoluter._run_device``; the tables
-stay in HBM from the batch call through the RCCL gather, and come to the host
-once, after it.
+``par_deconvolute_spectra`` runs every rank's block through the same host-buffer
+path as the single-process ``Deconvoluter.par_deconvolute_spectra`` on the rank's
+own GPU (LOCAL_RANK, see ``_native.default_device``): the compact Bruker rows are
+read from page-locked host memory by the smoother's own launch and the results are
+written by the kernels into page-locked memory, so a rank's block costs what the
+same block costs in one process. The block's results are then packed on the host
+and exchanged by ``gather_host``: one H2D copy of the packed rows, the two
+collectives, one D2H copy on the collecting rank (round 5; round 4 staged every
+block on the device through torch first, which doubled the per-call cost).
+``gather_packed`` / ``gather_tables`` remain for results that are already in HBM
+(bench.py's device-resident configurations).
 
 The fail-fast Result collect of the reference (deconvoluter.rs:704-707) is
 reproduced on every rank from the all_reduce: each raises the error of the FIRST
-failing spectrum in global order.
+failing spectrum in global order. An engine failure on one rank is carried the same
+way, so no rank is left waiting in a collective.
 """
 from __future__ import annotations
 
+import threading
 from typing import Callable, Sequence
 
 import numpy as np
@@ -38,32 +47,50 @@ def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
 _BUFS: dict = {}
 
 
-def _buf(key, shape, dtype, dev):
+def _key(key, dtype, dev, group):
+    # one set of buffers per process group and thread: two groups, or two threads
+    # collecting on the same device, never share them
+    return (key, dtype, str(dev), id(group), threading.get_ident())
+
+
+def _buf(key, shape, dtype, dev, group=None):
     """A grow-only tensor kept across calls (no per-call allocation of the gather
     buffers); the returned view is valid until the next call with the same key."""
     import torch
     n = 1
     for d in shape:
         n *= int(d)
-    t = _BUFS.get((key, dtype, str(dev)))
+    k = _key(key, dtype, dev, group)
+    t = _BUFS.get(k)
     if t is None or t.numel() < n:
-        t = torch.empty(max(n, 1), dtype=dtype, device=dev)
-        _BUFS[(key, dtype, str(dev))] = t
+        pin = str(dev) == "pinned"
+        t = torch.empty(max(n, 1), dtype=dtype, device="cpu" if pin else dev, pin_memory=pin)
+        _BUFS[k] = t
     return t[:n].view(*shape)
+
+
+def _global_dst(group, dst):
+    """dist.gather's dst is a global rank; the callers give a rank of ``group``."""
+    import torch.distributed as dist
+    if group is None or dst is None:
+        return dst
+    return dist.get_global_rank(group, dst)
 
 
 def _collect(out, inp, dst, group):
     """all_gather_into_tensor (dst None), or a gather of every rank's tensor to rank
-    ``dst`` only: one transfer per peer over its own link instead of a ring through
-    every rank. Returns the gathered tensor on the receiving ranks, else None."""
+    ``dst`` of ``group`` only: one transfer per peer over its own link instead of a
+    ring through every rank. Returns the gathered tensor on the receiving ranks,
+    else None."""
     import torch.distributed as dist
     if dst is None:
         dist.all_gather_into_tensor(out, inp, group=group)
         return out
+    gdst = _global_dst(group, dst)
     if dist.get_rank(group) == dst:
-        dist.gather(inp, list(out.chunk(dist.get_world_size(group))), dst=dst, group=group)
+        dist.gather(inp, list(out.chunk(dist.get_world_size(group))), dst=gdst, group=group)
         return out
-    dist.gather(inp, None, dst=dst, group=group)
+    dist.gather(inp, None, dst=gdst, group=group)
     return None
 
 
@@ -92,7 +119,7 @@ def gather_packed(status, counts, mse, tables, n_total: int, group=None, dst=0):
     max_items = max(hi - lo for lo, hi in per_rank)
     b = int(status.shape[0])
     lo = per_rank[rank][0]
-    hdr = _buf("hdr", (2,), torch.int64, dev)
+    hdr = _buf("hdr", (2,), torch.int64, dev, group)
     if b:
         width = counts.max().clamp(min=1, max=max(1, int(tables.shape[1]))).to(torch.int64)
         code = torch.arange(lo, lo + b, device=dev, dtype=torch.int64) * 1024 + status.to(torch.int64)
@@ -106,14 +133,14 @@ def gather_packed(status, counts, mse, tables, n_total: int, group=None, dst=0):
     w_all, f_all = (int(v) for v in hdr.tolist())
     first = None if f_all == _FAIL_NONE else ((-f_all) // 1024, (-f_all) % 1024)
     cols = 3 + 3 * w_all
-    pack = _buf("pack", (max_items, cols), torch.float64, dev)
+    pack = _buf("pack", (max_items, cols), torch.float64, dev, group)
     if b:
         pack[:b, 0] = status
         pack[:b, 1] = counts
         pack[:b, 2] = mse
         wt = min(w_all, int(tables.shape[1]))
         pack[:b, 3:3 + 3 * wt] = tables[:, :wt].reshape(b, 3 * wt)
-    recv = _buf("recv", (world * max_items, cols), torch.float64, dev)
+    recv = _buf("recv", (world * max_items, cols), torch.float64, dev, group)
     got = _collect(recv, pack, dst, group)
     if got is None:
         return first, None
@@ -132,29 +159,88 @@ def gather_tables(status, counts, mse, tables, n_total: int, group=None, dst=0):
     None. status/counts int32[b], mse f64[b], tables f64[b, w, 3] (rows past a
     spectrum's count are ignored). Returns (status, counts, mse, tables) of all
     ``n_total`` spectra, tables padded to the largest count over all ranks
-    (gather_packed: one width/failure all_reduce and one gather)."""
-    return gather_packed(status, counts, mse, tables, n_total, group, dst)[1]
+    (gather_packed: one width/failure all_reduce and one gather). The tensors are
+    the caller's own (copies out of the reused exchange buffers)."""
+    got = gather_packed(status, counts, mse, tables, n_total, group, dst)[1]
+    return None if got is None else tuple(t.clone() for t in got)
 
 
-def _to_results(status, counts, mse, tables) -> list[Result]:
-    st, cnt, m, tab = (t.cpu().numpy() for t in (status, counts, mse, tables))
-    return [(int(st[k]), tab[k, : int(cnt[k])].copy(), float(m[k])) for k in range(st.shape[0])]
+def gather_host(local: Sequence[Result], n_total: int, group=None, dst=0, error: str | None = None):
+    """The exchange of one multi-GPU call whose block results are on the host
+    (``Deconvoluter._run``: the kernels write them into page-locked memory).
+    Returns (first_error, results): first_error is (global index, status) of the
+    first failing spectrum in global order, or (global index, None) when a rank's
+    engine call raised (``error`` set on that rank), or None -- the same on every
+    rank; results is the list of all ``n_total`` (status, params, mse) in global
+    order on rank ``dst`` (every rank when dst is None), else None.
+
+    Two collectives, as ``gather_packed``: a two-element all_reduce(MAX) agreeing on
+    the table width and the first failure, then ONE gather of the packed
+    [status, count, mse, table rows] records. With nccl the records are packed into
+    a page-locked buffer and sent by one H2D copy (RCCL gathers device memory); the
+    collecting rank copies the gathered rows back once. Buffers are kept across
+    calls."""
+    import torch
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    nccl = dist.get_backend(group) == "nccl"
+    dev = torch.device("cuda", torch.cuda.current_device()) if nccl else torch.device("cpu")
+    host = "pinned" if nccl else "cpu"
+    per_rank = [shard_range(n_total, r, world) for r in range(world)]
+    max_items = max(hi - lo for lo, hi in per_rank)
+    lo = per_rank[rank][0]
+    b = len(local)
+    width = max([int(p.shape[0]) for _, p, _ in local] + [1])
+    fail = _FAIL_NONE
+    if error is not None:
+        fail = -(lo * 1024 + 1023)  # 1023: an engine failure on this rank
+    else:
+        for k, (st, _, _) in enumerate(local):
+            if st:
+                fail = -((lo + k) * 1024 + int(st))
+                break
+    hdr_h = _buf("hdr_h", (2,), torch.int64, host, group)
+    hdr_h[0], hdr_h[1] = width, fail
+    hdr = _buf("hdr_d", (2,), torch.int64, dev, group).copy_(hdr_h, non_blocking=True) if nccl else hdr_h
+    dist.all_reduce(hdr, op=dist.ReduceOp.MAX, group=group)
+    w_all, f_all = (int(v) for v in hdr.tolist())
+    if f_all != _FAIL_NONE:
+        idx, st = (-f_all) // 1024, (-f_all) % 1024
+        first = (idx, None if st == 1023 else st)
+        if st == 1023:  # no results to gather: every rank raises
+            return first, None
+    else:
+        first = None
+    cols = 3 + 3 * w_all
+    pk_h = _buf("pack_h", (max_items, cols), torch.float64, host, group)
+    a = pk_h.numpy()
+    for k, (st, p, m) in enumerate(local):
+        c = int(p.shape[0])
+        a[k, 0], a[k, 1], a[k, 2] = st, c, m
+        if c:
+            a[k, 3:3 + 3 * c] = np.asarray(p, dtype=np.float64).reshape(-1)
+    pk = _buf("pack_d", (max_items, cols), torch.float64, dev, group).copy_(pk_h, non_blocking=True) \
+        if nccl else pk_h
+    recv = _buf("recv", (world * max_items, cols), torch.float64, dev, group)
+    got = _collect(recv, pk, dst, group)
+    if got is None:
+        return first, None
+    if nccl:
+        got = _buf("recv_h", (world * max_items, cols), torch.float64, host, group).copy_(got)
+    g = got.numpy()
+    results = []
+    for r, (l, h) in enumerate(per_rank):
+        for k in range(h - l):
+            row = g[r * max_items + k]
+            c = int(row[1])
+            results.append((int(row[0]), row[3:3 + 3 * c].reshape(c, 3).copy(), float(row[2])))
+    return first, results
 
 
 def gather_results(local: Sequence[Result], n_total: int, group=None) -> list[Result]:
     """All-gather per-spectrum host results of every rank's shard, in global order
-    (host-compute variant of ``gather_tables``; CPU tensors, gloo)."""
-    import torch
-    b = len(local)
-    w = max([p.shape[0] for _, p, _ in local] + [1])
-    status = torch.tensor([s for s, _, _ in local], dtype=torch.int32)
-    counts = torch.tensor([p.shape[0] for _, p, _ in local], dtype=torch.int32)
-    mse = torch.tensor([m for _, _, m in local], dtype=torch.float64)
-    tables = torch.zeros((b, w, 3), dtype=torch.float64)
-    for i, (_, p, _) in enumerate(local):
-        if p.shape[0]:
-            tables[i, : p.shape[0]] = torch.from_numpy(np.ascontiguousarray(p))
-    return _to_results(*gather_tables(status, counts, mse, tables, n_total, group, dst=None))
+    (``gather_host`` with every rank collecting)."""
+    return gather_host(local, n_total, group, dst=None)[1]
 
 
 def deconvolute_distributed(spectra: Sequence, compute: Callable[[Sequence], list[Result]],
@@ -169,36 +255,41 @@ def deconvolute_distributed(spectra: Sequence, compute: Callable[[Sequence], lis
 
 
 def par_deconvolute_spectra(deconvoluter, spectra: Sequence, group=None, dst=0):
-    """Deconvoluter.par_deconvolute_spectra across all ranks of ``group`` (nccl):
-    each rank runs its shard on its own GPU, and the results stay in HBM through the
-    RCCL exchange (gather_packed: one width/failure all_reduce, one gather). Rank
-    ``dst`` (every rank when dst is None) returns the full list of
-    ``Deconvolution`` objects in input order, the other ranks None; every rank
-    raises the error of the first failing spectrum in global order, like the
-    reference's fail-fast Result collect (deconvoluter.rs:704-707)."""
-    import torch
-    from . import _native as nat
-    from ._deconvolution import Deconvolution
-    from .exceptions import from_status
+    """Deconvoluter.par_deconvolute_spectra across all ranks of ``group``: each rank
+    runs its contiguous block on its own GPU through the single-process host path
+    (``Deconvoluter._run``: in-launch decode of page-locked compact rows, results
+    written by the kernels into page-locked memory), then the block's results are
+    exchanged once (``gather_host``: one width/failure all_reduce, one gather; RCCL
+    over xGMI with nccl). Rank ``dst`` of the group (every rank when dst is None)
+    returns the full list of ``Deconvolution`` objects in input order, the other
+    ranks None; every rank raises the error of the first failing spectrum in global
+    order, like the reference's fail-fast Result collect (deconvoluter.rs:704-707),
+    and an engine failure on any rank raises on every rank."""
     import torch.distributed as dist
+    from ._deconvolution import Deconvolution
+    from .exceptions import UnexpectedError, from_status
 
     spectra = list(spectra)
     world, rank = dist.get_world_size(group), dist.get_rank(group)
-    dev_index = nat.default_device() if deconvoluter.device is None else deconvoluter.device
-    dev = torch.device("cuda", dev_index)
-    torch.cuda.set_device(dev)
+    if dist.get_backend(group) == "nccl":
+        import torch
+        from . import _native as nat
+        torch.cuda.set_device(nat.default_device() if deconvoluter.device is None else deconvoluter.device)
     lo, hi = shard_range(len(spectra), rank, world)
+    local, err = [], None
     if hi > lo:
-        status, counts, mse, tables = deconvoluter._run_device(spectra[lo:hi])
-    else:
-        status = torch.zeros(0, dtype=torch.int32, device=dev)
-        counts = torch.zeros(0, dtype=torch.int32, device=dev)
-        mse = torch.zeros(0, dtype=torch.float64, device=dev)
-        tables = torch.zeros((0, 1, 3), dtype=torch.float64, device=dev)
-    first, got = gather_packed(status, counts, mse, tables, len(spectra), group, dst)
+        try:
+            local = deconvoluter._run(spectra[lo:hi])
+        except Exception as e:  # carried through the all_reduce: no rank waits forever
+            err = e
+    first, got = gather_host(local, len(spectra), group, dst, error=None if err is None else repr(err))
+    if err is not None:
+        raise err
     if first is not None:
+        if first[1] is None:
+            raise UnexpectedError(f"GPU engine failure on the rank owning spectrum {first[0]}")
         raise from_status(first[1])
     if got is None:
         return None
-    settings = deconvoluter.settings
-    return [Deconvolution(params, m, settings) for _, params, m in _to_results(*got)]
+    snap = deconvoluter.settings
+    return [Deconvolution._of(params, m, snap) for _, params, m in got]

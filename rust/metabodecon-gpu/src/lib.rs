@@ -119,6 +119,8 @@ pub mod ffi {
         pub fn mdg_ctx_destroy(ctx: *mut MdgCtx) -> c_int;
         pub fn mdg_ctx_set_stream(ctx: *mut MdgCtx, hip_stream: *mut c_void) -> c_int;
         pub fn mdg_ctx_synchronize(ctx: *mut MdgCtx) -> c_int;
+        pub fn mdg_ctx_set_latency_mode(ctx: *mut MdgCtx, on: c_int) -> c_int;
+        pub fn mdg_ctx_reload_switches(ctx: *mut MdgCtx) -> c_int;
         pub fn mdg_deconvolute(
             ctx: *mut MdgCtx,
             x: *const f64,
@@ -321,6 +323,13 @@ impl GpuContext {
 
     pub fn exact_mse(&self) -> bool {
         self.options.load(Ordering::Relaxed) & ffi::MDG_OPTION_EXACT_MSE != 0
+    }
+
+    /// Latency mode (on by default): a one-spectrum call expects the GPU to itself and
+    /// takes the fit tiling fastest alone; turn it off on contexts that run
+    /// `par_deconvolute_spectrum` callers concurrently. Results are bit-identical.
+    pub fn set_latency_mode(&self, on: bool) -> Result<()> {
+        check(unsafe { ffi::mdg_ctx_set_latency_mode(self.raw(), on as c_int) })
     }
 
     fn options(&self) -> i32 {

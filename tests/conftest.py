@@ -25,3 +25,34 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def golden_dir():
     return GOLDEN
+
+
+class EngineEnv:
+    """MDG_* engine switches for a test: set in the environment and re-read by every
+    live engine context (the engine reads the environment only when a context is
+    created or on mdg_ctx_reload_switches, never on a call's path)."""
+
+    def __init__(self, mp):
+        self.mp = mp
+
+    def setenv(self, name, value):
+        self.mp.setenv(name, value)
+        self.reload()
+
+    def delenv(self, name, raising=True):
+        self.mp.delenv(name, raising=raising)
+        self.reload()
+
+    @staticmethod
+    def reload():
+        nat = sys.modules.get("metabodecon._native")
+        if nat is not None:
+            nat.reload_switches()
+
+
+@pytest.fixture
+def engine_env(monkeypatch):
+    e = EngineEnv(monkeypatch)
+    yield e
+    monkeypatch.undo()  # the switches the other tests expect, then re-read them
+    e.reload()

@@ -202,3 +202,128 @@ def test_gather_tables_worlds_uneven_and_empty_ranks(world, n):
         want = [[float(k * w * 3 + j * 3 + c + 100 * r) for c in range(3)] for j in range(counts[i])]
         assert tables[i][: counts[i]] == want, (i, r)
     assert all(got[r][2] == got[0][2] for r in range(world))  # the all-gather, everywhere
+
+
+class _OracleDeconvoluter:
+    """Stands in for Deconvoluter on CPU: ``_run`` is the oracle (test
+    infrastructure), the rest is what distributed.par_deconvolute_spectra reads."""
+
+    device = None
+
+    def __init__(self, fail_rank=None):
+        import metabodecon._native as nat
+        self.settings = nat.Settings()
+        self.fail_rank = fail_rank
+
+    def _run(self, block):
+        import torch.distributed as dist
+        import oracle
+        if self.fail_rank is not None and dist.get_rank() == self.fail_rank:
+            raise RuntimeError("injected engine failure")
+        out = []
+        for (x, y, sb, st, ign) in block:
+            r = oracle.deconvolute(x, y, sb, st, ignore=ign)
+            out.append((r.status, r.params, r.mse))
+        return out
+
+
+def _par_worker(rank, world, port, q, mode):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "metabodecon-rust_amd")]
+    import torch.distributed as dist
+    from metabodecon import exceptions as mexc
+    from metabodecon.distributed import par_deconvolute_spectra
+    from tests.golden.cases import load_case
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        spectra = [load_case(f"sim_{i:02d}") for i in range(1, 8)]
+        if mode == "results":
+            res = par_deconvolute_spectra(_OracleDeconvoluter(), spectra)
+            q.put((rank, None if res is None else [(d.params.tolist(), d.mse) for d in res]))
+        elif mode == "fail":
+            x, y, sb, st, ign = spectra[4]
+            spectra[4] = (x, np.full_like(y, 3.0), sb, st, ign)  # NoPeaksDetected
+            try:
+                par_deconvolute_spectra(_OracleDeconvoluter(), spectra, dst=None)
+                q.put((rank, "no error"))
+            except mexc.NoPeaksDetected:
+                q.put((rank, "NoPeaksDetected"))
+        elif mode == "engine":
+            try:
+                par_deconvolute_spectra(_OracleDeconvoluter(fail_rank=1), spectra)
+                q.put((rank, "no error"))
+            except Exception as e:  # every rank raises; none waits in a collective
+                q.put((rank, type(e).__name__))
+        elif mode == "subgroup":
+            # ADVICE r4: dst is a rank of the group; the group excludes global rank 0
+            sub = dist.new_group(ranks=list(range(1, world)))
+            if rank >= 1:
+                res = par_deconvolute_spectra(_OracleDeconvoluter(), spectra, group=sub)
+                q.put((rank, None if res is None else [(d.params.tolist(), d.mse) for d in res]))
+            else:
+                q.put((rank, "outside"))
+    finally:
+        dist.destroy_process_group()
+
+
+def _spawn(world, mode):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_par_worker, args=(r, world, port, q, mode)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return got
+
+
+def _oracle_sim():
+    import oracle
+    from tests.golden.cases import load_case
+    out = []
+    for i in range(1, 8):
+        x, y, sb, st, ign = load_case(f"sim_{i:02d}")
+        r = oracle.deconvolute(x, y, sb, st, ignore=ign)
+        out.append((r.params, r.mse))
+    return out
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_par_deconvolute_spectra_host_exchange(world):
+    """distributed.par_deconvolute_spectra (round 5: every rank's block through the
+    host path, the packed results exchanged by gather_host) with an oracle engine:
+    rank 0 gets the 7 sim results in input order, bit for bit, the others None."""
+    got = _spawn(world, "results")
+    want = _oracle_sim()
+    assert all(got[r] is None for r in range(1, world))
+    assert len(got[0]) == 7
+    for (p, m), (wp, wm) in zip(got[0], want):
+        assert np.array_equal(np.array(p).reshape(-1, 3), wp) and m == wm
+
+
+@pytest.mark.timeout(300)
+def test_par_deconvolute_spectra_failures_on_every_rank():
+    """The first failing spectrum raises its error on every rank (fail-fast collect,
+    deconvoluter.rs:704-707); an engine failure on one rank raises on every rank
+    instead of leaving the others in a collective."""
+    assert set(_spawn(3, "fail").values()) == {"NoPeaksDetected"}
+    got = _spawn(3, "engine")
+    assert got[1] == "RuntimeError" and got[0] == got[2] == "UnexpectedError", got
+
+
+@pytest.mark.timeout(300)
+def test_par_deconvolute_spectra_subgroup_without_global_rank_0():
+    """dst is a rank of the group: a group of global ranks 1..3 collects
+    on its rank 0 (global rank 1)."""
+    got = _spawn(4, "subgroup")
+    assert got[0] == "outside" and got[2] is None and got[3] is None
+    want = _oracle_sim()
+    for (p, m), (wp, wm) in zip(got[1], want):
+        assert np.array_equal(np.array(p).reshape(-1, 3), wp) and m == wm

@@ -133,12 +133,12 @@ def test_python_surface_accepts_many_regions():
 
 
 @pytest.mark.parametrize("graphs", ["0", "1"])
-def test_device_path_alternating_ignore_sets(graphs, monkeypatch):
+def test_device_path_alternating_ignore_sets(graphs, monkeypatch, engine_env):
     """the same device buffers, calls alternating between ignore-region
     sets (none, two, 70, two again, a different two), direct launches and cached
     graph replays: every call equals the oracle with that call's regions."""
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("MDG_GRAPHS", graphs)
+    engine_env.setenv("MDG_GRAPHS", graphs)
     ctx = nat.Context(0)
     try:
         cx, cy, csb, cst = increasing("blood_05")

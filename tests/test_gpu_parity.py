@@ -159,12 +159,12 @@ def test_single_spectrum_entry(ctx):
 
 
 @pytest.mark.parametrize("path", ["chain", "pipe", "generic"])
-def test_detected_peaks_match_oracle(ctx, path, monkeypatch):
+def test_detected_peaks_match_oracle(ctx, path, monkeypatch, engine_env):
     """Detected triples equal the oracle's; the selection (which reads the noise
     scores k_peaks computes for the peaks it writes) equals the golden, behind every
     smoother kernel (the chain smoother runs the set-up itself, the others after
     k_prep)."""
-    monkeypatch.setenv("MDG_SMOOTH", path)
+    engine_env.setenv("MDG_SMOOTH", path)
     x, y, sb, st, ign = load_case("blood_01")
     gpu_batch(ctx, x, y[None, :], [sb], st)
     det = ctx.last_peaks(0, "detected").astype(np.int64)
@@ -259,7 +259,7 @@ def test_reference_unit_superposition(ctx):
     assert abs(md.Lorentzian.superposition_vec(np.array([5.0]), trip)[0] - 51.466992) <= 1e-6
 
 
-def test_fused_prep_after_failures_and_other_smoothers(monkeypatch):
+def test_fused_prep_after_failures_and_other_smoothers(monkeypatch, engine_env):
     """The chain smoother runs k_prep's work itself and never reads the status the
     previous run left; k_flags returns its progress counters to zero. On one
     context: a failing spectrum (NoPeaksDetected), then a good one, the same on
@@ -273,11 +273,11 @@ def test_fused_prep_after_failures_and_other_smoothers(monkeypatch):
     x, y, sb, cst, _ = load_case("blood_07")
     o = oracle.deconvolute(x, y, sb, cst)
     for smooth, prep in [("chain", None), ("pipe", None), ("chain", "separate"), ("chain", None)]:
-        monkeypatch.setenv("MDG_SMOOTH", smooth)
+        engine_env.setenv("MDG_SMOOTH", smooth)
         if prep:
-            monkeypatch.setenv("MDG_PREP", prep)
+            engine_env.setenv("MDG_PREP", prep)
         else:
-            monkeypatch.delenv("MDG_PREP", raising=False)
+            engine_env.delenv("MDG_PREP", raising=False)
         status, *_ = gpu_batch(c, xf, flat[None, :], [(11.8, -2.2)], st)
         assert status[0] == 1, (smooth, prep)
         status, counts, out, mse = gpu_batch(c, x, y[None, :], [sb], cst)
@@ -353,10 +353,10 @@ def test_small_and_odd_shapes(ctx):
 @pytest.mark.parametrize("path", ["chain", "pipe", "generic"])
 @pytest.mark.parametrize("it,ws", [(1, 2), (2, 4), (3, 3), (5, 7), (8, 5), (10, 3), (3, 31),
                                    (4, 9), (2, 11)])
-def test_smoother_settings_sweep(ctx, it, ws, path, monkeypatch):
+def test_smoother_settings_sweep(ctx, it, ws, path, monkeypatch, engine_env):
     """Every smoother kernel (chain, lane-pipelined, one lane per spectrum, forced by
     MDG_SMOOTH) against the oracle; (3, 31) and iterations > 8 exercise fallbacks."""
-    monkeypatch.setenv("MDG_SMOOTH", path)
+    engine_env.setenv("MDG_SMOOTH", path)
     x, y, sb, _, _ = load_case("blood_05")
     st = oracle.make_settings(smooth_iterations=it, smooth_window=ws)
     o = oracle.deconvolute(x, y, sb, st)
@@ -463,21 +463,21 @@ def _smooth_rows(ctx, ys, it, ws):
 
 
 @pytest.mark.parametrize("path", ["chain", "pipe", "generic"])
-def test_smoothed_rows_bit_exact(ctx, path, monkeypatch):
+def test_smoothed_rows_bit_exact(ctx, path, monkeypatch, engine_env):
     """Smoothed intensities of every kernel equal the oracle's moving average bit for
     bit (moving_average.rs:53-83), on real spectra and a synthetic 128k one."""
-    monkeypatch.setenv("MDG_SMOOTH", path)
+    engine_env.setenv("MDG_SMOOTH", path)
     ys = np.stack([load_case(f"blood_{i:02d}")[1] for i in (1, 7, 16)] + [synth_spectrum(0)[1]])
     for s, row in enumerate(_smooth_rows(ctx, ys, 3, 3)):
         assert np.array_equal(row, oracle.moving_average(ys[s], 3, 3)), s
 
 
 @pytest.mark.parametrize("ws", [2, 3, 4, 5, 6, 7, 8])
-def test_chain_smoother_shapes(ctx, ws, monkeypatch):
+def test_chain_smoother_shapes(ctx, ws, monkeypatch, engine_env):
     """k_smooth_chain at the edges of its range: short spectra (generic head/tail
     blocks only), lengths off the block and group grids, up to 16 passes, batches
     that do not fill the 8-spectrum placement groups."""
-    monkeypatch.setenv("MDG_SMOOTH", "chain")
+    engine_env.setenv("MDG_SMOOTH", "chain")
     rng = np.random.default_rng(ws)
     for n, b, it in [(400, 1, 1), (401, 3, 2), (487, 2, 3), (577, 9, 5), (1000, 1, 16),
                      (4101, 13, 3), (20000, 2, 4)]:
@@ -488,10 +488,10 @@ def test_chain_smoother_shapes(ctx, ws, monkeypatch):
             assert np.array_equal(row, oracle.moving_average(ys[s], it, ws)), (n, b, it, s)
 
 
-def test_chain_smoother_repeated_launches(ctx, monkeypatch):
+def test_chain_smoother_repeated_launches(ctx, monkeypatch, engine_env):
     """Back-to-back launches rewrite the chain's hand-off buffers: a stale line in
     any cache would show as a mismatch in the second and third runs."""
-    monkeypatch.setenv("MDG_SMOOTH", "chain")
+    engine_env.setenv("MDG_SMOOTH", "chain")
     rng = np.random.default_rng(7)
     for rep in range(3):
         ys = rng.normal(0, 1, (5, 131072)) * 1e3 + rep
@@ -505,11 +505,11 @@ FIT_KERNELS = ["tf", "tf12", "tw7", "tw3s", "twf", "twf1", "twf3s", "twf:5", "tw
 
 
 @pytest.mark.parametrize("mode", ["fine", "coarse"])
-def test_peak_chunkings(ctx, mode, monkeypatch):
+def test_peak_chunkings(ctx, mode, monkeypatch, engine_env):
     """k_peaks over 64-word chunks (small batches) and 256-word chunks (large ones),
     forced by MDG_PEAKS, on a single spectrum and a batch of three: the oracle's
     results either way (peak lists, scores and the selection behind them)."""
-    monkeypatch.setenv("MDG_PEAKS", mode)
+    engine_env.setenv("MDG_PEAKS", mode)
     for name in ("blood_03", "sim_03"):
         x, y, sb, st, ign = load_case(name)
         o = oracle.deconvolute(x, y, sb, st, ignore=ign)
@@ -550,19 +550,19 @@ def test_selection_many_signal_peaks(ctx):
             assert abs(mse[k] - o.mse) <= MSE_RTOL * abs(o.mse), k
 
 
-def _force_fit(monkeypatch, path):
+def _force_fit(engine_env, path):
     kernel, _, g = path.partition(":")
-    monkeypatch.setenv("MDG_FITSUP", kernel)
+    engine_env.setenv("MDG_FITSUP", kernel)
     if g:
-        monkeypatch.setenv("MDG_TW_G", g)
+        engine_env.setenv("MDG_TW_G", g)
 
 
 @pytest.mark.parametrize("path", FIT_KERNELS)
-def test_fit_superposition_kernels(ctx, path, monkeypatch):
+def test_fit_superposition_kernels(ctx, path, monkeypatch, engine_env):
     """Every fit-superposition kernel the library ships (24- and 63-point term folds,
     one thread per point; forced by MDG_FITSUP) gives the oracle's Lorentzians bit for
     bit, including peak counts that are not multiples of the tiles and chunks."""
-    _force_fit(monkeypatch, path)
+    _force_fit(engine_env, path)
     names = ["sim_03", "blood_03", "synth_128k_2k_s1"]
     for name in names:
         x, y, sb, st, ign = load_case(name)
@@ -574,10 +574,10 @@ def test_fit_superposition_kernels(ctx, path, monkeypatch):
 
 
 @pytest.mark.parametrize("path", FIT_KERNELS)
-def test_fit_superposition_kernels_batch(ctx, path, monkeypatch):
+def test_fit_superposition_kernels_batch(ctx, path, monkeypatch, engine_env):
     """The fit kernels on a batch whose spectra have different peak counts (tail
     tiles, grid-stride loops, per-spectrum range flags) against the oracle."""
-    _force_fit(monkeypatch, path)
+    _force_fit(engine_env, path)
     rows, ref = [], []
     for seed in (3, 4, 5):
         x, y = synth_spectrum(seed, n=65536, n_peaks=700 + 300 * seed)[:2]
@@ -593,14 +593,14 @@ def test_fit_superposition_kernels_batch(ctx, path, monkeypatch):
 
 @pytest.mark.parametrize("npt", ["2", "4"])
 @pytest.mark.parametrize("near_cap", [None, "8", "0"])
-def test_mse_cases(ctx, near_cap, npt, monkeypatch):
+def test_mse_cases(ctx, near_cap, npt, monkeypatch, engine_env):
     """The MSE (k_mse_local, 2 and 4 points per thread) against the oracle: ignore
     regions (two in one spectrum), a short signal region (sim) and a batch whose
     spectra differ in peak count; also with a tiny near-list capacity (crowded tiles
     take the kernel's direct sum) and none at all (every tile direct)."""
-    monkeypatch.setenv("MDG_MSE_NPT", npt)
+    engine_env.setenv("MDG_MSE_NPT", npt)
     if near_cap is not None:
-        monkeypatch.setenv("MDG_MSE_NEARCAP", near_cap)
+        engine_env.setenv("MDG_MSE_NEARCAP", near_cap)
     for name in ["blood_01_water", "blood_02_two_regions_increasing", "sim_05", "synth_128k_2k_s0"]:
         x, y, sb, st, ign = load_case(name)
         o = oracle.deconvolute(x, y, sb, st, ignore=ign)
@@ -688,13 +688,13 @@ def test_one_newton_division_is_not_exact_on_hard_cases(ctx):
     assert tested > 0 and bad_hard > 0, (bad_hard, tested)
 
 
-def test_device_graph_replay(ctx, monkeypatch):
+def test_device_graph_replay(ctx, monkeypatch, engine_env):
     """With MDG_GRAPHS=1 mdg_deconvolute_batch_device replays a cached hipGraph for
     repeated argument sets: refilling the same device buffers with other spectra
     must still give the oracle's results on the replayed launch, and the same bits
     as the uncaptured pipeline (MDG_GRAPHS=0, the default)."""
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("MDG_GRAPHS", "1")
+    engine_env.setenv("MDG_GRAPHS", "1")
     names = [["blood_02", "blood_04"], ["blood_09", "blood_11"], ["blood_02", "blood_04"]]
     n = load_case("blood_02")[1].size
     b = 2
@@ -732,19 +732,19 @@ def test_device_graph_replay(ctx, monkeypatch):
             assert st_ == o.status and np.array_equal(p, o.params)
             assert abs(m - o.mse) <= MSE_RTOL * abs(o.mse)
         results.append(got)
-    monkeypatch.setenv("MDG_GRAPHS", "0")
+    engine_env.setenv("MDG_GRAPHS", "0")
     plain = run()  # last batch again, uncaptured
     for (s1, p1, m1), (s2, p2, m2) in zip(results[-1], plain):
         assert s1 == s2 and np.array_equal(p1, p2) and m1 == m2
 
 
-def test_graph_key_follows_kernel_overrides(monkeypatch):
+def test_graph_key_follows_kernel_overrides(monkeypatch, engine_env):
     """A cached pipeline graph is keyed by the kernel-choice overrides too: the
     same device buffers with MDG_SMOOTH / MDG_FITSUP switched between calls launch
     the newly chosen kernels (reported by the engine), each call equal to the
     oracle."""
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("MDG_GRAPHS", "1")
+    engine_env.setenv("MDG_GRAPHS", "1")
     cx, cy, csb, cst, _ = load_case("blood_03")
     n = cy.size
     c = nat.Context(0)
@@ -760,8 +760,8 @@ def test_graph_key_follows_kernel_overrides(monkeypatch):
     o = oracle.deconvolute(cx, cy, csb, cst)
     seen = []
     for sm_k, fit_k in [("chain", "tw7"), ("pipe", "tw7"), ("chain", "plain"), ("chain", "tw7")]:
-        monkeypatch.setenv("MDG_SMOOTH", sm_k)
-        monkeypatch.setenv("MDG_FITSUP", fit_k)
+        engine_env.setenv("MDG_SMOOTH", sm_k)
+        engine_env.setenv("MDG_FITSUP", fit_k)
         rc = nat.lib().mdg_deconvolute_batch_device(
             c.handle, 1, n, x.data_ptr(), 0, y.data_ptr(), n, sb.data_ptr(), ctypes.byref(s), None,
             0, out.data_ptr(), cap, cnt.data_ptr(), mse.data_ptr(), status.data_ptr())
@@ -846,13 +846,13 @@ def test_jcampdx_and_serde_inputs_through_the_device(tmp_path):
     assert r.mse == d.mse
 
 
-def test_graph_cache_survives_workspace_growth(ctx, monkeypatch):
+def test_graph_cache_survives_workspace_growth(ctx, monkeypatch, engine_env):
     """A cached pipeline graph bakes the workspace layout. Growing the workspace
     (a larger batch, then a longer spectrum on a fresh context) must drop the cached
     graphs, so B=1 -> B=2 -> B=1 -> longer N -> B=1 on the same tensors keeps
     giving the oracle's results (stale graph after reallocation)."""
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("MDG_GRAPHS", "1")
+    engine_env.setenv("MDG_GRAPHS", "1")
     c = nat.Context(0)
     try:
         names = ["sim_04", "sim_09"]
@@ -897,9 +897,10 @@ def test_graph_cache_survives_workspace_growth(ctx, monkeypatch):
 
 def test_par_deconvolute_spectra_rccl_world1():
     """The multi-GPU product path itself (metabodecon.distributed) on the box's GPU:
-    nccl (RCCL) process group of world size 1, the shard run device-resident by
-    Deconvoluter._run_device, tables gathered in HBM; results equal the goldens,
-    and an injected failure raises the first error in order."""
+    nccl (RCCL) process group of world size 1, the shard run through the
+    single-process host path (Deconvoluter._run), the packed results gathered over
+    RCCL (distributed.gather_host); results equal the goldens, and an injected
+    failure raises the first error in order."""
     import socket
     import torch
     import torch.distributed as dist
@@ -970,7 +971,7 @@ def test_ragged_lengths_through_the_python_surface():
         assert abs(d.mse - mse) <= MSE_RTOL * abs(mse)
 
 
-def test_graph_repoint_in_flight_bit_exact(monkeypatch):
+def test_graph_repoint_in_flight_bit_exact(monkeypatch, engine_env):
     """One cached pipeline graph serves calls on distinct device arrays
     (mdg_capi.hip repoint_graph): every call here passes its own x/y/sb rows and
     writes straight into its own result rows, and all calls are enqueued on two
@@ -979,7 +980,7 @@ def test_graph_repoint_in_flight_bit_exact(monkeypatch):
     CUDA/HIP contract: launches already enqueued are not affected). Every call
     must equal the oracle bit for bit, and the MSE within 1e-12."""
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("MDG_GRAPHS", "1")
+    engine_env.setenv("MDG_GRAPHS", "1")
     names = ["blood_02", "blood_05", "blood_07", "blood_11", "blood_13", "blood_16"]
     cases = [load_case(nm) for nm in names]
     refs = [oracle.deconvolute(c[0], c[1], c[2], c[3]) for c in cases]
@@ -1021,7 +1022,7 @@ def test_graph_repoint_in_flight_bit_exact(monkeypatch):
 
 
 @pytest.mark.parametrize("graphs", ["0", "1"])
-def test_concurrent_contexts_stream_bit_exact(graphs, monkeypatch):
+def test_concurrent_contexts_stream_bit_exact(graphs, monkeypatch, engine_env):
     """The bench's stream mode: 6 contexts, each on its own stream,
     run their pipelines (launched directly, or replayed as captured graphs with
     MDG_GRAPHS=1) on a stream of distinct spectra (input row
@@ -1032,7 +1033,7 @@ def test_concurrent_contexts_stream_bit_exact(graphs, monkeypatch):
     whole-CU chain smoother and the term-fold fit stay exact when other
     pipelines run beside them."""
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("MDG_GRAPHS", graphs)
+    engine_env.setenv("MDG_GRAPHS", graphs)
     names = ["blood_02", "blood_05", "blood_07", "blood_11", "blood_13", "blood_16",
              "sim_02", "sim_05", "sim_08", "sim_11", "sim_14", "sim_16"]
     cases = [load_case(nm) for nm in names]

@@ -124,7 +124,7 @@ def test_compact_rows_decode_bit_exact():
 
 @pytest.mark.parametrize("env", ["", "MDG_DEC_OVERLAP=0", "MDG_SMOOTH=pipe", "MDG_PREP=separate",
                                  "MDG_CHAIN_EXCL=0"])
-def test_compact_rows_decode_paths(env, monkeypatch):
+def test_compact_rows_decode_paths(env, monkeypatch, engine_env):
     """Page-locked compact rows are decoded from host memory by the pipeline: by the
     chain launch's decoders while pass 0 smooths the decoded chunks (default), or by
     a decode launch of their own before any other smoother / a separate prep
@@ -136,7 +136,7 @@ def test_compact_rows_decode_paths(env, monkeypatch):
     import oracle
     if env:
         k, v = env.split("=")
-        monkeypatch.setenv(k, v)
+        engine_env.setenv(k, v)
     read = _blood(md)
     ctx = nat.context()
     s = md.Deconvoluter().settings
@@ -243,6 +243,105 @@ def test_compact_rows_decode_odd_shapes(n, b, off):
     assert np.array_equal(c[4], f[4]) and np.array_equal(c[2], f[2]) and np.array_equal(c[3], f[3])
     assert np.array_equal(c[1], f[1])
     assert c[2].min() > 0  # every spectrum found its peaks
+
+
+def _compact_set(n, b, seed, blk_off=0):
+    """b synthetic compact rows of n points in one page-locked block (rows
+    adjacent, as Spectrum.read_bruker_set places them), with their axes, scales and
+    the f64 intensities the decode must produce."""
+    rng = np.random.default_rng(seed)
+    blk = nat.pinned_empty((b * n + blk_off + 4,), np.int32)
+    assert blk is not None
+    rows, axes, scales, ys = [], [], [], []
+    for i in range(b):
+        mx, wd, dv = 11.8 + 0.01 * i, 14.0, float(n - 1)
+        x = mx - (np.arange(n, dtype=np.float64) * wd) / dv
+        c = rng.uniform(1.0, 9.0, 40)
+        hw = rng.uniform(0.002, 0.01, 40) ** 2
+        a = rng.uniform(1e5, 1e7, 40) * hw
+        y = (a[:, None] / (hw[:, None] + (x[None, :] - c[:, None]) ** 2)).sum(0) + rng.normal(0, 50, n)
+        scale = 2.0 ** int(rng.integers(-2, 3))
+        raw = np.round(y / scale).astype(np.int32)
+        r = blk[blk_off + i * n: blk_off + (i + 1) * n]
+        r[:] = raw
+        rows.append(r)
+        axes.append((mx, wd, dv))
+        scales.append(scale)
+        ys.append(raw.astype(np.float64) * scale)
+    return blk, rows, np.array(axes, dtype=np.float64), np.array(scales, dtype=np.float64), ys
+
+
+def _run_compact(ctx, s, n, rows, axes, scales):
+    b = len(rows)
+    cap = n // 2 + 2
+    sb = np.array([[11.0, 0.5]] * b, dtype=np.float64)
+    out = np.zeros((b, cap, 3))
+    counts = np.zeros(b, dtype=np.uintp)
+    mse = np.zeros(b)
+    status = np.zeros(b, dtype=np.intc)
+    yr = np.array([r.ctypes.data for r in rows], dtype=np.uintp)
+    rc = nat.lib().mdg_deconvolute_rows_i32(
+        ctx.handle, b, n, nat.ptr(axes), yr.ctypes.data_as(ctypes.POINTER(nat._i32p)),
+        nat.ptr(scales), nat.ptr(sb), ctypes.byref(s), None, 0, nat.ptr(out), cap,
+        nat.ptr(counts, nat._szp), nat.ptr(mse), status.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+    return rc, out, counts, mse, status
+
+
+@pytest.mark.parametrize("n", [20001, 131071])
+@pytest.mark.parametrize("b", [2, 5, 16])
+def test_compact_rows_decode_poisoned_staging_under_load(n, b):
+    """the in-launch decode's cross-XCD hand-off (chain_decode ->
+    pass 0's feeder) under the conditions the microarchitecture guide says expose a
+    stale read: the staging rows are poisoned by a call on the same context
+    immediately before (other spectra of the same shape, so every staging line holds
+    other values and was just read, warm, by that call's chains), the rows are an odd
+    length (n % 16 != 0: before round 5 a 128-byte line straddled two chunks of two
+    decoders; now the rows are padded to whole lines), 2-16 spectra (32 or 64
+    decoders, rows on every XCD), and a second engine context runs batches on the
+    same GPU the whole time (uneven load). Every smoothed word of every spectrum is
+    checked against the oracle's moving average of the decoded intensities, three
+    poisoned rounds in a row."""
+    import threading
+
+    import metabodecon as md
+    import oracle
+    ctx = nat.context()
+    s = md.Deconvoluter().settings
+    cur = _compact_set(n, b, seed=1000 + n + b)
+    poison = _compact_set(n, b, seed=2000 + n + b, blk_off=3)
+    other = nat.Context(0)
+    busy_rows = _compact_set(65536, 8, seed=7)
+    stop = threading.Event()
+    busy_err = []
+
+    def busy():  # the second lane: compact batches on another context until stopped
+        try:
+            while not stop.is_set():
+                with other.lock:
+                    rc = _run_compact(other, s, 65536, busy_rows[1], busy_rows[2], busy_rows[3])[0]
+                if rc not in (0, 1, 2, 3):
+                    busy_err.append(rc)
+                    return
+        except Exception as e:  # pragma: no cover - reported below
+            busy_err.append(repr(e))
+    t = threading.Thread(target=busy)
+    t.start()
+    try:
+        ref = [oracle.moving_average(y, s.smooth_iterations, s.smooth_window) for y in cur[4]]
+        for rnd in range(3):
+            with ctx.lock:
+                _run_compact(ctx, s, n, poison[1], poison[2], poison[3])
+                rc, out, counts, mse, status = _run_compact(ctx, s, n, cur[1], cur[2], cur[3])
+                assert rc in (0, 1, 2, 3), rc
+                smoothed = [ctx.last_smoothed(k, n) for k in range(b)]
+            for k in range(b):
+                bad = np.flatnonzero(smoothed[k] != ref[k])
+                assert bad.size == 0, (rnd, k, bad[:8], bad.size)
+    finally:
+        stop.set()
+        t.join(timeout=120)
+    assert not busy_err, busy_err
+    other.close()
 
 
 def test_compact_rows_reject_bad_descriptors():

@@ -9,6 +9,11 @@ spin-wait protocols whose producers publish to other workgroups:
   * k_peaks: each chunk's {valid, bordered, kept} slot (decoupled look-back);
   * k_mse_local: each tile's partial (sc1 store), the arrival counter (atomic add)
     and its reset, read by the spectrum's last workgroup.
+Round 5 adds the CONSUMER side of the one cross-XCD hand-off
+that is not kept on one XCD by construction: the chain launch's decoders publish
+chunks of rows read from host memory, and pass 0's feeder must issue an agent-scope
+acquire (buffer_inv sc1) after its flag poll and before any load of the new chunks
+(test_decoded_chunks_acquired_before_loads).
 This test compiles the kernels exactly as the Makefile does and checks, for every
 publishing instruction of those kernels (global atomics and sc1 stores), that the
 lane-divergent region around it -- from the last exec-narrowing instruction before it
@@ -132,3 +137,52 @@ def test_checker_flags_a_spill_in_a_guarded_region():
     assert flagged(before) == []
     scan = guarded[:2] + ["\tv_readlane_b32 s14, v74, s11"] + guarded[3:]
     assert flagged(scan) == []
+
+
+LOAD_OF_ROWS = re.compile(r"^\s+(global_load_dwordx4|s_load_dwordx16|ds_write_b32|ds_write2)")
+
+
+def _acquire_after_poll(body):
+    """For every decoded-prefix poll in body (the ctz of the inverted ballot of the
+    chunk flags: s_ff1_i32_b64), the first instruction after it that loads rows or
+    publishes in_ready must come after a buffer_inv sc1. Returns the offending
+    (poll, load) pairs."""
+    bad = []
+    for k, line in enumerate(body):
+        if "s_ff1_i32_b64" not in line:
+            continue
+        acquired = False
+        for l2 in body[k + 1:]:
+            if re.match(r"^\s+buffer_inv sc1", l2):
+                acquired = True
+                break
+            if LOAD_OF_ROWS.match(l2):
+                break
+        if not acquired:
+            bad.append(line.strip())
+    return bad
+
+
+def test_decoded_chunks_acquired_before_loads(isa):
+    """Every k_smooth_chain instantiation: the feeder's poll of the decoders' chunk
+    flags is followed by an agent-scope acquire before its L2 pulls, scalar-cache
+    touches or in_ready store (MI355X_MICROARCH.md: one relaxed poll -> one agent
+    acquire -> wait -> loads); the decoded rows are 128-byte-line-owned per chunk
+    (kDecRowAlign), so the acquire is the whole consumer side."""
+    bodies = _bodies(isa, PROTOCOL_KERNELS["k_smooth_chain"])
+    assert len(bodies) >= 14
+    for name, body in bodies:
+        polls = [l for l in body if "s_ff1_i32_b64" in l]
+        assert polls, name  # the decoded-prefix poll is in every instantiation
+        assert not _acquire_after_poll(body), name
+
+
+def test_acquire_checker_flags_a_missing_acquire():
+    poll = ["\tv_cmp_eq_u32_e32 vcc, s83, v2", "\ts_not_b64 s[8:9], vcc", "\ts_ff1_i32_b64 s8, s[8:9]"]
+    good = poll + ["\ts_cbranch_scc1 .LBB24_212", "\tbuffer_inv sc1", "\tglobal_load_dwordx4 v[20:23], v[24:25], off"]
+    assert _acquire_after_poll(good) == []
+    missing = poll + ["\ts_cbranch_scc1 .LBB24_212", "\tglobal_load_dwordx4 v[20:23], v[24:25], off",
+                      "\tbuffer_inv sc1"]
+    assert _acquire_after_poll(missing) == ["s_ff1_i32_b64 s8, s[8:9]"]
+    touch = poll + ["\ts_load_dwordx16 s[40:55], s[56:57], 0x0"]
+    assert _acquire_after_poll(touch)

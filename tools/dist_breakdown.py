@@ -1,0 +1,65 @@
+"""configs[4] through distributed.par_deconvolute_spectra, taken apart (GPU box,
+under torch.distributed.run; nccl = RCCL): the whole call, the rank's block through
+the host path alone (Deconvoluter._run), the exchange alone (distributed.gather_host
+on that block's results), a barrier, and the single-process
+Deconvoluter.par_deconvolute_spectra of the whole set. Median ms of 20 calls each.
+
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \\
+        --master-addr 127.0.0.1 --master-port 29512 tools/dist_breakdown.py
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "metabodecon-rust_amd")]
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
+    ap.add_argument("--reps", type=int, default=20)
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import metabodecon as md
+    from metabodecon import _native as nat
+    from metabodecon.distributed import gather_host, par_deconvolute_spectra, shard_range
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    rank, world = dist.get_rank(), dist.get_world_size()
+    spectra = md.Spectrum.read_bruker_set(os.path.join(ROOT, "tests", "golden", "bruker", "blood"),
+                                          10, 10, (-2.2, 11.8))
+    dec = md.Deconvoluter()
+    dec.device = nat.default_device()
+    lo, hi = shard_range(len(spectra), rank, world)
+    block = spectra[lo:hi]
+
+    def med(f):
+        f()
+        ts = []
+        for _ in range(args.reps):
+            dist.barrier()
+            t = time.perf_counter()
+            f()
+            ts.append(time.perf_counter() - t)
+        return 1e3 * float(np.median(ts))
+    res = dec._run(block)
+    out = {
+        "world": world, "rank": rank, "spectra_per_rank": len(block),
+        "par_deconvolute_spectra_dist_ms": med(lambda: par_deconvolute_spectra(dec, spectra)),
+        "block_host_path_ms": med(lambda: dec._run(block)),
+        "gather_host_ms": med(lambda: gather_host(res, len(spectra))),
+        "barrier_ms": med(lambda: dist.barrier()),
+        "single_process_whole_set_ms": med(lambda: dec.par_deconvolute_spectra(spectra)),
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
