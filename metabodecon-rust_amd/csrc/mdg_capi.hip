@@ -818,6 +818,9 @@ EngineSwitches mdg::read_engine_switches() {
     if (f == "tf" || f == "tf12" || f == "tw7" || f == "tw3s" || f == "twf" || f == "twf1" || f == "twf3s" ||
         f == "plain")
         copy(w.fitsup, sizeof(w.fitsup), f);
+#ifdef MDG_DIAG
+    if (f == "mfma") copy(w.fitsup, sizeof(w.fitsup), f);  // the configs[2] experiment (not bit-exact)
+#endif
     w.tw_g = std::max(0, num("MDG_TW_G", 0));
     if (!str("MDG_TW_G").empty()) w.tw_g = std::max(1, w.tw_g);
     w.gfit = std::max(1, num("MDG_GFIT", 24));

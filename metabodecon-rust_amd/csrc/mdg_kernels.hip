@@ -2813,6 +2813,73 @@ __global__ __launch_bounds__(64 * (SH::EW + 1)) void k_fit_sup_tw(BatchArgs a, W
     else fit_tw_body<false, SH>(w, s, P, it, T, blockIdx.x, gridDim.x);
 }
 
+#ifdef MDG_DIAG
+// EXPERIMENT, diagnostic builds only (make diag; BASELINE configs[2], "superposition
+// recast as MFMA outer product"): the fit superposition with every
+// denominator hw2 + (x - maxp)^2 taken from v_mfma_f64_16x16x4_f64 as the product
+// [x'^2, x', 1, 0] . [1, -2m', m'^2 + hw2, 0] with x' = x - c, m' = maxp - c centred
+// on the tile's first point (to keep the cancellation near a peak small). A wave
+// owns 16 points (A rows) and walks the peaks 16 at a time (B columns); lane l then
+// holds the denominators of peak 16t + (l & 15) at points (l >> 4) + 4r, r = 0..3,
+// divides sfhw by them (div_rn under the fast flags) and accumulates per lane; the
+// 16 lanes of a row then add their partial sums. NOT bit-identical (the
+// denominators round differently and the sum is reordered), so never in the
+// product library: MDG_FITSUP=mfma selects it in the diagnostic build, and
+// tools/mfma_experiment.py measures it against the exact kernel and the oracle
+// (round 2: 1.87 against 1.395 ms per launch at B = 256, 3.7e-4 relative deviation
+// of the fitted parameters).
+template <bool FAST>
+__device__ __forceinline__ void fit_mfma_tile(const Workspace& w, size_t base, int P, int p0, int npts,
+                                              const double* __restrict__ params) {
+    typedef double v4d __attribute__((ext_vector_type(4)));
+    const int lane = threadIdx.x & 63;
+    const int col = lane & 15, kk = lane >> 4;
+    const double* rx = w.rx + 3 * base;
+    const double c = rx[min(p0, npts - 1)];
+    const double xa = rx[min(p0 + col, npts - 1)] - c;  // A: row = point p0 + col
+    const double av = kk == 0 ? xa * xa : kk == 1 ? xa : kk == 2 ? 1.0 : 0.0;
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int j0 = 0; j0 < P; j0 += 16) {
+        const int j = min(j0 + col, P - 1);
+        const double f = params[3 * j], h = params[3 * j + 1], m = params[3 * j + 2] - c;
+        const double bv = kk == 0 ? 1.0 : kk == 1 ? -2.0 * m : kk == 2 ? m * m + h : 0.0;
+        v4d d = {0.0, 0.0, 0.0, 0.0};
+        d = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, d, 0, 0, 0);
+        if (j0 + col < P) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[r] += FAST ? div_rn(f, d[r]) : f / d[r];
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) acc[r] += __shfl_xor(acc[r], o, 16);
+    }
+    if (col == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = p0 + kk + 4 * r;
+            if (i < npts) w.ratio[3 * base + i] = w.ry[3 * base + i] / acc[r];  // fitter_analytical.rs:42-47
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_fit_sup_mfma(BatchArgs a, Workspace w, int it) {
+    const int s = blockIdx.x % a.B, part = blockIdx.x / a.B, parts = gridDim.x / a.B;
+    if (w.status[s] || fit_done(w, s, it)) return;
+    const int P = w.sel_count[s];
+    const size_t base = (size_t)s * w.capD;
+    const double* __restrict__ params = w.params + 3 * base;
+    if (part == 0 && threadIdx.x == 0) w.unsafe[4 * s + ((it + 1) & 1)] = 0;
+    const bool fast = w.x_ok[s] && w.unsafe[4 * s + (it & 1)] == 0;
+    const int npts = 3 * P, wv = threadIdx.x >> 6;
+    for (int p0 = (part * 4 + wv) * 16; p0 < npts; p0 += parts * 64) {
+        if (fast) fit_mfma_tile<true>(w, base, P, p0, npts, params);
+        else fit_mfma_tile<false>(w, base, P, p0, npts, params);
+    }
+}
+#endif
+
 // K6i  the same term-fold tiles over ONE batch-wide list ("twf"): the tiles of all
 // spectra, spectrum after spectrum, grid-strided over a 1-D grid of about one
 // workgroup per slot of the chip. A (G, B) grid with a fixed G per spectrum leaves
@@ -3737,12 +3804,24 @@ static std::string fit_choice(const BatchArgs& a, const EngineSwitches& sw) {
     if (a.B == 1) return a.latency ? "tf12" : "tw7";
     return a.B <= 4 ? "tf" : a.B <= 24 ? "twf1" : "plain";
 }
-bool fit_sup_fused(const BatchArgs& a, const EngineSwitches& sw) { return fit_choice(a, sw) != "plain"; }
+bool fit_sup_fused(const BatchArgs& a, const EngineSwitches& sw) {
+    const std::string f = fit_choice(a, sw);
+    return f != "plain" && f != "mfma";  // those two leave the stencil update to k_fit_update
+}
 const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int it, const EngineSwitches& sw,
                            hipStream_t st) {
     const std::string f = fit_choice(a, sw);
     // MDG_TW_G (tuning): workgroups per spectrum; tiles beyond them grid-stride
     const int tg = sw.tw_g;
+#ifdef MDG_DIAG
+    if (f == "mfma") {
+        // experiment only (diagnostic builds; not bit-exact): 64 points per workgroup
+        const int g = std::max(1, std::min(2048, (3 * (a.N / 2 + 2) + 63) / 64));
+        const int parts = std::max(1, std::min(g, 8192 / a.B));
+        launch_k(k_fit_sup_mfma, dim3(parts * a.B), dim3(256), 0, st, a, w, it);
+        return "k_fit_sup_mfma";
+    }
+#endif
     if (f == "tw7") {
         // 7 evaluator waves: 1 peak block x 7 point subsets, 63 points per workgroup:
         // one workgroup per tile of a 2048-peak spectrum (98)

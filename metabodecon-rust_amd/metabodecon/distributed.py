@@ -165,6 +165,35 @@ def gather_tables(status, counts, mse, tables, n_total: int, group=None, dst=0):
     return None if got is None else tuple(t.clone() for t in got)
 
 
+class _Exchange:
+    """gather_host's buffers for one (process group, thread): flat, grow-only, with
+    their numpy views made once, so a call costs a few slices and copies (a 16-spectrum
+    call spent ~0.15 ms in per-call tensor views and shape handling when every buffer
+    was re-viewed each call)."""
+
+    def __init__(self, nccl, dev):
+        import torch
+        self.nccl, self.dev = nccl, dev
+        self.hdr_h = torch.zeros(2, dtype=torch.int64, pin_memory=nccl)
+        self.hdr_np = self.hdr_h.numpy()
+        self.hdr_d = self.hdr_h.to(dev) if nccl else self.hdr_h
+        self.cap = 0
+        self.rcap = 0
+
+    def grow(self, need, rneed):
+        import torch
+        if need > self.cap:
+            self.cap = max(need, 2 * self.cap)
+            self.pack_h = torch.empty(self.cap, dtype=torch.float64, pin_memory=self.nccl)
+            self.pack_np = self.pack_h.numpy()
+            self.pack_d = torch.empty(self.cap, dtype=torch.float64, device=self.dev) if self.nccl else self.pack_h
+        if rneed > self.rcap:
+            self.rcap = max(rneed, 2 * self.rcap)
+            self.recv_d = torch.empty(self.rcap, dtype=torch.float64, device=self.dev)
+            self.recv_h = torch.empty(self.rcap, dtype=torch.float64, pin_memory=True) if self.nccl else self.recv_d
+            self.recv_np = self.recv_h.numpy()
+
+
 def gather_host(local: Sequence[Result], n_total: int, group=None, dst=0, error: str | None = None):
     """The exchange of one multi-GPU call whose block results are on the host
     (``Deconvoluter._run``: the kernels write them into page-locked memory).
@@ -179,17 +208,19 @@ def gather_host(local: Sequence[Result], n_total: int, group=None, dst=0, error:
     [status, count, mse, table rows] records. With nccl the records are packed into
     a page-locked buffer and sent by one H2D copy (RCCL gathers device memory); the
     collecting rank copies the gathered rows back once. Buffers are kept across
-    calls."""
+    calls, per process group and thread."""
     import torch
     import torch.distributed as dist
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     nccl = dist.get_backend(group) == "nccl"
-    dev = torch.device("cuda", torch.cuda.current_device()) if nccl else torch.device("cpu")
-    host = "pinned" if nccl else "cpu"
-    per_rank = [shard_range(n_total, r, world) for r in range(world)]
-    max_items = max(hi - lo for lo, hi in per_rank)
-    lo = per_rank[rank][0]
-    b = len(local)
+    key = _key("exchange", None, torch.cuda.current_device() if nccl else "cpu", group)
+    ex = _BUFS.get(key)
+    if ex is None:
+        ex = _BUFS[key] = _Exchange(nccl, torch.device("cuda", torch.cuda.current_device()) if nccl
+                                    else torch.device("cpu"))
+    base, rem = divmod(n_total, world)
+    max_items = base + (1 if rem else 0)
+    lo = shard_range(n_total, rank, world)[0]
     width = max([int(p.shape[0]) for _, p, _ in local] + [1])
     fail = _FAIL_NONE
     if error is not None:
@@ -199,11 +230,11 @@ def gather_host(local: Sequence[Result], n_total: int, group=None, dst=0, error:
             if st:
                 fail = -((lo + k) * 1024 + int(st))
                 break
-    hdr_h = _buf("hdr_h", (2,), torch.int64, host, group)
-    hdr_h[0], hdr_h[1] = width, fail
-    hdr = _buf("hdr_d", (2,), torch.int64, dev, group).copy_(hdr_h, non_blocking=True) if nccl else hdr_h
-    dist.all_reduce(hdr, op=dist.ReduceOp.MAX, group=group)
-    w_all, f_all = (int(v) for v in hdr.tolist())
+    ex.hdr_np[0], ex.hdr_np[1] = width, fail
+    if nccl:
+        ex.hdr_d.copy_(ex.hdr_h, non_blocking=True)
+    dist.all_reduce(ex.hdr_d, op=dist.ReduceOp.MAX, group=group)
+    w_all, f_all = ex.hdr_d.tolist()
     if f_all != _FAIL_NONE:
         idx, st = (-f_all) // 1024, (-f_all) % 1024
         first = (idx, None if st == 1023 else st)
@@ -212,24 +243,26 @@ def gather_host(local: Sequence[Result], n_total: int, group=None, dst=0, error:
     else:
         first = None
     cols = 3 + 3 * w_all
-    pk_h = _buf("pack_h", (max_items, cols), torch.float64, host, group)
-    a = pk_h.numpy()
+    need = max_items * cols
+    ex.grow(need, world * need)
+    a = ex.pack_np[:need].reshape(max_items, cols)
     for k, (st, p, m) in enumerate(local):
         c = int(p.shape[0])
         a[k, 0], a[k, 1], a[k, 2] = st, c, m
         if c:
             a[k, 3:3 + 3 * c] = np.asarray(p, dtype=np.float64).reshape(-1)
-    pk = _buf("pack_d", (max_items, cols), torch.float64, dev, group).copy_(pk_h, non_blocking=True) \
-        if nccl else pk_h
-    recv = _buf("recv", (world * max_items, cols), torch.float64, dev, group)
-    got = _collect(recv, pk, dst, group)
+    pk = ex.pack_d[:need]
+    if nccl:
+        pk.copy_(ex.pack_h[:need], non_blocking=True)
+    got = _collect(ex.recv_d[:world * need], pk, dst, group)
     if got is None:
         return first, None
     if nccl:
-        got = _buf("recv_h", (world * max_items, cols), torch.float64, host, group).copy_(got)
-    g = got.numpy()
+        ex.recv_h[:world * need].copy_(got)
+    g = ex.recv_np[:world * need].reshape(world * max_items, cols)
     results = []
-    for r, (l, h) in enumerate(per_rank):
+    for r in range(world):
+        l, h = shard_range(n_total, r, world)
         for k in range(h - l):
             row = g[r * max_items + k]
             c = int(row[1])

@@ -49,17 +49,21 @@ def brief(path):
     print("  ".join(f"{k} {sum(v) / len(v):.1f}x{len(v)}" for k, v in per.items()))
 
 
-if __name__ == "__main__":
-    if sys.argv[1] == "--summary":
-        summary(sys.argv[2])
-        sys.exit()
-    if sys.argv[1] == "--brief":
-        brief(sys.argv[2])
-        sys.exit()
+def main():
+    import argparse
+    ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
+    ap.add_argument("batch", nargs="?", type=int, default=16, help="blood spectra per call")
+    ap.add_argument("--summary", metavar="CSV", help="print the last call's kernels of a trace")
+    ap.add_argument("--brief", metavar="CSV", help="mean duration per kernel of the last call")
+    args = ap.parse_args()
+    if args.summary:
+        return summary(args.summary)
+    if args.brief:
+        return brief(args.brief)
     sys.path[:0] = [ROOT, os.path.join(ROOT, "metabodecon-rust_amd")]
     import metabodecon as md
     from metabodecon import _native as nat
-    b = int(sys.argv[1])
+    b = args.batch
     S = md.Spectrum.read_bruker_set(os.path.join(ROOT, "tests/golden/bruker/blood"), 10, 10,
                                     (-2.2, 11.8))[:b]
     dec = md.Deconvoluter()
@@ -67,3 +71,7 @@ if __name__ == "__main__":
     for _ in range(5):
         dec._run_batch(ctx, S, list(range(b)), len(S[0]), dec._ignore_array())
     print("ok")
+
+
+if __name__ == "__main__":
+    main()

@@ -32,10 +32,13 @@ def med(fn, calls):
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("calls", nargs="?", type=int, default=200)
+    calls = ap.parse_args().calls
     import torch
     import metabodecon as md
     from metabodecon import _native as nat
-    calls = int(sys.argv[1]) if len(sys.argv) > 1 else 200
     sp = md.Spectrum.read_bruker(os.path.join(ROOT, "tests/golden/bruker/blood/blood_01"), 10, 10,
                                  (-2.2, 11.8))
     dec = md.Deconvoluter()

@@ -1,28 +1,33 @@
 """configs[4] experiment: the 16 blood spectra through
-Deconvoluter.par_deconvolute_spectra with L lanes (one spectrum per engine context,
-concurrently) against one batched call (L = 1 -> B = 16), host buffers in and out.
+Deconvoluter.par_deconvolute_spectra with L lanes (engine contexts running
+concurrently, one spectrum each at L = 16) against one batched call of 16, host
+buffers in and out; results compared bit for bit between the settings.
 
-    GPU box: python tools/c4_lanes.py   (prints one line per setting)
+    GPU box: python tools/c4_lanes.py [--lanes 16 1 ...]   (prints one line per setting)
 """
+import argparse
 import os
 import sys
 import time
 
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "32")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [ROOT, os.path.join(ROOT, "metabodecon-rust_amd")]
-
-import numpy as np  # noqa: E402
-
-import metabodecon as md  # noqa: E402
 
 
 def main():
+    ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
+    ap.add_argument("--lanes", type=int, nargs="+", default=[16, 1, 16, 1])
+    args = ap.parse_args()
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "32")
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "metabodecon-rust_amd")]
+    import numpy as np
+    import metabodecon as md
     spectra = md.Spectrum.read_bruker_set(os.path.join(ROOT, "tests", "golden", "bruker", "blood"),
                                           10, 10, (-2.2, 11.8))
     ref = None
-    for lanes in (16, 1, 16, 1):  # 16 lanes, or (any L < 16) one batched call of 16
+    for lanes in args.lanes:
         md.Deconvoluter.LANES = lanes
+        # one batch below ONE_LANE_UPTO spectra unless lanes are asked for
+        md.Deconvoluter.ONE_LANE_UPTO = 16 if lanes == 1 else 0
         dec = md.Deconvoluter()
         for _ in range(2):
             res = dec.par_deconvolute_spectra(spectra)

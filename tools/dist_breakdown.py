@@ -48,12 +48,57 @@ def main():
             ts.append(time.perf_counter() - t)
         return 1e3 * float(np.median(ts))
     res = dec._run(block)
+    from metabodecon._deconvolution import Deconvolution
+    gloo = dist.new_group(backend="gloo")
+    hh = torch.zeros(2, dtype=torch.int64)
+    hp = torch.zeros(2, dtype=torch.int64).pin_memory()
+    hd = torch.zeros(2, dtype=torch.int64, device="cuda")
+
+    def hdr_rccl():
+        hd.copy_(hp, non_blocking=True)
+        dist.all_reduce(hd, op=dist.ReduceOp.MAX)
+        return hd.tolist()
+    cols = 3 + 3 * 1400
+    pk = torch.zeros((len(block), cols), dtype=torch.float64, device="cuda")
+    rv = torch.zeros((world * len(block), cols), dtype=torch.float64, device="cuda")
+    rh = torch.zeros((world * len(block), cols), dtype=torch.float64).pin_memory()
+
+    def gath():
+        if rank == 0:
+            dist.gather(pk, list(rv.chunk(world)), dst=0)
+            rh.copy_(rv)
+        else:
+            dist.gather(pk, None, dst=0)
+
+    def stamped():  # par_deconvolute_spectra's steps with a stamp after each
+        t = [time.perf_counter()]
+        torch.cuda.set_device(dec.device)
+        t.append(time.perf_counter())
+        loc = dec._run(block)
+        t.append(time.perf_counter())
+        first, got = gather_host(loc, len(spectra))
+        t.append(time.perf_counter())
+        if got is not None:
+            snap = dec.settings
+            [Deconvolution._of(p, m, snap) for _, p, m in got]
+        t.append(time.perf_counter())
+        return np.diff(t)
+    stamped()
+    parts = []
+    for _ in range(args.reps):
+        dist.barrier()
+        parts.append(stamped())
+    parts = 1e3 * np.median(np.array(parts), axis=0)
     out = {
+        "stamped_ms": dict(zip(["set_device", "run_block", "gather_host", "results"], parts.tolist())),
         "world": world, "rank": rank, "spectra_per_rank": len(block),
         "par_deconvolute_spectra_dist_ms": med(lambda: par_deconvolute_spectra(dec, spectra)),
         "block_host_path_ms": med(lambda: dec._run(block)),
         "gather_host_ms": med(lambda: gather_host(res, len(spectra))),
         "barrier_ms": med(lambda: dist.barrier()),
+        "hdr_rccl_ms": med(lambda: hdr_rccl()),
+        "hdr_gloo_ms": med(lambda: dist.all_reduce(hh, op=dist.ReduceOp.MAX, group=gloo)),
+        "gather_rccl_540k_ms": med(lambda: gath()),
         "single_process_whole_set_ms": med(lambda: dec.par_deconvolute_spectra(spectra)),
     }
     if rank == 0:

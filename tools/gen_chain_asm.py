@@ -167,6 +167,8 @@ def program(ws):
 
 
 def main():
+    import argparse
+    argparse.ArgumentParser(description=__doc__.split("\n\n")[0]).parse_args()
     lines = ["// Generated by tools/gen_chain_asm.py -- do not edit.",
              f"// Steady loop of the k_smooth_chain chain wave, CB = {CB} ticks per block.",
              f"#define MDG_CHAIN_CB {CB}", f"#define MDG_CHAIN_BPT {BPT}", f"#define MDG_CHAIN_G {G}", ""]

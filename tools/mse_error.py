@@ -1,21 +1,26 @@
-"""Relative MSE deviation of every MSE kernel from the oracle's left-fold MSE
-(compute_mse, deconvoluter.rs:828-862) over all golden cases and a few synthetic
-spectra: python tools/mse_error.py  (GPU). Prints the max |rel| per kernel."""
+"""Relative deviation of the engine's MSE from the oracle's left-fold MSE
+(compute_mse, deconvoluter.rs:828-862) over all golden cases and two more synthetic
+spectra (GPU box), for each MSE form the library ships: the local expansions with 2
+and with 4 points per thread (MDG_MSE_NPT; the default picks by batch size) and the
+exact-order option (MDG_OPTION_EXACT_MSE, expected 0). Prints the max |rel| per form.
+
+    python tools/mse_error.py
+"""
+import argparse
 import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [ROOT, os.path.join(ROOT, "metabodecon-rust_amd")]
-
-import numpy as np  # noqa: E402
-
-import oracle  # noqa: E402
-from tests.golden.cases import CASES, load_case, synth_spectrum  # noqa: E402
-from tests.test_gpu_parity import gpu_batch  # noqa: E402
-from metabodecon import _native as nat  # noqa: E402
 
 
 def main():
+    argparse.ArgumentParser(description=__doc__.split("\n\n")[0]).parse_args()
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "metabodecon-rust_amd")]
+    import numpy as np
+    import oracle
+    from metabodecon import _native as nat
+    from tests.golden.cases import CASES, load_case, synth_spectrum
+    from tests.test_gpu_parity import gpu_batch
     ctx = nat.context(0)
     cases = []
     for name in CASES:
@@ -27,18 +32,22 @@ def main():
         x, y, _ = synth_spectrum(seed)
         o = oracle.deconvolute(x, y, (11.8, -2.2), threads=16)
         cases.append((f"synth_{seed}", x, y, (11.8, -2.2), oracle.default_settings(), (), o.mse))
-    for kind in ("local", "local1", "quad", "n", "plain"):
-        os.environ["MDG_MSE"] = "local" if kind.startswith("local") else kind
-        os.environ["MDG_MSE_NPT"] = "1" if kind == "local1" else "2"
+    for form, npt, exact in (("local, 2 points per thread", "2", False),
+                             ("local, 4 points per thread", "4", False), ("exact order", "2", True)):
+        os.environ["MDG_MSE_NPT"] = npt
+        ctx.reload_switches()  # the engine reads its switches per context, not per call
         worst, wname = 0.0, None
         for name, x, y, sb, st, ign, ref in cases:
-            status, counts, out, mse = gpu_batch(ctx, x, y[None, :], [sb], st, ign)
+            s = nat.Settings()
+            for f, _ in nat.Settings._fields_:
+                setattr(s, f, getattr(st, f, 0))
+            s.options = nat.OPTION_EXACT_MSE if exact else 0
+            status, counts, out, mse = gpu_batch(ctx, x, y[None, :], [sb], s, ign)
             assert status[0] == 0, (name, status[0])
             rel = abs(mse[0] - ref) / abs(ref)
             if rel > worst:
                 worst, wname = rel, name
-        print(f"MDG_MSE={kind}: max |rel err| {worst:.3e} ({wname}) over {len(cases)} spectra",
-              flush=True)
+        print(f"{form}: max |rel err| {worst:.3e} ({wname}) over {len(cases)} spectra", flush=True)
 
 
 if __name__ == "__main__":

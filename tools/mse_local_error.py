@@ -82,11 +82,15 @@ def report(name, xs, ys, P, shapes):
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
+    ap.add_argument("cases", nargs="*", help="golden case names (default: five)")
+    names_arg = ap.parse_args().cases
     from cases import load_case, synth_spectrum
     import oracle
     shapes = [(256, 5.0, 20), (256, 5.0, 20, True), (512, 5.0, 20), (512, 5.0, 20, True),
               (512, 4.0, 24, True)]
-    names = sys.argv[1:] or ["blood_01", "blood_05", "blood_09", "sim_01", "synth"]
+    names = names_arg or ["blood_01", "blood_05", "blood_09", "sim_01", "synth"]
     for nm in names:
         if nm == "synth":
             x, y, _ = synth_spectrum(0)

@@ -116,4 +116,9 @@ def main(rnd, tags):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2:])
+    import argparse
+    ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
+    ap.add_argument("round", help="round tag of the output files, e.g. r05")
+    ap.add_argument("tags", nargs="+", help="workload tags (gpurun_out/prof_<tag>), or calib")
+    a = ap.parse_args()
+    main(a.round, a.tags)

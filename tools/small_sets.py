@@ -17,6 +17,8 @@ import metabodecon as md  # noqa: E402
 
 
 def main():
+    import argparse
+    argparse.ArgumentParser(description=__doc__.split("\n\n")[0]).parse_args()
     spectra = md.Spectrum.read_bruker_set(os.path.join(ROOT, "tests", "golden", "bruker", "blood"),
                                           10, 10, (-2.2, 11.8))
     D = md.Deconvoluter

@@ -22,8 +22,12 @@ from metabodecon import _native as nat  # noqa: E402
 
 
 def main():
-    S = int(sys.argv[1]) if len(sys.argv) > 1 else 4
-    K = int(sys.argv[2]) if len(sys.argv) > 2 else 40
+    import argparse
+    ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
+    ap.add_argument("contexts", nargs="?", type=int, default=4)
+    ap.add_argument("spectra", nargs="?", type=int, default=40)
+    a = ap.parse_args()
+    S, K = a.contexts, a.spectra
     dev = torch.device("cuda", 0)
     n, cap = 131072, 4096
     settings = nat.default_settings()
