@@ -179,6 +179,12 @@ int mdg_ctx_set_latency_mode(mdg_ctx* ctx, int on);
  * bit-exact) are read from the environment once, when the context is created; this
  * reads them again (nothing else on a call's path reads the environment). */
 int mdg_ctx_reload_switches(mdg_ctx* ctx);
+/* roctx ranges ("prep", "smooth", "detect", "select", "fit_superposition", ...) around
+ * every pipeline stage this context launches (default off; MDG_ROCTX=1 at context
+ * creation turns it on): a rocprofv3 trace with --marker-trace --hip-trace
+ * --kernel-trace attributes each kernel to its stage with no events in the stream.
+ * MDG_ERR_HIP when the roctx library cannot be loaded (the ranges stay off). */
+int mdg_ctx_set_tracing(mdg_ctx* ctx, int on);
 
 /* ---- hot path: host buffers ------------------------------------------------
  * x, y: n chemical shifts / intensities of a validated Spectrum

@@ -14,6 +14,7 @@
 #include <cstddef>
 #include <cstdio>
 #include <cstring>
+#include <dlfcn.h>
 #include <map>
 #include <mutex>
 #include <string>
@@ -41,6 +42,34 @@ struct Pending {
     hipEvent_t a, b;
 };
 
+// roctx ranges around each pipeline stage (mdg_ctx_set_tracing / MDG_ROCTX=1), so a
+// rocprofv3 trace (--marker-trace with --kernel-trace and --hip-trace) attributes
+// every kernel to its stage through the host-side launch inside the range, without
+// hipEvents in the stream. The roctx library is opened on first use (dlopen): a
+// process that never traces does not load it.
+const char* const kStageNames[kStages] = {"prep", "smooth", "detect", "select", "fit_init",
+                                          "fit_superposition", "fit_update", "retain",
+                                          "mse_superposition", "mse_reduce", "superposition_vec",
+                                          "synth"};
+struct Roctx {
+    int (*push)(const char*) = nullptr;
+    int (*pop)() = nullptr;
+};
+const Roctx& roctx() {
+    static const Roctx r = [] {
+        Roctx t;
+        void* h = dlopen("librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (h) {
+            t.push = (int (*)(const char*))dlsym(h, "roctxRangePushA");
+            t.pop = (int (*)())dlsym(h, "roctxRangePop");
+            if (!t.push || !t.pop) t.push = nullptr, t.pop = nullptr;
+        }
+        return t;
+    }();
+    return r;
+}
+
 struct Buffer {
     void* p = nullptr;
     size_t bytes = 0;
@@ -58,6 +87,8 @@ struct mdg_ctx {
     // latency mode (mdg_ctx_set_latency_mode): a B = 1 pipeline expects the GPU to
     // itself and takes the finer fit tiles (fit_choice)
     int latency = 1;
+    // roctx ranges around the pipeline's stages (mdg_ctx_set_tracing, MDG_ROCTX=1)
+    bool tracing = false;
     std::mutex mu;
     // workspace arena
     Buffer arena;
@@ -167,13 +198,16 @@ struct StageTimer {
     mdg_ctx* c;
     int stage;
     hipEvent_t a = nullptr;
+    bool range = false;
     StageTimer(mdg_ctx* c_, int s) : c(c_), stage(s) {
+        if (c->tracing && roctx().push) range = roctx().push(kStageNames[stage]) >= 0;
         if ((c->profile_mask >> stage) & 1u) {
             a = get_event(c);
             if (a) (void)hipEventRecord(a, c->stream);
         }
     }
     ~StageTimer() {
+        if (range) roctx().pop();
         if (a) {
             hipEvent_t b = get_event(c);
             if (b) {
@@ -831,6 +865,7 @@ EngineSwitches mdg::read_engine_switches() {
     w.graphs = str("MDG_GRAPHS") == "1";
     w.host_direct = str("MDG_HOST_DIRECT").substr(0, 1) != "0";
     w.dec_overlap = str("MDG_DEC_OVERLAP").substr(0, 1) != "0";
+    w.roctx = str("MDG_ROCTX") == "1";
 #ifdef MDG_DIAG
     copy(w.diag_skip, sizeof(w.diag_skip), str("MDG_DIAG_SKIP"));
     copy(w.diag_dup, sizeof(w.diag_dup), str("MDG_DIAG_DUP"));
@@ -863,6 +898,7 @@ int mdg_ctx_create(int device, mdg_ctx** out) {
     }
     c->stream = c->own;
     c->sw = read_engine_switches();
+    c->tracing = c->sw.roctx != 0;
     *out = c;
     return MDG_OK;
 }
@@ -978,7 +1014,15 @@ int mdg_ctx_reload_switches(mdg_ctx* c) {
     const EngineSwitches w = read_engine_switches();
     std::lock_guard<std::mutex> g(c->mu);
     c->sw = w;
+    c->tracing = w.roctx != 0;
     return MDG_OK;
+}
+
+int mdg_ctx_set_tracing(mdg_ctx* c, int on) {
+    if (!c || (on != 0 && on != 1)) return MDG_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> g(c->mu);
+    c->tracing = on != 0;
+    return c->tracing && !roctx().push ? MDG_ERR_HIP : MDG_OK;
 }
 
 int mdg_ctx_last_peaks(mdg_ctx* c, size_t spectrum, int which, int32_t* left, int32_t* center,

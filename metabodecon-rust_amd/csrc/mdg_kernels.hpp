@@ -135,6 +135,7 @@ struct EngineSwitches {
     int graphs = 0;              // MDG_GRAPHS=1
     int host_direct = 1;         // MDG_HOST_DIRECT=0: device copies of the small inputs / results
     int dec_overlap = 1;         // MDG_DEC_OVERLAP=0: compact rows by DMA + decode launch
+    int roctx = 0;               // MDG_ROCTX=1: roctx ranges around the pipeline stages
     // diagnostic builds only (make diag)
     char diag_skip[32] = {};
     char diag_dup[64] = {};

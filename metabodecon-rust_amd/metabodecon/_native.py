@@ -54,7 +54,7 @@ EXPORTS = [
     "mdg_queue_create", "mdg_queue_submit", "mdg_queue_flush", "mdg_queue_set_flush_us",
     "mdg_queue_synchronize",
     "mdg_queue_lane", "mdg_queue_stats", "mdg_queue_destroy", "mdg_queue_fail_next_launch",
-    "mdg_jcampdx_decode", "mdg_ctx_set_latency_mode", "mdg_ctx_reload_switches",
+    "mdg_jcampdx_decode", "mdg_ctx_set_latency_mode", "mdg_ctx_reload_switches", "mdg_ctx_set_tracing",
 ]
 
 
@@ -238,6 +238,7 @@ def _declare(L):
     L.mdg_ctx_stage_kernel.argtypes = [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p)]
     L.mdg_ctx_set_latency_mode.argtypes = [_vp, ctypes.c_int]
     L.mdg_ctx_reload_switches.argtypes = [_vp]
+    L.mdg_ctx_set_tracing.argtypes = [_vp, ctypes.c_int]
     L.mdg_deconvolute.argtypes = [_vp, _dp, _dp, _sz, ctypes.c_double, ctypes.c_double, sp, _dp,
                                   _sz, _dp, _sz, _szp, _dp]
     L.mdg_deconvolute_batch.argtypes = [_vp, _sz, _sz, _dp, _sz, _dp, _sz, _dp, sp, _dp, _sz,
@@ -404,6 +405,12 @@ class Context:
         st = lib().mdg_ctx_set_latency_mode(self.handle, 1 if on else 0)
         if st:
             raise RuntimeError(strerror(st))
+
+    def set_tracing(self, on: bool) -> bool:
+        """roctx ranges around every pipeline stage of this context (rocprofv3
+        --marker-trace attributes the kernels to stages); False when the roctx
+        library is not available."""
+        return lib().mdg_ctx_set_tracing(self.handle, 1 if on else 0) == 0
 
     def reload_switches(self):
         """Re-read the MDG_* engine switches from the environment (the engine reads

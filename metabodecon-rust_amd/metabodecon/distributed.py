@@ -207,8 +207,9 @@ def gather_host(local: Sequence[Result], n_total: int, group=None, dst=0, error:
     the table width and the first failure, then ONE gather of the packed
     [status, count, mse, table rows] records. With nccl the records are packed into
     a page-locked buffer and sent by one H2D copy (RCCL gathers device memory); the
-    collecting rank copies the gathered rows back once. Buffers are kept across
-    calls, per process group and thread."""
+    collecting rank copies the other ranks' rows back once and keeps its own block's
+    results as they are (the caller's arrays: they are not copied). Buffers are kept
+    across calls, per process group and thread."""
     import torch
     import torch.distributed as dist
     world, rank = dist.get_world_size(group), dist.get_rank(group)
@@ -245,23 +246,34 @@ def gather_host(local: Sequence[Result], n_total: int, group=None, dst=0, error:
     cols = 3 + 3 * w_all
     need = max_items * cols
     ex.grow(need, world * need)
-    a = ex.pack_np[:need].reshape(max_items, cols)
-    for k, (st, p, m) in enumerate(local):
-        c = int(p.shape[0])
-        a[k, 0], a[k, 1], a[k, 2] = st, c, m
-        if c:
-            a[k, 3:3 + 3 * c] = np.asarray(p, dtype=np.float64).reshape(-1)
+    # a receiving rank keeps its own block's results where they are (they never
+    # leave host memory): the collecting rank of a gather neither packs nor sends
+    # them -- its part of the output is left unread -- and every receiver copies back
+    # only the other ranks' parts
     pk = ex.pack_d[:need]
-    if nccl:
-        pk.copy_(ex.pack_h[:need], non_blocking=True)
+    if dst is None or rank != dst:  # (an all-gather sends every rank's part)
+        a = ex.pack_np[:need].reshape(max_items, cols)
+        for k, (st, p, m) in enumerate(local):
+            c = int(p.shape[0])
+            a[k, 0], a[k, 1], a[k, 2] = st, c, m
+            if c:
+                a[k, 3:3 + 3 * c] = np.asarray(p, dtype=np.float64).reshape(-1)
+        if nccl:
+            pk.copy_(ex.pack_h[:need], non_blocking=True)
     got = _collect(ex.recv_d[:world * need], pk, dst, group)
     if got is None:
         return first, None
-    if nccl:
-        ex.recv_h[:world * need].copy_(got)
+    if nccl and world > 1:  # the other ranks' parts: before and after this rank's own
+        if rank > 0:
+            ex.recv_h[:rank * need].copy_(got[:rank * need])
+        if rank < world - 1:
+            ex.recv_h[(rank + 1) * need:world * need].copy_(got[(rank + 1) * need:])
     g = ex.recv_np[:world * need].reshape(world * max_items, cols)
     results = []
     for r in range(world):
+        if r == rank:
+            results.extend((int(st), p, float(m)) for st, p, m in local)
+            continue
         l, h = shard_range(n_total, r, world)
         for k in range(h - l):
             row = g[r * max_items + k]

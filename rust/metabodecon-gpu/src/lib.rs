@@ -121,6 +121,7 @@ pub mod ffi {
         pub fn mdg_ctx_synchronize(ctx: *mut MdgCtx) -> c_int;
         pub fn mdg_ctx_set_latency_mode(ctx: *mut MdgCtx, on: c_int) -> c_int;
         pub fn mdg_ctx_reload_switches(ctx: *mut MdgCtx) -> c_int;
+        pub fn mdg_ctx_set_tracing(ctx: *mut MdgCtx, on: c_int) -> c_int;
         pub fn mdg_deconvolute(
             ctx: *mut MdgCtx,
             x: *const f64,

@@ -83,6 +83,51 @@ def main():
             [Deconvolution._of(p, m, snap) for _, p, m in got]
         t.append(time.perf_counter())
         return np.diff(t)
+    from metabodecon import distributed as D
+
+    def stamped_gather(loc):  # gather_host's steps (nccl, dst 0) with a stamp after each
+        t = [time.perf_counter()]
+        ex = D._BUFS[D._key("exchange", None, torch.cuda.current_device(), None)]
+        width = max([int(p.shape[0]) for _, p, _ in loc] + [1])
+        ex.hdr_np[0], ex.hdr_np[1] = width, D._FAIL_NONE
+        ex.hdr_d.copy_(ex.hdr_h, non_blocking=True)
+        dist.all_reduce(ex.hdr_d, op=dist.ReduceOp.MAX)
+        w_all, f_all = ex.hdr_d.tolist()
+        t.append(time.perf_counter())
+        cols = 3 + 3 * w_all
+        mi = len(loc)
+        need = mi * cols
+        ex.grow(need, world * need)
+        a = ex.pack_np[:need].reshape(mi, cols)
+        for k, (st, p, m) in enumerate(loc):
+            c = int(p.shape[0])
+            a[k, 0], a[k, 1], a[k, 2] = st, c, m
+            if c:
+                a[k, 3:3 + 3 * c] = np.asarray(p, dtype=np.float64).reshape(-1)
+        t.append(time.perf_counter())
+        pk = ex.pack_d[:need]
+        pk.copy_(ex.pack_h[:need], non_blocking=True)
+        t.append(time.perf_counter())
+        got = D._collect(ex.recv_d[:world * need], pk, 0, None)
+        t.append(time.perf_counter())
+        if got is not None:
+            ex.recv_h[:world * need].copy_(got)
+        t.append(time.perf_counter())
+        if got is not None:
+            g = ex.recv_np[:world * need].reshape(world * mi, cols)
+            out = []
+            for k in range(world * mi):
+                row = g[k]
+                c = int(row[1])
+                out.append((int(row[0]), row[3:3 + 3 * c].reshape(c, 3).copy(), float(row[2])))
+        t.append(time.perf_counter())
+        return np.diff(t)
+    gather_host(res, len(spectra))  # creates the exchange buffers
+    gparts = []
+    for _ in range(args.reps):
+        dist.barrier()
+        gparts.append(stamped_gather(res))
+    gparts = 1e3 * np.median(np.array(gparts), axis=0)
     stamped()
     parts = []
     for _ in range(args.reps):
@@ -90,6 +135,7 @@ def main():
         parts.append(stamped())
     parts = 1e3 * np.median(np.array(parts), axis=0)
     out = {
+        "gather_stamped_ms": dict(zip(["header", "pack", "h2d", "gather", "d2h", "unpack"], gparts.tolist())),
         "stamped_ms": dict(zip(["set_device", "run_block", "gather_host", "results"], parts.tolist())),
         "world": world, "rank": rank, "spectra_per_rank": len(block),
         "par_deconvolute_spectra_dist_ms": med(lambda: par_deconvolute_spectra(dec, spectra)),

@@ -47,6 +47,12 @@ def main():
 
     B, n, cap = args.batch, 131072, 4096
     dev = torch.device("cuda", 0)
+    # the diagnostic build's kernels stamp phases into this buffer (mdg_debug_set_diag:
+    # [0, 1 << 22) records, stamp slots after)
+    import ctypes
+    diag = torch.zeros((1 << 22) + 1024, dtype=torch.int64, device=dev)
+    nat.lib().mdg_debug_set_diag.argtypes = [ctypes.c_void_p]
+    assert nat.lib().mdg_debug_set_diag(diag.data_ptr()) == 0
     slot = bench.Slot(nat, torch, dev, B, n, cap)
     x, y = bench.synth_device(nat, slot.ctx, torch, B, n, 2048, 0, dev)
     sb = torch.tensor([bench.SB] * B, dtype=torch.float64, device=dev)
