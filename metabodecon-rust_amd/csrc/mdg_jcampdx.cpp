@@ -222,29 +222,48 @@ void pass_3(const std::string& s, std::string& out) {
 struct M4 {
     size_t start, val0, val1, tok0, tok1;
 };
+// Linear in the run: the token class never holds whitespace, so after a \s+ that
+// ends at a whitespace-run end only the run's next character can start the token
+// (no loop over shorter second runs), and a first \s+ shorter than its run leaves an
+// empty value followed by the rest of the same run (one check for all of them, ADVICE
+// r4: the nested loops were quadratic in a long whitespace run).
 template <class TokC>
 bool match_at(const std::string& s, size_t p, int dmin, TokC tokc, M4& m) {
     const size_t wmax = run(s, p, ws_c);
-    for (size_t w = wmax; w > p; --w) {  // \s+ greedy
+    auto token_after = [&](size_t d, size_t& w2) {  // \s+ then the token's first character
+        w2 = run(s, d, ws_c);
+        return w2 > d && w2 < s.size() && tokc(s[w2]);
+    };
+    size_t w2;
+    {  // \s+ greedy: the whole run first
+        const size_t w = wmax;
         const size_t smax = run(s, w, sign_c);
         for (size_t sg = smax + 1; sg-- > w;) {  // [+-]* greedy
             const size_t dmax = run(s, sg, digit_c);
             for (size_t d = dmax + 1; d-- > sg;) {  // \d* (or \d+) greedy
                 if ((int)(d - sg) < dmin) break;
-                const size_t w2max = run(s, d, ws_c);
-                for (size_t w2 = w2max; w2 > d; --w2) {  // \s+ greedy
-                    if (w2 < s.size() && tokc(s[w2])) {
-                        m.start = p;
-                        m.val0 = w;
-                        m.val1 = d;
-                        m.tok0 = w2;
-                        m.tok1 = run(s, w2 + 1, digit_c);
-                        return true;
-                    }
+                if (token_after(d, w2)) {
+                    m.start = p;
+                    m.val0 = w;
+                    m.val1 = d;
+                    m.tok0 = w2;
+                    m.tok1 = run(s, w2 + 1, digit_c);
+                    return true;
                 }
                 // the signs and digits shorter: the next item starts on a sign or digit
             }
         }
+    }
+    // \s+ shorter than the run (w in (p, wmax)): s[w] is whitespace, so the sign and
+    // digit items are empty (no match when digits are required), and the second \s+
+    // is the rest of the run -- the same candidate for every such w; greedy takes the
+    // longest first \s+, w = wmax - 1
+    if (dmin == 0 && wmax >= p + 2 && token_after(wmax - 1, w2)) {
+        m.start = p;
+        m.val0 = m.val1 = wmax - 1;
+        m.tok0 = w2;
+        m.tok1 = run(s, w2 + 1, digit_c);
+        return true;
     }
     return false;
 }

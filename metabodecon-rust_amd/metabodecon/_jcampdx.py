@@ -343,15 +343,18 @@ def read_jcampdx_arrays(path: str):
 def decode_native(data: str, factor: float, hint: int) -> np.ndarray | None:
     """The block through the engine library's decoder (mdg_jcampdx_decode: the same
     passes in C++, ~100x faster than the regex passes); None for the blocks it leaves
-    to decode_asdf / decode_affn (non-ASCII text, data the reference rejects). The
-    library is required (NativeLibraryError without it), like the rest of the reader's
-    consumers."""
+    to decode_asdf / decode_affn (non-ASCII text, data the reference rejects), and
+    when the engine library is missing or stale (reading a file needs no GPU: the regex
+    restatement then decodes it)."""
     from . import _native as nat
     import ctypes
     if not data.isascii():
         return None
     raw = data.encode("ascii")
-    L = nat.lib()
+    try:
+        L = nat.lib()
+    except (nat.NativeLibraryError, OSError):
+        return None
     n = ctypes.c_size_t(0)
     cap = max(1, int(hint))
     for _ in range(2):

@@ -141,3 +141,35 @@ def test_affn_floats_agree():
             assert b is not None and same(a, b), text
         else:
             assert b is None or "nan" in text.lower(), text
+
+
+@pytest.mark.timeout(60)
+def test_long_whitespace_runs_are_linear():
+    """the DIF/DUP token matcher was quadratic in the length of a whitespace
+    run that does not match. 400k blanks between values (and before a DIF token after
+    an empty value, the shorter-first-run candidate) decode in well under a second,
+    with the restatement's bits."""
+    import time
+    native("1 2")  # the library's first load is not the decoder's time
+    shapes = (lambda k: "1 2" + " " * k + "3 4", lambda k: "5" + " " * k + "J2 7",
+              lambda k: "@" + " " * k + "%1 " + " " * k + "A")
+    for make in shapes:
+        t = time.perf_counter()
+        native(make(400_000))
+        assert time.perf_counter() - t < 1.0, make(0)
+        # the same shape, short enough for the regex restatement (itself quadratic
+        # here: Python's backtracking), bit for bit
+        got, want = native(make(100)), python(make(100))
+        if isinstance(got, np.ndarray) and isinstance(want, np.ndarray):
+            assert np.array_equal(got, want)
+        else:
+            assert not isinstance(got, np.ndarray) and not isinstance(want, np.ndarray)
+
+
+def test_decode_native_declines_without_the_library(monkeypatch):
+    """reading a JCAMP-DX file needs no engine library; when it is missing
+    or stale the regex restatement decodes the block."""
+    def missing():
+        raise nat.NativeLibraryError("libmdgpu.so missing")
+    monkeypatch.setattr(nat, "lib", missing)
+    assert jdx.decode_native("1 2 3", 1.0, 3) is None
