@@ -13,6 +13,8 @@
 #   forcedist    bench.py under torch.distributed.run at world 1 (RCCL gather, configs_dist)
 #   prof         the round's profile set (tools/prof_all.sh)
 #   c4           configs[4] by lanes and hardware queues (bench.py --c4-only)
+#   roctx        per-stage kernel time from the engine's roctx ranges (B = 16, 1)
+#   pmcfit       PMC counter groups of the shipped small-batch fits (B = 16, 1)
 #   foldab       term-fold fits: pipelined fold asm against the compiler's schedule
 #   fitdiag      small-batch fit: PMC passes of tools/blood_trace.py 16 and the stamped
 #                tools/ubench/fit_diag over term-fold shapes (build fit_diag first)
@@ -107,6 +109,21 @@ for step in "$@"; do
         MDG_FITSUP=$fk timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/$tag -o run -- python3 tools/blood_trace.py $b > gpurun_out/run/$tag.log 2>&1 || { echo "STOP $tag"; exit 3; }
         f=$(find gpurun_out/$tag -name run_kernel_trace.csv | head -1)
         echo "== $tag $(python tools/blood_trace.py --summary "$f" | grep -E "fit|total" | awk '{s+=$4; n++} END {print n, s}')" | tee -a $log
+      done ;;
+    roctx)
+      # stage attribution from the engine's roctx ranges (no hipEvents in the stream):
+      # one blood call of 16 and of 1 spectra, kernel + HIP API + marker traces
+      for b in 16 1; do
+        tag=roctx_b$b
+        MDG_ROCTX=1 run trace_$tag 180 rocprofv3 --kernel-trace --hip-trace --marker-trace --output-format csv -d gpurun_out/$tag -o run -- python3 tools/blood_trace.py $b
+        run stages_$tag 60 python tools/roctx_stages.py gpurun_out/$tag --out gpurun_out/roctx_stages_b$b.json
+      done ;;
+    pmcfit)
+      # PMC passes of the shipped small-batch fits (twf1 at B = 16, tf12 at B = 1 in
+      # latency mode), summarised per batch (tools/pmc_groups.py)
+      for b in 16 1; do
+        run pmcfit_b$b 900 bash tools/pmc_fit.sh $b
+        run pmcgroups_b$b 60 python tools/pmc_groups.py gpurun_out/pmcfit_b$b --out gpurun_out/pmc_fit_b$b.json
       done ;;
     foldab)
       # the term-fold fits' fold wave: pipelined asm (fold_lds_row) against the compiler's

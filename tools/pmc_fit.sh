@@ -4,11 +4,12 @@
 # a kernel trace of the same command for the durations, then the stamped
 # microbenchmark tools/ubench/fit_diag (built on the CPU with -DMDG_DIAG).
 #   bash tools/pmc_fit.sh [B] [fit_diag args ...]
-# Outputs under gpurun_out/pmcfit/; summarise with tools/pmc_groups.py.
+# Outputs under gpurun_out/pmcfit_b<B>/ (PMCFIT_TAG overrides the suffix); summarise
+# with tools/pmc_groups.py.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 B=${1:-16}
-O=gpurun_out/pmcfit
+O=gpurun_out/pmcfit${PMCFIT_TAG:-_b$B}
 mkdir -p $O
 timeout -s KILL 60 rocprofv3 -L > $O/avail.txt 2>&1
 echo "list rc=$?"
@@ -32,7 +33,7 @@ for g in A L M; do
   [ $rc -eq 0 ] || exit $rc
 done
 shift
-if [ -x tools/ubench/fit_diag ]; then
+if [ $# -gt 0 ] && [ -x tools/ubench/fit_diag ]; then
   timeout -k 10 120 tools/ubench/fit_diag "$@" > $O/fit_diag.log 2>&1
   echo "fit_diag rc=$?"
 fi
