@@ -2509,103 +2509,6 @@ __device__ __forceinline__ const double* params_version(const Workspace& w, size
     return ((v & 1) ? w.params_alt : w.params) + 3 * base;
 }
 
-// The fold wave's pass over one chunk row of a term-fold fit (T[q][0 .. 2*NR) in
-// LDS, this lane's point): acc += t in peak order, the reference's left fold
-// (lorentzian.rs:606-611; fma(1.0, t, acc) rounds as acc + t). Software-pipelined
-// in one asm block: eight 16-byte LDS reads stay in flight (lgkmcnt(7) before each
-// pair of adds, the slot reloaded 8 reads ahead), so the dependent add chain runs
-// without waiting on LDS latency. The compiler's form issued 16 reads, then waited
-// for them while it added, and only then issued the next 16: 10.8 cycles per term
-// alone against ~4.3 for the add chain itself.
-#ifndef MDG_FOLD_ASM
-#define MDG_FOLD_ASM 1
-#endif
-template <int NR>
-__device__ __forceinline__ double fold_lds_row(double acc, const double* row) {
-    static_assert(NR % 8 == 0 && NR >= 16, "whole groups of eight 16-byte reads");
-    asm volatile(
-        "s_waitcnt lgkmcnt(0)\n"
-        "v_mov_b32 v52, %[addr]\n"
-        "v_mov_b64 v[54:55], %[acc]\n"
-        "ds_read_b128 v[20:23], v52 offset:0\n"
-        "ds_read_b128 v[24:27], v52 offset:16\n"
-        "ds_read_b128 v[28:31], v52 offset:32\n"
-        "ds_read_b128 v[32:35], v52 offset:48\n"
-        "ds_read_b128 v[36:39], v52 offset:64\n"
-        "ds_read_b128 v[40:43], v52 offset:80\n"
-        "ds_read_b128 v[44:47], v52 offset:96\n"
-        "ds_read_b128 v[48:51], v52 offset:112\n"
-        "s_mov_b32 s40, %[trips]\n"
-        "Lfoldlds%=:\n"
-        "s_waitcnt lgkmcnt(7)\n"
-        "v_fmac_f64 v[54:55], 1.0, v[20:21]\n"
-        "v_fmac_f64 v[54:55], 1.0, v[22:23]\n"
-        "ds_read_b128 v[20:23], v52 offset:128\n"
-        "s_waitcnt lgkmcnt(7)\n"
-        "v_fmac_f64 v[54:55], 1.0, v[24:25]\n"
-        "v_fmac_f64 v[54:55], 1.0, v[26:27]\n"
-        "ds_read_b128 v[24:27], v52 offset:144\n"
-        "s_waitcnt lgkmcnt(7)\n"
-        "v_fmac_f64 v[54:55], 1.0, v[28:29]\n"
-        "v_fmac_f64 v[54:55], 1.0, v[30:31]\n"
-        "ds_read_b128 v[28:31], v52 offset:160\n"
-        "s_waitcnt lgkmcnt(7)\n"
-        "v_fmac_f64 v[54:55], 1.0, v[32:33]\n"
-        "v_fmac_f64 v[54:55], 1.0, v[34:35]\n"
-        "ds_read_b128 v[32:35], v52 offset:176\n"
-        "s_waitcnt lgkmcnt(7)\n"
-        "v_fmac_f64 v[54:55], 1.0, v[36:37]\n"
-        "v_fmac_f64 v[54:55], 1.0, v[38:39]\n"
-        "ds_read_b128 v[36:39], v52 offset:192\n"
-        "s_waitcnt lgkmcnt(7)\n"
-        "v_fmac_f64 v[54:55], 1.0, v[40:41]\n"
-        "v_fmac_f64 v[54:55], 1.0, v[42:43]\n"
-        "ds_read_b128 v[40:43], v52 offset:208\n"
-        "s_waitcnt lgkmcnt(7)\n"
-        "v_fmac_f64 v[54:55], 1.0, v[44:45]\n"
-        "v_fmac_f64 v[54:55], 1.0, v[46:47]\n"
-        "ds_read_b128 v[44:47], v52 offset:224\n"
-        "s_waitcnt lgkmcnt(7)\n"
-        "v_fmac_f64 v[54:55], 1.0, v[48:49]\n"
-        "v_fmac_f64 v[54:55], 1.0, v[50:51]\n"
-        "ds_read_b128 v[48:51], v52 offset:240\n"
-        "v_add_u32 v52, 128, v52\n"
-        "s_sub_u32 s40, s40, 1\n"
-        "s_cmp_lg_u32 s40, 0\n"
-        "s_cbranch_scc1 Lfoldlds%=\n"
-        "s_waitcnt lgkmcnt(7)\n"
-        "v_fmac_f64 v[54:55], 1.0, v[20:21]\n"
-        "v_fmac_f64 v[54:55], 1.0, v[22:23]\n"
-        "s_waitcnt lgkmcnt(6)\n"
-        "v_fmac_f64 v[54:55], 1.0, v[24:25]\n"
-        "v_fmac_f64 v[54:55], 1.0, v[26:27]\n"
-        "s_waitcnt lgkmcnt(5)\n"
-        "v_fmac_f64 v[54:55], 1.0, v[28:29]\n"
-        "v_fmac_f64 v[54:55], 1.0, v[30:31]\n"
-        "s_waitcnt lgkmcnt(4)\n"
-        "v_fmac_f64 v[54:55], 1.0, v[32:33]\n"
-        "v_fmac_f64 v[54:55], 1.0, v[34:35]\n"
-        "s_waitcnt lgkmcnt(3)\n"
-        "v_fmac_f64 v[54:55], 1.0, v[36:37]\n"
-        "v_fmac_f64 v[54:55], 1.0, v[38:39]\n"
-        "s_waitcnt lgkmcnt(2)\n"
-        "v_fmac_f64 v[54:55], 1.0, v[40:41]\n"
-        "v_fmac_f64 v[54:55], 1.0, v[42:43]\n"
-        "s_waitcnt lgkmcnt(1)\n"
-        "v_fmac_f64 v[54:55], 1.0, v[44:45]\n"
-        "v_fmac_f64 v[54:55], 1.0, v[46:47]\n"
-        "s_waitcnt lgkmcnt(0)\n"
-        "v_fmac_f64 v[54:55], 1.0, v[48:49]\n"
-        "v_fmac_f64 v[54:55], 1.0, v[50:51]\n"
-        "v_mov_b64 %[acc], v[54:55]\n"
-        : [acc] "+v"(acc)
-        : [addr] "v"(lds_offset(row)), [trips] "s"(NR / 8 - 1)
-        : "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32",
-          "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45",
-          "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v54", "v55", "s40", "scc", "memory");
-    return acc;
-}
-
 template <bool FAST, int QT = kTfQ>
 __device__ __forceinline__ void fit_tf_body(const Workspace& w, int s, int P, int it, double* T) {
     constexpr int Q = QT, EW = kTfEW, J = 64 * EW;
@@ -2672,16 +2575,15 @@ __device__ __forceinline__ void fit_tf_body(const Workspace& w, int s, int P, in
                 const double2* row = (const double2*)(T + (c & 1) * Q * RS + q * RS);
                 const int cn = min(J, P - c * J);
                 if (cn == J) {
-#if MDG_FOLD_ASM
-                    acc = fold_lds_row<J / 2>(acc, (const double*)row);
-#else  // the compiler's schedule (A/B builds only: make ... HIPFLAGS+=-DMDG_FOLD_ASM=0)
+                    // (round 5: a software-pipelined asm form, eight 16-byte reads kept in
+                    // flight, was slower than this schedule -- ten tf12 launches 113 against
+                    // 95 us at B = 1, twf1 385 against 370 at B = 16)
 #pragma unroll 16
                     for (int k = 0; k < J / 2; ++k) {
                         const double2 v = row[k];
                         acc = __builtin_fma(v.x, one, acc);
                         acc = __builtin_fma(v.y, one, acc);
                     }
-#endif
                 } else {
                     const double* r1 = (const double*)row;
                     for (int k = 0; k < cn; ++k) acc = __builtin_fma(r1[k], one, acc);
@@ -2774,6 +2676,14 @@ __device__ __forceinline__ void fit_tw_body(const Workspace& w, int s, int P, in
     DIAG_DECL
 #ifdef MDG_DIAG
     _d_acc[7] = _d_t;
+    // where the wave runs (fit_diag's placement analysis): HW_ID (wave / SIMD / CU / SE /
+    // workgroup slot) and XCC_ID, one record per (block, wave) after the KSTAMP slots
+    if (lane == 0 && g_diag) {
+        const unsigned hw = __builtin_amdgcn_s_getreg((4) | (0 << 6) | ((32 - 1) << 11));
+        const unsigned xcc = __builtin_amdgcn_s_getreg((20) | (0 << 6) | ((16 - 1) << 11));
+        const size_t r = kDiagStampBase + 4096 + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + wv;
+        g_diag[r] = (long long)(((unsigned long long)xcc << 32) | hw) | (1ll << 62);
+    }
 #endif
     for (int tile = tile0; tile < tiles; tile += tstep) {
         const int p0 = tile * QQ;
@@ -2858,16 +2768,15 @@ __device__ __forceinline__ void fit_tw_body(const Workspace& w, int s, int P, in
                 const double2* row = (const double2*)(T + (SH::SB ? 0 : (c & 1) * QQ * RS) + q * RS);
                 const int cn = min(J, P - c * J);
                 if (cn == J) {
-#if MDG_FOLD_ASM
-                    acc = fold_lds_row<J / 2>(acc, (const double*)row);
-#else  // the compiler's schedule (A/B builds only: make ... HIPFLAGS+=-DMDG_FOLD_ASM=0)
+                    // (round 5: a software-pipelined asm form, eight 16-byte reads kept in
+                    // flight, was slower than this schedule -- ten tf12 launches 113 against
+                    // 95 us at B = 1, twf1 385 against 370 at B = 16)
 #pragma unroll 16
                     for (int k = 0; k < J / 2; ++k) {
                         const double2 v = row[k];
                         acc = __builtin_fma(v.x, one, acc);
                         acc = __builtin_fma(v.y, one, acc);
                     }
-#endif
                 } else {
                     const double* r1 = (const double*)row;
                     for (int k = 0; k < cn; ++k) acc = __builtin_fma(r1[k], one, acc);

@@ -36,3 +36,29 @@ def test_gen_chain_asm_help_writes_nothing():
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_chain_asm.py"), "--help"],
                    capture_output=True, timeout=60, check=True)
     assert os.stat(inc).st_mtime_ns == before
+
+
+UBENCH = sorted(glob.glob(os.path.join(ROOT, "tools", "ubench", "*.hip")))
+HIPCC = "/opt/rocm/bin/hipcc"
+HIP_FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off", "-fno-fast-math",
+             "-DMDG_DIAG", "-fsyntax-only"]
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
+@pytest.mark.parametrize("path", UBENCH, ids=os.path.basename)
+def test_ubench_source_compiles_against_the_engine(path):
+    """The microbenchmarks include the engine's kernel source: an API change there
+    (round 5: the launchers take the context's EngineSwitches) must not leave them
+    stale."""
+    r = subprocess.run([HIPCC] + HIP_FLAGS + [path], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
+def test_ubench_check_has_power(tmp_path):
+    bad = tmp_path / "stale.hip"
+    bad.write_text('#include "%s"\nusing namespace mdg;\n'
+                   'void f(const BatchArgs& a, const Workspace& w) { launch_fit_sup(a, w, 24, 0, 0); }\n'
+                   % os.path.join(ROOT, "metabodecon-rust_amd", "csrc", "mdg_kernels.hip"))
+    r = subprocess.run([HIPCC] + HIP_FLAGS + [str(bad)], capture_output=True, text=True, timeout=600)
+    assert r.returncode != 0

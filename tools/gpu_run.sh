@@ -15,7 +15,6 @@
 #   c4           configs[4] by lanes and hardware queues (bench.py --c4-only)
 #   roctx        per-stage kernel time from the engine's roctx ranges (B = 16, 1)
 #   pmcfit       PMC counter groups of the shipped small-batch fits (B = 16, 1)
-#   foldab       term-fold fits: pipelined fold asm against the compiler's schedule
 #   fitdiag      small-batch fit: PMC passes of tools/blood_trace.py 16 and the stamped
 #                tools/ubench/fit_diag over term-fold shapes (build fit_diag first)
 #   twfdiag      the batch-wide tile-list fit (k_fit_sup_twf) against the (G, B) grids
@@ -125,17 +124,6 @@ for step in "$@"; do
         run pmcfit_b$b 900 bash tools/pmc_fit.sh $b
         run pmcgroups_b$b 60 python tools/pmc_groups.py gpurun_out/pmcfit_b$b --out gpurun_out/pmc_fit_b$b.json
       done ;;
-    foldab)
-      # the term-fold fits' fold wave: pipelined asm (fold_lds_row) against the compiler's
-      # schedule (tools/ubench/libmdgpu_fold0.so, built with -DMDG_FOLD_ASM=0), two rounds,
-      # ten fit launches of one blood call at B = 1 (tf12) and B = 16 (twf1, tf)
-      for r in 1 2; do for lib in new fold0; do for bk in 1:tf12 16:twf1 16:tw7 4:tf; do
-        b=${bk%%:*}; fk=${bk#*:}; tag=foldab_${lib}_b${b}_${fk}_r$r
-        if [ $lib = fold0 ]; then envs="MDGPU_LIB=tools/ubench/libmdgpu_fold0.so MDGPU_ALLOW_STALE=1"; else envs=""; fi
-        env $envs MDG_FITSUP=$fk timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/$tag -o run -- python3 tools/blood_trace.py $b > gpurun_out/run/$tag.log 2>&1 || { echo "STOP $tag"; exit 3; }
-        f=$(find gpurun_out/$tag -name run_kernel_trace.csv | head -1)
-        echo "== $tag $(python tools/blood_trace.py --summary "$f" | grep -E "fit" | awk '{s+=$4; n++} END {print n, s}')" | tee -a $log
-      done; done; done ;;
     msediag)
       # the MSE kernel at small batches: tile workgroups per spectrum and points per thread
       for v in "" "MDG_MSE_PARTS=128" "MDG_MSE_PARTS=64" "MDG_MSE_NPT=4" "MDG_MSE_NPT=4 MDG_MSE_PARTS=64"; do

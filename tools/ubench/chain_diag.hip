@@ -29,7 +29,7 @@ int main(int argc, char** argv) {
         (void)hipMemset(diag, 0, (size_t)B * P * 32 * 8);
         hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
         (void)hipEventRecord(e0);
-        launch_smooth(a, w, P, WS, 0);
+        launch_smooth(a, w, P, WS, EngineSwitches{}, 0);
         (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
         float ms; (void)hipEventElapsedTime(&ms, e0, e1);
         printf("B=%d smooth %.3f ms (%s)\n", B, ms, hipGetErrorString(hipGetLastError()));

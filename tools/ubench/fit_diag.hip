@@ -10,6 +10,8 @@
 #include "../../metabodecon-rust_amd/csrc/mdg_kernels.hip"
 #include <algorithm>
 #include <cstdio>
+#include <cstring>
+#include <map>
 #include <vector>
 using namespace mdg;
 
@@ -68,7 +70,8 @@ int main(int argc, char** argv) {
     (void)hipMalloc(&sel, 4 * B); (void)hipMemcpy(sel, selv.data(), 4 * B, hipMemcpyHostToDevice);
     (void)hipMalloc(&xok, 4 * B); (void)hipMemcpy(xok, ones.data(), 4 * B, hipMemcpyHostToDevice);
     (void)hipMalloc(&unsafe, 16 * B); (void)hipMemset(unsafe, 0, 16 * B);
-    const size_t nd = kDiagStampBase + 1024;  // every DIAG_FLUSH record the guard allows
+    // every DIAG_FLUSH record the guard allows, the KSTAMP slots and the placement records
+    const size_t nd = kDiagStampBase + 4096 + ((size_t)1 << 20);
     (void)hipMalloc(&diag, nd * 8);
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_diag), &diag, sizeof(diag));
     BatchArgs a{}; a.B = B; a.N = N;
@@ -100,8 +103,12 @@ int main(int argc, char** argv) {
         int sq = 0, spb = 0, sps = 0, sg = 0;
         const bool sbuf = ks[0] == 'S';
         const bool shape = (ks[0] == 's' || sbuf) && sscanf(k + 1, "%d.%d.%d@%d", &sq, &spb, &sps, &sg) == 4;
-        setenv("MDG_FITSUP", shape ? "tw7" : ks.substr(0, ks.find('/')).c_str(), 1);
-        w.params_alt = fit_sup_fused(a) ? d_alt : nullptr;
+        // the engine's switches (normally read when a context is created): the kernel to run
+        EngineSwitches sw;
+        std::strncpy(sw.fitsup, shape ? "tw7" : ks.substr(0, ks.find('/')).c_str(), sizeof(sw.fitsup) - 1);
+        if (const char* tg = std::getenv("MDG_TW_G")) sw.tw_g = std::max(1, std::atoi(tg));
+        a.latency = 1;
+        w.params_alt = fit_sup_fused(a, sw) ? d_alt : nullptr;
         float best = 1e30f;
         int shape_ew = 0;
         for (int rep = 0; rep < 6; ++rep) {
@@ -109,7 +116,7 @@ int main(int argc, char** argv) {
             hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
             (void)hipEventRecord(e0);
             if (shape) shape_ew = launch_shape(sq, spb, sps, a, w, sg, sbuf);
-            else launch_fit_sup(a, w, 24, 0, 0);
+            else launch_fit_sup(a, w, 24, 0, sw, 0);
             (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
             float ms; (void)hipEventElapsedTime(&ms, e0, e1);
             if (rep > 0 && ms < best) best = ms;
@@ -123,6 +130,34 @@ int main(int argc, char** argv) {
         printf("%-6s B=%d P=%d  %.2f us/launch  %.3f T evals/s  same_as_dpp=%d\n", k, B, P, best * 1e3,
                evals / (best * 1e-3) / 1e12, (int)same);
         if (shape && !shape_ew) { printf("%s: unknown shape\n", k); continue; }
+        {
+            // placement of the fold waves (wave EW of each block): HW_ID fields (gfx9:
+            // wave 3:0, SIMD 5:4, CU 11:8, SH 12, SE 15:13, TG slot 19:16) and XCC_ID;
+            // blocks sharing a CU whose fold waves share a SIMD compete for its issue
+            std::vector<long long> d(nd);
+            (void)hipMemcpy(d.data(), diag, nd * 8, hipMemcpyDeviceToHost);
+            const int EWp = shape ? shape_ew : (ks.rfind("tf", 0) == 0 ? kTfEW : 7);
+            std::map<long long, std::vector<int>> cu_fold;  // CU key -> fold SIMDs of its blocks
+            int simd_hist[4] = {0, 0, 0, 0}, recs = 0;
+            for (size_t b = 0; b < (1u << 16); ++b) {
+                const long long v = d[kDiagStampBase + 4096 + b * 16 + EWp];
+                if (!(v >> 62)) continue;
+                const unsigned hw = (unsigned)v, xcc = (unsigned)((v >> 32) & 0xffff);
+                const int simd = (hw >> 4) & 3;
+                const long long cu = ((long long)xcc << 16) | (((hw >> 13) & 7) << 8) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 15);
+                cu_fold[cu].push_back(simd);
+                simd_hist[simd] += 1;
+                ++recs;
+            }
+            int shared = 0, pairs = 0;
+            for (auto& kv : cu_fold) {
+                const auto& v = kv.second;
+                for (size_t i = 0; i < v.size(); ++i)
+                    for (size_t j = i + 1; j < v.size(); ++j) { ++pairs; shared += v[i] == v[j]; }
+            }
+            printf("   fold waves: %d blocks on %zu CUs, SIMD histogram %d/%d/%d/%d, same-CU pairs %d, sharing a SIMD %d\n",
+                   recs, cu_fold.size(), simd_hist[0], simd_hist[1], simd_hist[2], simd_hist[3], pairs, shared);
+        }
         if (ks.rfind("tw7", 0) == 0 || shape) {
             // tw: waves 0..EW-1 evaluators, wave EW the fold wave; grid (g, B); a block
             // with blockIdx.x >= tiles has no work. Slots: see fit_tw_body.

@@ -19,7 +19,7 @@ int main(int argc, char** argv) {
     for (int rep = 0; rep < 2; ++rep) {
         hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
         (void)hipEventRecord(e0);
-        launch_smooth(a, w, P, 3, 0);
+        launch_smooth(a, w, P, 3, EngineSwitches{}, 0);
         (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
         float ms; (void)hipEventElapsedTime(&ms, e0, e1);
         printf("B=%d smooth %.3f ms\n", B, ms);
