@@ -641,6 +641,17 @@ def lane_contexts(device: int | None, n: int) -> list[Context]:
         return lanes[:n]
 
 
+def release_context(device: int | None = None) -> None:
+    """Destroy the shared context of `device` (all devices when None): its idle stream
+    holds a hardware queue. It is re-created by the next call that needs it."""
+    with _ctx_lock:
+        for d in ([device] if device is not None else list(_ctx)):
+            c = _ctx.pop(d, None)
+            if c is not None:
+                with c.lock:
+                    c.close()
+
+
 def release_lanes(device: int | None = None) -> None:
     """Destroy the lane contexts of `device` (all devices when None): their idle
     streams still hold hardware queues, and with 16 of them alive a single-stream
