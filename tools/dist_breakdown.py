@@ -49,6 +49,17 @@ def main():
         return 1e3 * float(np.median(ts))
     res = dec._run(block)
     from metabodecon._deconvolution import Deconvolution
+
+    def bench_form():  # bench.py dist_c4's loop: barriers on both sides of the call
+        ts = []
+        par_deconvolute_spectra(dec, spectra)
+        for _ in range(args.reps):
+            dist.barrier()
+            t = time.perf_counter()
+            par_deconvolute_spectra(dec, spectra)
+            dist.barrier()
+            ts.append(time.perf_counter() - t)
+        return 1e3 * float(np.median(ts))
     gloo = dist.new_group(backend="gloo")
     hh = torch.zeros(2, dtype=torch.int64)
     hp = torch.zeros(2, dtype=torch.int64).pin_memory()
@@ -139,6 +150,7 @@ def main():
         "stamped_ms": dict(zip(["set_device", "run_block", "gather_host", "results"], parts.tolist())),
         "world": world, "rank": rank, "spectra_per_rank": len(block),
         "par_deconvolute_spectra_dist_ms": med(lambda: par_deconvolute_spectra(dec, spectra)),
+        "bench_form_ms": bench_form(),
         "block_host_path_ms": med(lambda: dec._run(block)),
         "gather_host_ms": med(lambda: gather_host(res, len(spectra))),
         "barrier_ms": med(lambda: dist.barrier()),
