@@ -845,6 +845,7 @@ EngineSwitches mdg::read_engine_switches() {
                : sm == "generic" ? EngineSwitches::SM_GENERIC
                                  : EngineSwitches::SM_OTHER;
     w.chain_excl = str("MDG_CHAIN_EXCL").substr(0, 1) != "0";
+    w.chain_l2ahead = std::max(0, num("MDG_CHAIN_L2AHEAD", 0));
     const std::string pk = str("MDG_PEAKS");
     w.peaks = pk.empty() ? 0 : pk == "fine" ? 1 : 2;
     const std::string f = str("MDG_FITSUP");

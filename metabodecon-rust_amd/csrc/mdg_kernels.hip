@@ -653,7 +653,14 @@ constexpr int kChainScBatch = MDG_CHAIN_SCB;  // output blocks per scaler batch
 constexpr int kChainG = MDG_CHAIN_G;      // ticks per stored checkpoint in steady blocks
 static_assert(kChainG % 8 == 0 && kChainCB % kChainG == 0, "checkpoint groups tile the blocks");
 constexpr int kChainPrefetch = MDG_CHAIN_PF;  // input blocks touched into the scalar cache ahead
-constexpr int kChainL2Ahead = 64;        // pass-0 input blocks pulled into L2 ahead
+// Input blocks each chain pulls into L2 ahead of itself: at most 64, and about 1 MB
+// of pulled lines per XCD in all (launch_chain). At B = 256 an XCD runs 96 chains, and
+// 64 blocks (48 KB) ahead each was 4.6 MB against a 4 MB L2: lines were evicted before
+// the chain and its scalers read them, and the scalers read them again from memory
+// (round 5, queue 256 x 2: smoother reads 7.4 -> 4.3 MB per spectrum, headline
+// 15.9k -> 16.5k spectra/s with 16 or 8 blocks; 32: 16.2k)
+constexpr int kChainL2Ahead = 64;
+constexpr int kChainL2Bytes = 1 << 20;
 constexpr unsigned kChainSpins = 1u << 22;
 // largest chain grid (workgroups, padded to 8 spectra x passes) launched with
 // whole-CU workgroups: 8 spectra x 3 passes at the defaults, 232 CUs left free
@@ -867,7 +874,8 @@ __device__ __forceinline__ void chain_decode(const BatchArgs& a, const Workspace
 // k_fit_sup_tf launch lasts as long as its slowest workgroup).
 template <int WS, bool EXCL>
 __global__ __launch_bounds__(64 * (2 + kChainScalers)) void k_smooth_chain(BatchArgs a, Workspace w, int P,
-                                                                            int fused_prep, int ndec) {
+                                                                            int fused_prep, int ndec,
+                                                                            int l2ahead) {
     if constexpr (EXCL) {
         asm volatile("v_mov_b32 v255, 0" ::: "v255");
         asm volatile("v_accvgpr_write_b32 a255, 0" ::: "a255");
@@ -1023,10 +1031,10 @@ __global__ __launch_bounds__(64 * (2 + kChainScalers)) void k_smooth_chain(Batch
             }
             const int rd = CTL_LD(raw_done);
             // learn what the upstream pass has published (pass 0: everything)
-            if (p > 0 && up < min(nIB, rd + kChainL2Ahead))
+            if (p > 0 && up < min(nIB, rd + l2ahead))
                 up = __hip_atomic_load(const_cast<int32_t*>(up_flag), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
-            if (p == 0 && ndec > 0 && up < min(nIB, rd + kChainL2Ahead)) {
+            if (p == 0 && ndec > 0 && up < min(nIB, rd + l2ahead)) {
                 // lane c reads chunk c's flag; the decoded prefix is the run of set
                 // flags from chunk 0 (kDecChunks == 64: one per lane)
                 static_assert(kDecChunks == 64, "one flag per feeder lane");
@@ -1053,7 +1061,7 @@ __global__ __launch_bounds__(64 * (2 + kChainScalers)) void k_smooth_chain(Batch
             // pull published full input blocks into L2 (16 per wait), so the
             // scalar-cache touches below hit L2 instead of HBM / the MALL
             // (every pass: without it, 11.7 / 12.3 / 12.5 cycles per tick, passes 0..2)
-            const int l2lim = min(min(N / CB, up), rd + kChainL2Ahead);
+            const int l2lim = min(min(N / CB, up), rd + l2ahead);
             bool prog = false;
             if (l2lim - l2 >= 16 || (l2lim > l2 && (l2lim == N / CB || l2 < pf + 4))) {
                 const int cnt = min(16, l2lim - l2);
@@ -3709,12 +3717,17 @@ static const char* launch_chain(const BatchArgs& a, const Workspace& w, int iter
     // decoders up to 4 spectra, 64 beyond (chain_decode; a multiple of 8 keeps the
     // chain workgroups' XCD mapping)
     const int ndec = a.dec_rows && fused_prep ? (a.B <= 4 ? 32 : 64) : 0;
+    // input blocks pulled into L2 ahead of each chain (MDG_CHAIN_L2AHEAD: measurements)
+    const int per_xcd = (int)cdiv((int)grid, 8);
+    const int l2ahead = sw.chain_l2ahead > 0
+                            ? sw.chain_l2ahead
+                            : std::max(8, std::min(kChainL2Ahead, kChainL2Bytes / (per_xcd * kChainCB * 8)));
     if (excl) {
         launch_k((k_smooth_chain<WS, true>), dim3(grid + ndec), dim3(64 * (2 + kChainScalers)), 0, st,
-                           a, w, iters, fused_prep, ndec);
+                           a, w, iters, fused_prep, ndec, l2ahead);
     } else {
         launch_k((k_smooth_chain<WS, false>), dim3(grid + ndec), dim3(64 * (2 + kChainScalers)), 0, st,
-                           a, w, iters, fused_prep, ndec);
+                           a, w, iters, fused_prep, ndec, l2ahead);
     }
     static const char* names[2][9] = {
         {"", "", "k_smooth_chain<2, false>", "k_smooth_chain<3, false>", "k_smooth_chain<4, false>",

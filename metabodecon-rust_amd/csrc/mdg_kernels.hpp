@@ -124,6 +124,7 @@ struct EngineSwitches {
     enum { SM_DEFAULT = 0, SM_CHAIN, SM_PIPE, SM_GENERIC, SM_OTHER };
     int smooth = SM_DEFAULT;     // MDG_SMOOTH = chain | pipe | generic (other values: the generic kernel)
     int chain_excl = 1;          // MDG_CHAIN_EXCL=0: never whole-CU chain workgroups
+    int chain_l2ahead = 0;       // MDG_CHAIN_L2AHEAD: blocks each chain pulls into L2 ahead (0: by grid)
     int peaks = 0;               // MDG_PEAKS: 0 by batch size, 1 fine, 2 coarse (any other value)
     char fitsup[8] = {};         // MDG_FITSUP: a shipped fit kernel's name ("": by batch size)
     int tw_g = 0;                // MDG_TW_G: term-fold workgroups (0: the kernel's default)
