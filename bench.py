@@ -1078,11 +1078,15 @@ def dist_c4(args, nat, torch, dist, dev, rank, world):
         res = par_deconvolute_spectra(dec, spectra)
     ts = []
     for _ in range(30):
+        # a set's time is the slowest rank's, from a common start to that rank's return
+        # (rank dst returns once every rank's block has reached it); the closing
+        # barrier only re-aligns the ranks for the next set
         dist.barrier()
         t0 = time.perf_counter()
         res = par_deconvolute_spectra(dec, spectra)
+        t = time.perf_counter() - t0
         dist.barrier()
-        ts.append(max_over_ranks(dist, torch, dev, [time.perf_counter() - t0])[0])
+        ts.append(max_over_ranks(dist, torch, dev, [t])[0])
     ok = 0
     for k, d in enumerate(res or []):  # the results reach rank 0 (the collecting caller)
         gd = np.load(os.path.join(GOLDEN, f"blood_{k + 1:02d}.npz"))
