@@ -3238,11 +3238,17 @@ __device__ __forceinline__ void mse_publish_fold(const BatchArgs& a, const Works
 //   - near ones, |z_j - t| <= kLocR r: summed directly per point (quad_term);
 //   - far ones: their sum is a power series in u = (x - t) / r,
 //       sum_j a_j / (x - z_j) = -sum_k [sum_j a_j w_j (r w_j)^k] u^k,  w_j = 1 / (z_j - t),
-//     |u| <= 1 and |r w_j| < 1 / kLocR, so kLocP = 20 terms leave ~5^-20 of each
+//     |u| <= 1 and |r w_j| < 1 / kLocR, so kLocP = 30 terms leave ~3^-30 of each
 //     far term; only the imaginary parts are needed (u is real).
-// Per point that is ~20 Horner steps plus ~1.5% of the Lorentzians directly, and
-// per tile one pass over the Lorentzians (~5 instructions per term and power)
-// instead of 256 x P divisions. Measured against a long-double direct sum
+// Per point that is ~30 Horner steps plus a few % of the Lorentzians directly, and
+// per tile one pass over the Lorentzians (~3 instructions per term and power)
+// instead of 256 x P divisions. The radius trades the two: the near terms cost ~25
+// issue slots per four per point, the far ones ~3 per power per tile, so a smaller
+// radius with more powers wins while the near list dominates (round 5, queue 256 x 2,
+// MSE us per spectrum: R = 5 / 20 powers 3.54-3.57, R = 4 / 30 3.48, R = 3 / 30
+// 3.08-3.09, R = 2.5 / 40 3.76-3.82 -- 204 VGPRs, occupancy 2; the MSE's max
+// relative error against the oracle 1.34e-14 in every form, tools/mse_error.py).
+// MDG_LOC_R / MDG_LOC_P (build-time; PK a multiple of 10) reproduce the sweep. Measured against a long-double direct sum
 // (tools/mse_local_error.py): the MSE within a few 1e-15 relative on the
 // synthetic and blood spectra, the order of the direct f64 sum's own error; the
 // tests hold it to MSE_RTOL = 1e-12 like every MSE kernel. Every reduction has a
@@ -3250,8 +3256,14 @@ __device__ __forceinline__ void mse_publish_fold(const BatchArgs& a, const Works
 // (x_ok, unsafe_kept) and tiles with more near Lorentzians than the list holds
 // (kLocNear) sum every term directly.
 // ----------------------------------------------------------------------------------
-constexpr int kLocP = 20;         // expansion terms
-constexpr double kLocR = 5.0;     // far: |z - t| > kLocR * r
+#ifndef MDG_LOC_P
+#define MDG_LOC_P 30
+#endif
+#ifndef MDG_LOC_R
+#define MDG_LOC_R 3.0
+#endif
+constexpr int kLocP = MDG_LOC_P;      // expansion terms
+constexpr double kLocR = MDG_LOC_R;   // far: |z - t| > kLocR * r
 constexpr int kLocNear = 512;     // near Lorentzians kept per tile (LDS)
 constexpr int kLocTP = 256;       // points per tile (one per thread)
 
@@ -3276,8 +3288,8 @@ __device__ __forceinline__ double sup_retained_direct(double x, const_f64_ptr pr
 // NPT points per thread: a tile of kLocTP * NPT points shares one coefficient pass
 template <int NPT>
 __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int nparts, int near_cap) {
-    constexpr int BS = 256, NW = BS / 64, TP = kLocTP * NPT, PK = kLocP, PH = PK / 2;
-    static_assert(kLocTP == BS && PK % 2 == 0 && PH * 16 <= BS, "tile shape");
+    constexpr int BS = 256, NW = BS / 64, TP = kLocTP * NPT, PK = kLocP, PH = 10, NH = PK / PH;
+    static_assert(kLocTP == BS && PK % PH == 0 && PH * 16 <= BS, "tile shape");
     const int s = blockIdx.x % a.B, part = blockIdx.x / a.B;
     // LDS: the coefficient reduction (PH x BS) and, after the tile loop, the
     // partials of the final fold share one buffer
@@ -3446,7 +3458,7 @@ __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int
             // sum the coefficients over the block, PH at a time: 16 threads per
             // coefficient, 16 values each, then a butterfly over the 16 lanes
 #pragma unroll
-            for (int hf = 0; hf < 2; ++hf) {
+            for (int hf = 0; hf < NH; ++hf) {
 #pragma unroll
                 for (int k = 0; k < PH; ++k) red[k * BS + tid] = L[hf * PH + k];
                 __syncthreads();

@@ -6,7 +6,8 @@ numpy, against a long-double direct sum of the Lorentzians.
 For each golden case (oracle parameters from tests/golden/expected/*.npz) and
 for the synthetic configs[1] spectrum it prints the largest relative error of
 the superposition over the signal region and the relative error of the MSE,
-for the kernel's tile shape (256 points, R = 5, 20 terms) and neighbours.
+for the kernel's tile shapes (512 and 1024 points, R = 3, 30 terms since round 5;
+R = 5, 20 terms before) and neighbours.
 """
 import os
 import sys
@@ -89,7 +90,7 @@ def main():
     from cases import load_case, synth_spectrum
     import oracle
     shapes = [(256, 5.0, 20), (256, 5.0, 20, True), (512, 5.0, 20), (512, 5.0, 20, True),
-              (512, 4.0, 24, True)]
+              (512, 4.0, 24, True), (512, 3.0, 30, True), (1024, 3.0, 30, True)]
     names = names_arg or ["blood_01", "blood_05", "blood_09", "sim_01", "synth"]
     for nm in names:
         if nm == "synth":
