@@ -112,6 +112,14 @@ pub mod ffi {
             b: f64,
             n_out: *mut usize,
         ) -> c_int;
+        pub fn mdg_jcampdx_decode(
+            data: *const c_char,
+            len: usize,
+            factor: f64,
+            out: *mut f64,
+            cap: usize,
+            n_out: *mut usize,
+        ) -> c_int;
         pub fn mdg_device_count(count: *mut c_int) -> c_int;
         pub fn mdg_host_alloc(device: c_int, bytes: usize, out: *mut *mut c_void) -> c_int;
         pub fn mdg_host_free(p: *mut c_void) -> c_int;
@@ -785,6 +793,41 @@ pub fn gpu_superposition_vec<L: AsRef<Lorentzian>>(
         )
     })?;
     Ok(out)
+}
+
+/// One JCAMP-DX data block (the text after `##XYDATA=` / `##DATA TABLE=`, trimmed)
+/// decoded natively into intensities times `factor`, as `JcampDx::decode_asdf` /
+/// `decode_affn` do (spectrum/formats/jcampdx.rs:892-1091). `None` when the native
+/// decoder leaves the block to the reader's own decode (non-ASCII text, or data the
+/// reference rejects, which the reader's decode then reports with its own error).
+/// Host only: no GPU is touched.
+pub fn jcampdx_decode(block: &str, factor: f64) -> Result<Option<Vec<f64>>> {
+    // a first guess; DUP counts can expand a short token into many values, so a block
+    // that needs more reports its count with MDG_CAPACITY (nothing written) and is
+    // decoded again into a buffer of that size
+    let mut out = vec![0f64; block.len() + 1];
+    loop {
+        let mut n = 0usize;
+        let rc = unsafe {
+            ffi::mdg_jcampdx_decode(
+                block.as_ptr() as *const c_char,
+                block.len(),
+                factor,
+                out.as_mut_ptr(),
+                out.len(),
+                &mut n,
+            )
+        };
+        match rc {
+            ffi::MDG_INVALID_ARGUMENT => return Ok(None),
+            ffi::MDG_CAPACITY if n > out.len() => out.resize(n, 0.0),
+            _ => {
+                check(rc)?;
+                out.truncate(n);
+                return Ok(Some(out));
+            }
+        }
+    }
 }
 
 /// ABI version of the loaded library (mdgpu.h `MDG_ABI_VERSION`).
