@@ -722,13 +722,14 @@ def headline_queue(args, nat, torch, dist, dev, rank, world):
             roof["rocprof_source"] = rc["source"]
     if roof and qprof.get(roof["stage"], (0, 0))[1]:
         ms, cnt = qprof[roof["stage"]]
+        tsum = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_q{B}_trace_summary.json")))
         roof["in_queue"] = {
             "avg_launch_ms": ms / cnt, "launches": cnt,
             "note": ("the same kernel timed inside the running queue (hipEvents on both lanes' "
                      "streams, batches overlapping): a launch shares the GPU with the other "
-                     "lane's work, so it lasts longer than alone; the mean over the timed "
-                     f"batches of a rocprofv3 trace (profiles/r03_q{B}_trace_summary.json) is "
-                     "this figure")}
+                     "lane's work, so it lasts longer than alone"
+                     + (f"; the mean over the timed batches of a rocprofv3 trace "
+                        f"({os.path.relpath(tsum[-1], ROOT)}) is this figure" if tsum else ""))}
     L = sbi_len(14.8, -20.0 / (n - 1.0), SB[0], SB[1])
     iters = settings.fit_iterations
     flops = float(np.mean([pipeline_work(p, int(k), L, iters) for p, k in zip(P_sel, counts)]))

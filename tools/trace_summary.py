@@ -3,8 +3,10 @@
     python tools/trace_summary.py <run_kernel_trace.csv> --batches N --max-batch B [--out f.json]
 
 The timed region of the bench is the last N batches the queue launched: from the
-start of the N-th last k_queue_gather to the end of the last k_queue_scatter (the
-profiled pass after it runs without the queue). Over that window it reports:
+start of the N-th last batch's first kernel to the end of the last k_queue_scatter
+(the profiled pass after it runs without the queue). A batch's first kernel is its
+k_queue_gather when the queue copies rows (distinct axes), else its smoother launch
+(since round 5 the queue reads shared-axis rows in place). Over that window it reports:
 - per kernel: launches, total / mean duration, share of the summed kernel time,
   kernel time per spectrum;
 - the window's spectra/s under the tracer;
@@ -41,10 +43,12 @@ def main():
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]),
                          r["Queue_Id"]))
     rows.sort()
-    gathers = [r for r in rows if r[2] == "k_queue_gather"]
     scatters = [r for r in rows if r[2] == "k_queue_scatter"]
-    t0 = gathers[-a.batches][0]
     t1 = max(r[1] for r in scatters)
+    starts = [r for r in rows if r[2] == "k_queue_gather" and r[0] < t1]
+    if not starts:
+        starts = [r for r in rows if r[2].startswith("k_smooth") and r[0] < t1]
+    t0 = starts[-a.batches][0]
     win = [r for r in rows if r[0] >= t0 and r[1] <= t1]
     span = (t1 - t0) * 1e-9
     spectra = a.batches * a.max_batch
