@@ -861,6 +861,7 @@ EngineSwitches mdg::read_engine_switches() {
     w.gfit = std::max(1, num("MDG_GFIT", 24));
     w.mse_npt = str("MDG_MSE_NPT").empty() ? 0 : (num("MDG_MSE_NPT", 2) == 4 ? 4 : 2);
     w.mse_parts = str("MDG_MSE_PARTS").empty() ? 0 : std::max(1, num("MDG_MSE_PARTS", 1));
+    w.mse_pk = str("MDG_MSE_PK").empty() ? 0 : (num("MDG_MSE_PK", 20) == 30 ? 30 : 20);
     w.mse_nearcap = str("MDG_MSE_NEARCAP").empty() ? -1 : std::max(0, num("MDG_MSE_NEARCAP", 0));
     w.prep_separate = str("MDG_PREP") == "separate";
     w.graphs = str("MDG_GRAPHS") == "1";

@@ -2492,6 +2492,25 @@ __device__ __forceinline__ bool fit_done(const Workspace& w, int s, int it) {
     return w.fit_iters_s && it >= w.fit_iters_s[s];
 }
 
+// What a term-fold launch needs of spectrum s before its first parameter load, read
+// together: one memory round trip. Written as branches (status, then fit_iters_s,
+// then sel_count, then x_ok and unsafe) they were a chain of dependent loads, each
+// waited for before the next was issued (the ISA of k_fit_sup_tf: six waits before
+// the first parameter load), which a B = 1 launch of a few microseconds pays in full.
+struct FitHead {
+    bool live;  // neither failed nor past its own iteration count
+    bool fast;  // x_ok and no parameter outside the fast ranges (slot it % 3)
+    int P;
+};
+__device__ __forceinline__ FitHead fit_head(const Workspace& w, int s, int it) {
+    const int st = w.status[s], P = w.sel_count[s], xo = w.x_ok[s], un = w.unsafe[4 * s + it % 3];
+    const int fi = w.fit_iters_s ? w.fit_iters_s[s] : 0x7fffffff;
+    // every value used here, so the compiler cannot sink a load behind the branch on
+    // another (it did: status first, the rest after its wait)
+    asm volatile("" ::"v"(st), "v"(P), "v"(xo), "v"(un), "v"(fi));
+    return {st == 0 && it < fi, xo != 0 && un == 0, P};
+}
+
 // K6e  fit superposition + stencil update, term-fold form (small batches). A
 // workgroup owns Q = 24 reduced points = 8 peaks of one spectrum. EW evaluator
 // waves compute the terms of a chunk of J = 64*EW peaks (lane = peak, parameters
@@ -2630,11 +2649,11 @@ template <int Q>
 __global__ __launch_bounds__(64 * (kTfEW + 1)) void k_fit_sup_tf(BatchArgs a, Workspace w, int it) {
     __shared__ __attribute__((aligned(16))) double T[tf_lds<Q>()];
     const int s = blockIdx.y;
-    if (w.status[s] || fit_done(w, s, it)) return;
-    const int P = w.sel_count[s];
+    const FitHead h = fit_head(w, s, it);
+    if (!h.live) return;
     if (blockIdx.x == 0 && threadIdx.x == 0) w.unsafe[4 * s + (it + 2) % 3] = 0;
-    if (w.x_ok[s] && w.unsafe[4 * s + it % 3] == 0) fit_tf_body<true, Q>(w, s, P, it, T);
-    else fit_tf_body<false, Q>(w, s, P, it, T);
+    if (h.fast) fit_tf_body<true, Q>(w, s, h.P, it, T);
+    else fit_tf_body<false, Q>(w, s, h.P, it, T);
 }
 
 // K6h  term-fold fit, wide tiles ("tw"): Q = 63 points (21 peaks) per workgroup
@@ -2829,11 +2848,11 @@ template <class SH>
 __global__ __launch_bounds__(64 * (SH::EW + 1)) void k_fit_sup_tw(BatchArgs a, Workspace w, int it) {
     __shared__ __attribute__((aligned(16))) double T[SH::LDS];
     const int s = blockIdx.y;
-    if (w.status[s] || fit_done(w, s, it)) return;
-    const int P = w.sel_count[s];
+    const FitHead h = fit_head(w, s, it);
+    if (!h.live) return;
     if (blockIdx.x == 0 && threadIdx.x == 0) w.unsafe[4 * s + (it + 2) % 3] = 0;
-    if (w.x_ok[s] && w.unsafe[4 * s + it % 3] == 0) fit_tw_body<true, SH>(w, s, P, it, T, blockIdx.x, gridDim.x);
-    else fit_tw_body<false, SH>(w, s, P, it, T, blockIdx.x, gridDim.x);
+    if (h.fast) fit_tw_body<true, SH>(w, s, h.P, it, T, blockIdx.x, gridDim.x);
+    else fit_tw_body<false, SH>(w, s, h.P, it, T, blockIdx.x, gridDim.x);
 }
 
 #ifdef MDG_DIAG
@@ -2921,11 +2940,14 @@ __global__ __launch_bounds__(64 * (SH::EW + 1)) void k_fit_sup_twf(BatchArgs a, 
     if (threadIdx.x < 64) {
         const int s = threadIdx.x;
         int tiles = 0, P = 0, fast = 0;
-        if (s < a.B && !w.status[s] && !fit_done(w, s, it)) {
-            P = w.sel_count[s];
-            tiles = (3 * P + QQ - 1) / QQ;
-            fast = w.x_ok[s] && w.unsafe[4 * s + it % 3] == 0;
-            if (blockIdx.x == 0) w.unsafe[4 * s + (it + 2) % 3] = 0;
+        if (s < a.B) {
+            const FitHead h = fit_head(w, s, it);
+            if (h.live) {
+                P = h.P;
+                tiles = (3 * P + QQ - 1) / QQ;
+                fast = h.fast;
+                if (blockIdx.x == 0) w.unsafe[4 * s + (it + 2) % 3] = 0;
+            }
         }
         int x = tiles;
 #pragma unroll
@@ -3235,35 +3257,35 @@ __device__ __forceinline__ void mse_publish_fold(const BatchArgs& a, const Works
 // complex pole z_j = maxp_j + i s_j, each term is Im[a_j / (x - z_j)] with
 // a_j = sfhw_j / s_j. A tile of 256 consecutive points (centre t, half range r)
 // splits the Lorentzians into
-//   - near ones, |z_j - t| <= kLocR r: summed directly per point (quad_term);
+//   - near ones, |z_j - t| <= R r: summed directly per point (quad_term);
 //   - far ones: their sum is a power series in u = (x - t) / r,
 //       sum_j a_j / (x - z_j) = -sum_k [sum_j a_j w_j (r w_j)^k] u^k,  w_j = 1 / (z_j - t),
-//     |u| <= 1 and |r w_j| < 1 / kLocR, so kLocP = 30 terms leave ~3^-30 of each
-//     far term; only the imaginary parts are needed (u is real).
-// Per point that is ~30 Horner steps plus a few % of the Lorentzians directly, and
+//     |u| <= 1 and |r w_j| < 1 / R, so PK terms leave ~R^-PK of each far term
+//     (R = 3 with 30 terms, or R = 5 with 20); only the imaginary parts are needed
+//     (u is real).
+// Per point that is PK Horner steps plus a few % of the Lorentzians directly, and
 // per tile one pass over the Lorentzians (~3 instructions per term and power)
 // instead of 256 x P divisions. The radius trades the two: the near terms cost ~25
-// issue slots per four per point, the far ones ~3 per power per tile, so a smaller
-// radius with more powers wins while the near list dominates (round 5, queue 256 x 2,
-// MSE us per spectrum: R = 5 / 20 powers 3.54-3.57, R = 4 / 30 3.48, R = 3 / 30
-// 3.08-3.09, R = 2.5 / 40 3.76-3.82 -- 204 VGPRs, occupancy 2; the MSE's max
-// relative error against the oracle 1.34e-14 in every form, tools/mse_error.py).
-// MDG_LOC_R / MDG_LOC_P (build-time; PK a multiple of 10) reproduce the sweep. Measured against a long-double direct sum
+// issue slots per four per point, the far ones ~3 per power per tile, so at
+// throughput (large batches) a smaller radius with more powers wins while the near
+// list dominates; a small batch waits on a tile's latency instead, which the longer
+// far-field recurrence adds to. Round 5, MSE us per spectrum in the queue (256 x 2):
+// R = 5 / 20 powers 3.54-3.57, R = 4 / 30 3.48, R = 3 / 30 3.08-3.09, R = 2.5 / 40
+// 3.76-3.82 (204 VGPRs, occupancy 2); blood at B = 16, us per launch: 56.2 (R = 5)
+// against 62.7 (R = 3). So PK = 30 from B = kMsePk30MinB and for the 2-point tiles
+// of B < 8, 20 in between (launch_mse; MDG_MSE_PK overrides). Measured against a
+// long-double direct sum
 // (tools/mse_local_error.py): the MSE within a few 1e-15 relative on the
-// synthetic and blood spectra, the order of the direct f64 sum's own error; the
+// synthetic and blood spectra, the order of the direct f64 sum's own error; against
+// the oracle 1.34e-14 at most for either order (tools/mse_error.py); the
 // tests hold it to MSE_RTOL = 1e-12 like every MSE kernel. Every reduction has a
 // fixed order, so results are deterministic. Spectra outside the fast ranges
 // (x_ok, unsafe_kept) and tiles with more near Lorentzians than the list holds
 // (kLocNear) sum every term directly.
 // ----------------------------------------------------------------------------------
-#ifndef MDG_LOC_P
-#define MDG_LOC_P 30
-#endif
-#ifndef MDG_LOC_R
-#define MDG_LOC_R 3.0
-#endif
-constexpr int kLocP = MDG_LOC_P;      // expansion terms
-constexpr double kLocR = MDG_LOC_R;   // far: |z - t| > kLocR * r
+constexpr int kMsePk30MinB = 32;  // PK = 30 (R = 3) from this batch size (and below 8)
+template <int PK>
+constexpr double loc_radius() { return PK >= 30 ? 3.0 : 5.0; }  // far: |z - t| > R * r
 constexpr int kLocNear = 512;     // near Lorentzians kept per tile (LDS)
 constexpr int kLocTP = 256;       // points per tile (one per thread)
 
@@ -3286,9 +3308,10 @@ __device__ __forceinline__ double sup_retained_direct(double x, const_f64_ptr pr
 }
 
 // NPT points per thread: a tile of kLocTP * NPT points shares one coefficient pass
-template <int NPT>
+template <int NPT, int PK>
 __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int nparts, int near_cap) {
-    constexpr int BS = 256, NW = BS / 64, TP = kLocTP * NPT, PK = kLocP, PH = 10, NH = PK / PH;
+    constexpr int BS = 256, NW = BS / 64, TP = kLocTP * NPT, PH = 10, NH = PK / PH;
+    constexpr double kLocR = loc_radius<PK>();
     static_assert(kLocTP == BS && PK % PH == 0 && PH * 16 <= BS, "tile shape");
     const int s = blockIdx.x % a.B, part = blockIdx.x / a.B;
     // LDS: the coefficient reduction (PH x BS) and, after the tile loop, the
@@ -3301,11 +3324,16 @@ __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int
     __shared__ int wcnt[NW];
     __shared__ int lds_i[NW + 1];
     const int tid = threadIdx.x, wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    // the spectrum's scalars, loaded together (one memory round trip; behind the
+    // branches below they were a chain of dependent loads, as in fit_head)
+    const int st = w.status[s], panic = w.mse_panic[s], P = w.sel_count[s], nig = w.n_ig[s],
+              xok = w.x_ok[s], fis = w.fit_iters_s ? w.fit_iters_s[s] : 0x7fffffff;
+    asm volatile("" ::"v"(st), "v"(panic), "v"(P), "v"(nig), "v"(xok), "v"(fis));  // (fit_head)
     // k_retain's work, fused: one extra workgroup per spectrum (part == nparts)
     // reports a failed spectrum or compacts its retained Lorentzians into the
     // caller's rows, beside the tiles; the last tile workgroup reports the MSE
     if (part == nparts) {
-        if (w.status[s]) {
+        if (st) {
             if (tid == 0) {
                 a.out_count[s] = 0;
                 a.out_mse[s] = 0.0;
@@ -3316,20 +3344,19 @@ __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int
         retain_body<BS>(a, w, s, lds_i);
         return;
     }
-    if (w.status[s]) return;
-    if (w.mse_panic[s]) {
+    if (st) return;
+    if (panic) {
         if (part == 0) mse_panic_out(a, s);
         return;
     }
     KSTAMP(30);
-    const int P = w.sel_count[s];
     const size_t pbase = (size_t)s * w.capD;
-    const double* __restrict__ prmv = final_params(w, s, pbase);
+    // final_params with the preloaded iteration count
+    const double* __restrict__ prmv = params_version(w, pbase, w.params_alt ? min(fis, w.fit_iters) : 0);
     const const_f64_ptr prm = (const_f64_ptr)prmv;
     const double* x = a.x + (size_t)s * a.x_stride;
     const double* y = y_row(a, s);
-    const int nig = w.n_ig[s];
-    const int64_t total = mse_len(w, s);
+    const int64_t total = w.ig_cum[(size_t)s * (w.ig_cap + 2) + nig + 1];  // mse_len
     // every workgroup counts the retained Lorentzians (the last one reports the
     // capacity status) and checks their fast ranges (k_retain's unsafe_kept)
     int cnt = 0, uns = 0;
@@ -3342,7 +3369,7 @@ __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int
     }
     int kept_n;
     (void)block_exclusive_scan<BS>(cnt, lds_i, &kept_n);
-    const bool fast = w.x_ok[s] && !__syncthreads_or(uns);
+    const bool fast = xok && !__syncthreads_or(uns);
     KSTAMP(31);
     double acc = 0.0;
     for (int64_t v0 = (int64_t)part * TP; v0 < total; v0 += (int64_t)nparts * TP) {
@@ -3953,12 +3980,25 @@ const char* launch_mse(const BatchArgs& a, const Workspace& w, int nparts, const
     // own direct fallback for crowded tiles
     const int cap = sw.mse_nearcap >= 0 ? std::min(kLocNear, sw.mse_nearcap) : kLocNear;
     // nparts tile workgroups per spectrum plus its retain workgroup
-    if (mse_npt(a, sw) == 4) {
-        launch_k(k_mse_local<4>, dim3((nparts + 1) * a.B), dim3(256), 0, st, a, w, nparts, cap);
-        return "k_mse_local<4>";
+    const dim3 g((nparts + 1) * a.B);
+    const int npt = mse_npt(a, sw);
+    // 20 powers only for the 4-point tiles of small batches (blood, us per launch:
+    // B = 16 56.6 against 63.3 with 30; B = 1, 2-point tiles: 17.3 against 16.8)
+    const bool pk30 = sw.mse_pk ? sw.mse_pk == 30 : (a.B >= kMsePk30MinB || npt == 2);
+    if (npt == 4) {
+        if (pk30) {
+            launch_k(k_mse_local<4, 30>, g, dim3(256), 0, st, a, w, nparts, cap);
+            return "k_mse_local<4, 30>";
+        }
+        launch_k(k_mse_local<4, 20>, g, dim3(256), 0, st, a, w, nparts, cap);
+        return "k_mse_local<4, 20>";
     }
-    launch_k(k_mse_local<kLocNPT>, dim3((nparts + 1) * a.B), dim3(256), 0, st, a, w, nparts, cap);
-    return "k_mse_local<2>";
+    if (pk30) {
+        launch_k(k_mse_local<kLocNPT, 30>, g, dim3(256), 0, st, a, w, nparts, cap);
+        return "k_mse_local<2, 30>";
+    }
+    launch_k(k_mse_local<kLocNPT, 20>, g, dim3(256), 0, st, a, w, nparts, cap);
+    return "k_mse_local<2, 20>";
 }
 void launch_mse_exact(const double* sup, const double* y, int64_t n, const Workspace& w,
                       double* scratch, double* out, hipStream_t st) {

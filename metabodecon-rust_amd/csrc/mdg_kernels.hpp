@@ -131,6 +131,7 @@ struct EngineSwitches {
     int gfit = 24;               // MDG_GFIT: k_fit_sup workgroups per spectrum
     int mse_npt = 0;             // MDG_MSE_NPT = 2 | 4 (0: by batch size)
     int mse_parts = 0;           // MDG_MSE_PARTS (0: by shape)
+    int mse_pk = 0;              // MDG_MSE_PK = 20 | 30 expansion powers (0: by batch size)
     int mse_nearcap = -1;        // MDG_MSE_NEARCAP (-1: kLocNear)
     int prep_separate = 0;      // MDG_PREP=separate
     int graphs = 0;              // MDG_GRAPHS=1

@@ -591,14 +591,17 @@ def test_fit_superposition_kernels_batch(ctx, path, monkeypatch, engine_env):
         assert abs(mse[s] - o.mse) <= MSE_RTOL * abs(o.mse), s
 
 
+@pytest.mark.parametrize("pk", ["20", "30"])
 @pytest.mark.parametrize("npt", ["2", "4"])
 @pytest.mark.parametrize("near_cap", [None, "8", "0"])
-def test_mse_cases(ctx, near_cap, npt, monkeypatch, engine_env):
-    """The MSE (k_mse_local, 2 and 4 points per thread) against the oracle: ignore
-    regions (two in one spectrum), a short signal region (sim) and a batch whose
-    spectra differ in peak count; also with a tiny near-list capacity (crowded tiles
-    take the kernel's direct sum) and none at all (every tile direct)."""
+def test_mse_cases(ctx, near_cap, npt, pk, monkeypatch, engine_env):
+    """The MSE (k_mse_local, 2 and 4 points per thread, 20 powers at radius 5 and 30
+    at radius 3) against the oracle: ignore regions (two in one spectrum), a short
+    signal region (sim) and a batch whose spectra differ in peak count; also with a
+    tiny near-list capacity (crowded tiles take the kernel's direct sum) and none at
+    all (every tile direct)."""
     engine_env.setenv("MDG_MSE_NPT", npt)
+    engine_env.setenv("MDG_MSE_PK", pk)
     if near_cap is not None:
         engine_env.setenv("MDG_MSE_NEARCAP", near_cap)
     for name in ["blood_01_water", "blood_02_two_regions_increasing", "sim_05", "synth_128k_2k_s0"]:

@@ -1,8 +1,9 @@
 """Relative deviation of the engine's MSE from the oracle's left-fold MSE
 (compute_mse, deconvoluter.rs:828-862) over all golden cases and two more synthetic
 spectra (GPU box), for each MSE form the library ships: the local expansions with 2
-and with 4 points per thread (MDG_MSE_NPT; the default picks by batch size) and the
-exact-order option (MDG_OPTION_EXACT_MSE, expected 0). Prints the max |rel| per form.
+and with 4 points per thread (MDG_MSE_NPT) and 20 or 30 powers (MDG_MSE_PK; the
+defaults pick both by batch size) and the exact-order option (MDG_OPTION_EXACT_MSE,
+expected 0). Prints the max |rel| per form.
 
     python tools/mse_error.py
 """
@@ -32,9 +33,11 @@ def main():
         x, y, _ = synth_spectrum(seed)
         o = oracle.deconvolute(x, y, (11.8, -2.2), threads=16)
         cases.append((f"synth_{seed}", x, y, (11.8, -2.2), oracle.default_settings(), (), o.mse))
-    for form, npt, exact in (("local, 2 points per thread", "2", False),
-                             ("local, 4 points per thread", "4", False), ("exact order", "2", True)):
+    forms = [(f"local, {npt} points per thread, {pk} powers", npt, pk, False)
+             for npt in ("2", "4") for pk in ("20", "30")] + [("exact order", "2", "20", True)]
+    for form, npt, pk, exact in forms:
         os.environ["MDG_MSE_NPT"] = npt
+        os.environ["MDG_MSE_PK"] = pk
         ctx.reload_switches()  # the engine reads its switches per context, not per call
         worst, wname = 0.0, None
         for name, x, y, sb, st, ign, ref in cases:
