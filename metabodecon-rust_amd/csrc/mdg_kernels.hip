@@ -1295,7 +1295,9 @@ __global__ void k_flags(BatchArgs a, Workspace w) {
     // next run (whatever this spectrum's status)
     if (blockIdx.x == 0 && (int)threadIdx.x < w.chain_P)
         w.chain_flags[((size_t)s * w.chain_P + threadIdx.x) * 32] = 0;
-    if (w.status[s]) return;
+    // the status is loaded with the row (one memory round trip, not two); the row
+    // of a failed spectrum is read and ignored
+    const int st = w.status[s];
     const int N = a.N;
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     const double* sm = w.smooth_ptr + (size_t)s * w.smooth_stride;
@@ -1306,6 +1308,7 @@ __global__ void k_flags(BatchArgs a, Workspace w) {
         fr = d0 > dm && (d0 >= dp || (d0 < 0. && dp >= 0.));
         fl = d0 > dp && (d0 >= dm || (d0 < 0. && dm >= 0.));
     }
+    if (st) return;
     // k_peaks' per-chunk slots start empty
     if (k < peak_slots(w.W)) ((unsigned long long*)w.peak_cnt)[(size_t)s * peak_slots(w.W) + k] = 0;
     const uint64_t bc = __ballot(fc), br = __ballot(fr), bl = __ballot(fl);
@@ -1483,7 +1486,7 @@ __global__ __launch_bounds__(BS) void k_peaks(BatchArgs a, Workspace w, int dete
     constexpr int PER = STAGE ? (SN + BS - 1) / BS : 1;
     __shared__ double ys[SN];
     __shared__ int pk[3 * PCAP];
-    if (w.status[s]) return;  // uniform per spectrum: no chunk waits for a returned one
+    const int st = w.status[s];  // (checked after the row's loads are issued)
     KSTAMP(0);
     const double* __restrict__ sm = w.smooth_ptr + (size_t)s * w.smooth_stride;
     const int lo = chunk * SPAN - MARG;
@@ -1492,6 +1495,7 @@ __global__ __launch_bounds__(BS) void k_peaks(BatchArgs a, Workspace w, int dete
 #pragma unroll
         for (int u = 0; u < PER; ++u) stv[u] = sm[min(max(lo + u * BS + (int)threadIdx.x, 0), a.N - 1)];
     }
+    if (st) return;  // uniform per spectrum: no chunk waits for a returned one
     const int nch = (w.W + WORDS - 1) / WORDS;
     unsigned long long* slot = (unsigned long long*)w.peak_cnt + (size_t)s * peak_slots(w.W);
     // four threads per mask word, each the peaks centred in 16 of its bits: thread
@@ -2137,8 +2141,11 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
     __shared__ long long lds_l[BS / 64 + 1];
     __shared__ double thr_sh;
     __shared__ WinLds wl;
-    if (w.status[s]) return;
-    const int P = w.det_count[s];
+    // the spectrum's scalars in one memory round trip (as fit_head)
+    const int st = w.status[s], P = w.det_count[s];
+    const int64_t sbi0 = w.sbi[2 * s], sbi1 = w.sbi[2 * s + 1];
+    asm volatile("" ::"v"(st), "v"(P), "v"(sbi0), "v"(sbi1));
+    if (st) return;
     if (P == 0) {  // peaks.len() - 1 underflows in peak_region_boundaries
         if (threadIdx.x == 0) w.status[s] = MDG_REFERENCE_PANIC;
         return;
@@ -2147,7 +2154,6 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
     const int* pl = w.det_l + base;
     const int* pc = w.det_c + base;
     const int* pr = w.det_r + base;
-    const int64_t sbi0 = w.sbi[2 * s], sbi1 = w.sbi[2 * s + 1];
     double* scores = w.scores + base;
     KSTAMP(10);
     // #(center <= sbi0) and #(center <= sbi1) over the ascending centers (scores:
