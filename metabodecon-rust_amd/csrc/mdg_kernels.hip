@@ -2144,7 +2144,7 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
     // the spectrum's scalars in one memory round trip (as fit_head)
     const int st = w.status[s], P = w.det_count[s];
     const int64_t sbi0 = w.sbi[2 * s], sbi1 = w.sbi[2 * s + 1];
-    asm volatile("" ::"v"(st), "v"(P), "v"(sbi0), "v"(sbi1));
+    asm volatile("" ::"s"(st), "s"(P), "s"(sbi0), "s"(sbi1));
     if (st) return;
     if (P == 0) {  // peaks.len() - 1 underflows in peak_region_boundaries
         if (threadIdx.x == 0) w.status[s] = MDG_REFERENCE_PANIC;
@@ -3276,10 +3276,11 @@ __device__ __forceinline__ void mse_publish_fold(const BatchArgs& a, const Works
 // throughput (large batches) a smaller radius with more powers wins while the near
 // list dominates; a small batch waits on a tile's latency instead, which the longer
 // far-field recurrence adds to. Round 5, MSE us per spectrum in the queue (256 x 2):
-// R = 5 / 20 powers 3.54-3.57, R = 4 / 30 3.48, R = 3 / 30 3.08-3.09, R = 2.5 / 40
-// 3.76-3.82 (204 VGPRs, occupancy 2); blood at B = 16, us per launch: 56.2 (R = 5)
-// against 62.7 (R = 3). So PK = 30 from B = kMsePk30MinB and for the 2-point tiles
-// of B < 8, 20 in between (launch_mse; MDG_MSE_PK overrides). Measured against a
+// R = 5 / 20 powers 3.52-3.57, R = 4 / 30 3.48, R = 3 / 30 3.07-3.12, R = 2.5 / 40
+// 3.76-3.82 (204 VGPRs, occupancy 2); blood, us per launch: B = 16 53.4 against 56.8,
+// B = 1 17.2 either way. So PK = 30 (MDG_MSE_PK=20 selects the round-4 form). The
+// <4, 30> form needs 168 VGPRs, the most that keeps 3 waves per SIMD: at 188 (an asm
+// use-point on its head loads) it ran 3.7 us per spectrum. Measured against a
 // long-double direct sum
 // (tools/mse_local_error.py): the MSE within a few 1e-15 relative on the
 // synthetic and blood spectra, the order of the direct f64 sum's own error; against
@@ -3289,7 +3290,6 @@ __device__ __forceinline__ void mse_publish_fold(const BatchArgs& a, const Works
 // (x_ok, unsafe_kept) and tiles with more near Lorentzians than the list holds
 // (kLocNear) sum every term directly.
 // ----------------------------------------------------------------------------------
-constexpr int kMsePk30MinB = 32;  // PK = 30 (R = 3) from this batch size (and below 8)
 template <int PK>
 constexpr double loc_radius() { return PK >= 30 ? 3.0 : 5.0; }  // far: |z - t| > R * r
 constexpr int kLocNear = 512;     // near Lorentzians kept per tile (LDS)
@@ -3334,7 +3334,8 @@ __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int
     // branches below they were a chain of dependent loads, as in fit_head)
     const int st = w.status[s], panic = w.mse_panic[s], P = w.sel_count[s], nig = w.n_ig[s],
               xok = w.x_ok[s], fis = w.fit_iters_s ? w.fit_iters_s[s] : 0x7fffffff;
-    asm volatile("" ::"v"(st), "v"(panic), "v"(P), "v"(nig), "v"(xok), "v"(fis));  // (fit_head)
+    // (no asm use-point as in fit_head: pinning them cost the <4, 30> form 20 VGPRs and
+    // so a wave per SIMD; the compiler issues most of them together anyway)
     // k_retain's work, fused: one extra workgroup per spectrum (part == nparts)
     // reports a failed spectrum or compacts its retained Lorentzians into the
     // caller's rows, beside the tiles; the last tile workgroup reports the MSE
@@ -3988,9 +3989,7 @@ const char* launch_mse(const BatchArgs& a, const Workspace& w, int nparts, const
     // nparts tile workgroups per spectrum plus its retain workgroup
     const dim3 g((nparts + 1) * a.B);
     const int npt = mse_npt(a, sw);
-    // 20 powers only for the 4-point tiles of small batches (blood, us per launch:
-    // B = 16 56.6 against 63.3 with 30; B = 1, 2-point tiles: 17.3 against 16.8)
-    const bool pk30 = sw.mse_pk ? sw.mse_pk == 30 : (a.B >= kMsePk30MinB || npt == 2);
+    const bool pk30 = sw.mse_pk != 20;  // 30 powers unless MDG_MSE_PK=20 (round 5)
     if (npt == 4) {
         if (pk30) {
             launch_k(k_mse_local<4, 30>, g, dim3(256), 0, st, a, w, nparts, cap);

@@ -186,3 +186,37 @@ def test_acquire_checker_flags_a_missing_acquire():
     assert _acquire_after_poll(missing) == ["s_ff1_i32_b64 s8, s[8:9]"]
     touch = poll + ["\ts_load_dwordx16 s[40:55], s[56:57], 0x0"]
     assert _acquire_after_poll(touch)
+
+
+# Occupancy the hot kernels were measured at (waves per SIMD, from the compiler's
+# kernel info): a register-pressure regression costs a wave per SIMD silently -- round
+# 5's k_mse_local<4, 30> went from 168 to 188 VGPRs (3 -> 2 waves) through one asm
+# use-point and ran 20% slower.
+MIN_OCCUPANCY = {
+    r"^_ZN3mdg9k_fit_supENS_9BatchArgsENS_9WorkspaceEi$": 7,
+    r"^_ZN3mdg11k_mse_localILi4ELi30EE": 3,
+    r"^_ZN3mdg11k_mse_localILi2ELi30EE": 3,
+    r"^_ZN3mdg12k_fit_sup_tfILi12EE": 4,
+    r"^_ZN3mdg13k_fit_sup_twfINS_7TwShapeILi63ELi1ELi7ELb0EEEEE": 4,
+}
+
+
+def _kernel_info(isa):
+    info, name = {}, None
+    for line in isa:
+        m = re.match(r"^(_ZN3mdg\w+):\s*(;.*)?$", line)
+        if m:
+            name = m.group(1)
+        m = re.match(r"^; Occupancy: (\d+)", line.strip()) or re.match(r"^\s*; Occupancy: (\d+)", line)
+        if m and name:
+            info.setdefault(name, int(m.group(1)))
+    return info
+
+
+def test_hot_kernels_keep_their_occupancy(isa):
+    info = _kernel_info(isa)
+    for pat, lo in MIN_OCCUPANCY.items():
+        hits = {n: o for n, o in info.items() if re.match(pat, n)}
+        assert hits, pat
+        for n, o in hits.items():
+            assert o >= lo, (n, o, lo)
