@@ -213,6 +213,8 @@ def gather_host(local: Sequence[Result], n_total: int, group=None, dst=0, error:
     import torch
     import torch.distributed as dist
     world, rank = dist.get_world_size(group), dist.get_rank(group)
+    if n_total == 0:  # the same on every rank: nothing to agree on or exchange
+        return None, ([] if dst is None or rank == dst else None)
     nccl = dist.get_backend(group) == "nccl"
     key = _key("exchange", None, torch.cuda.current_device() if nccl else "cpu", group)
     ex = _BUFS.get(key)

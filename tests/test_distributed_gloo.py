@@ -257,6 +257,9 @@ def _par_worker(rank, world, port, q, mode):
                 q.put((rank, "no error"))
             except Exception as e:  # every rank raises; none waits in a collective
                 q.put((rank, type(e).__name__))
+        elif mode == "empty":  # an empty set: the reference returns an empty Vec
+            res = par_deconvolute_spectra(_OracleDeconvoluter(), [])
+            q.put((rank, None if res is None else len(res)))
         elif mode == "subgroup":
             # dst is a rank of the group; the group excludes global rank 0
             sub = dist.new_group(ranks=list(range(1, world)))
@@ -306,6 +309,14 @@ def test_par_deconvolute_spectra_host_exchange(world):
     assert len(got[0]) == 7
     for (p, m), (wp, wm) in zip(got[0], want):
         assert np.array_equal(np.array(p).reshape(-1, 3), wp) and m == wm
+
+
+@pytest.mark.timeout(300)
+def test_par_deconvolute_spectra_empty_set():
+    """No spectra: rank 0 gets an empty list, the others None, and no collective runs
+    (every rank sees the same empty input)."""
+    got = _spawn(2, "empty")
+    assert got[0] == 0 and got[1] is None, got
 
 
 @pytest.mark.timeout(300)
