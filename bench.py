@@ -93,15 +93,20 @@ def parse(argv=None):
                          "many hardware queues round-robin; <= 32). 0: queue mode leaves the "
                          "environment as it is (HIP's default is 4; the queue needs one per "
                          "lane), stream mode sets 32")
-    ap.add_argument("--n", type=int, default=131072)
+    ap.add_argument("--n", "--points", dest="n", type=int, default=131072,
+                    help="points per spectrum (--points when launched through --gpus N: "
+                         "torchrun's parser takes --n for an ambiguous prefix of its own options)")
     ap.add_argument("--peaks", type=int, default=2048)
     ap.add_argument("--hw-scale", type=float, default=1.0, help="half-width scale (configs[3]: 2)")
     ap.add_argument("--cap", type=int, default=4096)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = len(sched_getaffinity)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-reps", type=int, default=3,
+                    help="multi-rank runs: reps of the rank-0 CPU baseline (N = 1: 5)")
     ap.add_argument("--no-configs", action="store_true", help="headline only")
-    ap.add_argument("--configs", default="0,1h,2,3,4",
-                    help="secondary configs to measure (1h: configs[1] from page-locked host rows)")
+    ap.add_argument("--configs", default="0,1h,2,3,4,h",
+                    help="secondary configs to measure (1h: configs[1] from page-locked host rows; "
+                         "h: the reference's own benchmark harness, sim spectra)")
     ap.add_argument("--no-profile", action="store_true", help="no per-stage HIP events")
     ap.add_argument("--copy-io", action="store_true",
                     help="stage each step's spectrum and results through the context's own rows")
@@ -118,6 +123,9 @@ def parse(argv=None):
     ap.add_argument("--c4-only", action="store_true",
                     help="measure configs[4] only and print its JSON block (bench.py runs itself "
                          "this way under GPU_MAX_HW_QUEUES=32 for the second environment)")
+    ap.add_argument("--harness-only", action="store_true",
+                    help="measure the reference's benches/deconvoluter.rs sim functions only and "
+                         "print their JSON block (bench.py runs itself this way)")
     ap.add_argument("--c0-only", action="store_true",
                     help="measure configs[0] only and print its JSON block (bench.py runs itself "
                          "this way: a fresh process, as a user's single-spectrum caller runs it)")
@@ -139,7 +147,9 @@ def spawn_ranks(args) -> int:
     the GPU) and return its exit status."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
-           f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+           f"--master-port={_free_port()}", os.path.abspath(__file__)] + \
+        ["--points" if a == "--n" else "--points=" + a[4:] if a.startswith("--n=") else a
+         for a in sys.argv[1:]]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     return subprocess.run(cmd, env=env).returncode
@@ -186,9 +196,10 @@ def host_threads(args):
     return (min(aff, quota) if quota else aff), aff, quota
 
 
-def median_rate(fn, units, reps=CPU_REPS):
+def median_rate(fn, units, reps=CPU_REPS, warm=True):
     """units / median wall time of `reps` runs of fn() (one untimed warm-up)."""
-    fn()
+    if warm:
+        fn()
     ts = []
     for _ in range(reps):
         t = time.perf_counter()
@@ -585,14 +596,29 @@ def headline_queue(args, nat, torch, dist, dev, rank, world):
     submit_all(max(WS, args.max_batch * args.lanes), 0)  # warm-up: every lane sizes its rows
     q.synchronize()
     torch.cuda.synchronize()
+    gstat = {}
     if dist_on:  # RCCL connections are set up by the first collectives, not in the timing
         from metabodecon.distributed import gather_packed
 
         def gather():
             # the (status, count, mse) records and the Lorentzian tables (padded to the
             # largest count of any rank) to rank 0, the caller that receives the
-            # results: distributed.gather_packed, one packed gather over RCCL/xGMI
-            return gather_packed(status, cnt, mse, out, world * KS, dst=0)[1]
+            # results: distributed.gather_packed, one packed gather over RCCL/xGMI per
+            # step's S spectra, so rank 0's receive buffer holds world x S records
+            # (world x 512 x ~50 KB at 8 ranks), not the whole run's world x K x S
+            # (3.6 GB at 8 ranks and 20 steps); statuses checked
+            # per step. Returns True when every gathered status is 0 (rank 0).
+            ok, nbytes, width = True, 0, 0
+            for k in range(K):
+                sl = slice(k * S, (k + 1) * S)
+                g = gather_packed(status[sl], cnt[sl], mse[sl], out[sl], world * S, dst=0)[1]
+                if g is not None:
+                    ok = ok and int(g[0].abs().max()) == 0 and g[0].shape[0] == world * S
+                    width = max(width, int(g[3].shape[1]))
+                    nbytes += S * (3 + 3 * int(g[3].shape[1])) * 8
+            gstat.update(bytes_per_rank=nbytes, table_width=width,
+                         recv_buffer_bytes=world * S * (3 + 3 * width) * 8, collectives=2 * K)
+            return ok
         gather()
         torch.cuda.synchronize()
     status.fill_(-1)
@@ -638,7 +664,7 @@ def headline_queue(args, nat, torch, dist, dev, rank, world):
         g = gather()
         torch.cuda.synchronize()
         dist.barrier()
-        assert g is None or (int(g[0].abs().max()) == 0 and g[0].shape[0] == world * KS)
+        assert g
     elapsed = time.perf_counter() - t0
     gather_s = elapsed - t_compute
     if dist_on:
@@ -742,6 +768,7 @@ def headline_queue(args, nat, torch, dist, dev, rank, world):
         "selected_peaks": P_sel[:4], "kept_peaks": [int(c) for c in cnt_h[:4]],
         "verified": verified, "step_spectra": S,
         "gather_ms": 1e3 * gather_s if dist_on else None,
+        "gather": dict(gstat) if dist_on else None,
     }
     q.close()
     gen.close()
@@ -963,6 +990,82 @@ def bruker_set(args, nat, torch, dev):
                              "the pipeline reads the page-locked compact rows itself)"}
 
 
+SIM = os.path.join(ROOT, "tests", "golden", "bruker", "sim")
+HARNESS_SB = (3.34, 3.56)  # benches/deconvoluter.rs:17-19, 40-44
+
+
+def _rate(fn, units, steps, warm=3):
+    for _ in range(warm):
+        fn()
+    t = time.perf_counter()
+    for _ in range(steps):
+        r = fn()
+    el = time.perf_counter() - t
+    return units * steps / el, el / steps * 1e3, r
+
+
+def harness_gpu(args, nat, torch, dev):
+    """The reference's own benchmark harness (benches/deconvoluter.rs:8-48) on the GPU,
+    through the Python surface with host buffers, as a user's process calls it:
+    - deconvolute_sim_spectrum / parallel_deconvolute_sim_spectrum: sim_01 (2048
+      points, sb (3.34, 3.56)) one call after another (the reference's sequential and
+      rayon forms are the same pipeline here);
+    - parallel_deconvolute_sim_spectra: the 16 sim spectra in one
+      par_deconvolute_spectra call;
+    - the blood functions are configs[0] and configs[4].
+    Each result is checked against the goldens (sim_XX_harness, oracle outputs).
+    A 2048-point spectrum is a chain of ~15 dependent launches that each do little
+    work: the case most likely to lose to a CPU, reported either way."""
+    import metabodecon as md
+    sim1 = md.Spectrum.read_bruker(os.path.join(SIM, "sim_01"), 10, 10, HARNESS_SB)
+    sims = md.Spectrum.read_bruker_set(SIM, 10, 10, HARNESS_SB)
+    dec = md.Deconvoluter()
+    dec.device = dev.index
+
+    def golden(k):
+        return np.load(os.path.join(GOLDEN, f"sim_{k + 1:02d}_harness.npz"))
+
+    def same(d, k):
+        g = golden(k)
+        return bool(np.array_equal(d.params, g["params"]) and
+                    abs(d.mse - float(g["mse"])) <= 1e-12 * abs(float(g["mse"])))
+    out = {}
+    for key, fn in (("deconvolute_sim_spectrum", lambda: dec.deconvolute_spectrum(sim1)),
+                    ("parallel_deconvolute_sim_spectrum", lambda: dec.par_deconvolute_spectrum(sim1))):
+        v, ms, d = _rate(fn, 1, 200)
+        out[key] = {"value": v, "unit": "spectra/s", "ms_per_call": ms, "calls": 200,
+                    "verified": same(d, 0)}
+    v, ms, res = _rate(lambda: dec.par_deconvolute_spectra(sims), len(sims), 50)
+    out["parallel_deconvolute_sim_spectra"] = {
+        "value": v, "unit": "spectra/s", "ms_per_call": ms, "calls": 50, "spectra_per_call": len(sims),
+        "verified": f"{sum(same(d, k) for k, d in enumerate(res))}/{len(res)} (goldens)"}
+    out["source"] = ("benches/deconvoluter.rs:12-48 (criterion, sample_size 50): sim_01 and the 16 "
+                     "sim spectra at sb (3.34, 3.56); Python surface, host buffers, a fresh process")
+    return out
+
+
+def harness_cpu(threads, reps=CPU_REPS):
+    """The same harness on the host cores: the oracle (C restatement) on the same
+    spectra; the reference's sequential form on one thread, its rayon forms on
+    `threads` (one spectrum per worker for the set)."""
+    import metabodecon as md
+    import oracle
+    sim1 = md.Spectrum.read_bruker(os.path.join(SIM, "sim_01"), 10, 10, HARNESS_SB)
+    sims = md.Spectrum.read_bruker_set(SIM, 10, 10, HARNESS_SB)
+    x, y, sb = sim1.chemical_shifts, sim1.intensities, sim1.signal_boundaries
+    seq, _ = median_rate(lambda: [oracle.deconvolute(x, y, sb, threads=1) for _ in range(20)], 20, reps)
+    par, _ = median_rate(lambda: [oracle.deconvolute(x, y, sb, threads=threads) for _ in range(20)], 20, reps)
+    X = np.stack([s.chemical_shifts for s in sims])
+    Y = np.stack([s.intensities for s in sims])
+    SBs = np.array([s.signal_boundaries for s in sims])
+    st, _ = median_rate(lambda: oracle.deconvolute_batch(X, Y, SBs, threads=min(threads, len(sims)),
+                                                         cap=X.shape[1] // 2 + 2), len(sims), reps)
+    return {"deconvolute_sim_spectrum": seq, "parallel_deconvolute_sim_spectrum": par,
+            "parallel_deconvolute_sim_spectra": st, "unit": "spectra/s",
+            "threads": {"deconvolute_sim_spectrum": 1, "parallel_deconvolute_sim_spectrum": threads,
+                        "parallel_deconvolute_sim_spectra": min(threads, len(sims))}}
+
+
 # ------------------------------------------------------------------ multi-rank configs
 C3_N, C3_POINTS, C3_PEAKS, C3_CAP = 4096, 65536, 1024, 2048
 GOLDEN = os.path.join(ROOT, "tests", "golden", "expected")
@@ -1126,25 +1229,58 @@ def dist_configs_dry(args, rank, world):
 
 
 # ------------------------------------------------------------------ CPU baselines
-def cpu_baselines(args, threads, Yh, x, blood_sp, blood_set, c3):
-    """The oracle (C restatement, -O3, no FMA) timed on this host: median of 5."""
+def cpu_synthetic(args, threads, Yh, x, reps=CPU_REPS):
+    """The headline's CPU baseline: the oracle (C restatement, -O3, no FMA) on the
+    same synthetic spectra, one spectrum per worker thread at a time (the reference's
+    par_deconvolute_spectra over rayon), median of `reps`; plus one spectrum on one
+    thread."""
     import oracle
     n = x.size
-    out = {"threads": threads, "nproc": os.cpu_count(), "cpu": _cpu_model(), "reps": CPU_REPS}
-    # configs[1]/[2]: synthetic spectra, one per worker thread (par_deconvolute_spectra)
     S = min(Yh.shape[0], 2 * threads)
     sb = np.array([SB] * S)
     rate, ts = median_rate(lambda: oracle.deconvolute_batch(x, Yh[:S], sb, threads=threads,
-                                                            cap=args.cap), S)
-    single, ts1 = median_rate(lambda: oracle.deconvolute(x, Yh[0], SB, threads=1), 1)
-    out["synthetic"] = {
+                                                            cap=args.cap), S, reps)
+    single, ts1 = median_rate(lambda: oracle.deconvolute(x, Yh[0], SB, threads=1), 1, max(1, reps // 2))
+    return {
         "value": rate, "unit": "spectra/s", "cores": threads, "kind": "port",
         "sample": (f"{S} synthetic {n}-pt/{args.peaks}-peak spectra per rep over {threads} "
-                   f"threads (one spectrum per thread at a time), median of {CPU_REPS} reps "
+                   f"threads (one spectrum per thread at a time), median of {reps} reps "
                    f"({statistics.median(ts):.2f} s); oracle C restatement -O3 "
                    f"-ffp-contract=off; host {_cpu_model()}, nproc {os.cpu_count()}, "
                    f"threads = min(affinity, cgroup CPU quota)"),
         "single_core_value": single}
+
+
+def cpu_baseline_ranks(args, dist, rank, world, sample):
+    """The host-core CPU baseline on a multi-rank run (north_star: 'spectra/s at
+    1/2/4/8 GPUs and the host-core CPU baseline reported in the same run'): rank 0
+    times the oracle after the timed region while every other rank waits on the
+    process group's TCP store (a blocking socket wait: no spinning host thread takes
+    cores from the measurement). `sample()` returns (x, Y) host arrays (rank 0 only).
+    Returns the record on rank 0, else None."""
+    store = dist.distributed_c10d._get_default_store()
+    key = "bench_cpu_baseline_done"
+    if rank != 0:
+        store.wait([key])
+        return None
+    try:
+        threads, aff, quota = host_threads(args)
+        x, Y = sample(threads)
+        cb = cpu_synthetic(args, threads, Y, x, args.cpu_reps)
+        cb["affinity_cpus"], cb["cgroup_quota_cpus"] = aff, quota
+        cb["measured"] = (f"rank 0 of {world}, after the timed region, the other ranks parked "
+                          "on the TCP store")
+        return cb
+    finally:
+        store.set(key, "1")
+
+
+def cpu_baselines(args, threads, Yh, x, blood_sp, blood_set, c3):
+    """The oracle (C restatement, -O3, no FMA) timed on this host: median of 5."""
+    import oracle
+    out = {"threads": threads, "nproc": os.cpu_count(), "cpu": _cpu_model(), "reps": CPU_REPS}
+    # configs[1]/[2]: synthetic spectra, one per worker thread (par_deconvolute_spectra)
+    out["synthetic"] = cpu_synthetic(args, threads, Yh, x)
     if blood_sp is not None:  # configs[0]: benches/deconvoluter.rs:8-30
         bx, by = blood_sp.chemical_shifts, blood_sp.intensities
         bsb = blood_sp.signal_boundaries
@@ -1198,11 +1334,19 @@ def dry_run(args, world, rank):
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     configs = dist_configs_dry(args, rank, world) if world > 1 else {}
+    cb = None
+    if world > 1 and not args.no_cpu_baseline:
+        def sample(threads):  # the host twin of the device generator (small: a dry run)
+            from tests.golden.cases import synth_spectrum
+            ys = [synth_spectrum(k, n=args.n, n_peaks=args.peaks, threads=threads)
+                  for k in range(threads)]
+            return ys[0][0], np.stack([t[1] for t in ys])
+        cb = cpu_baseline_ranks(args, dist, rank, world, sample)
     if rank == 0:
         print(json.dumps({"metric": "spectra/s (128k pts, ~2k peaks)", "value": None,
                           "unit": "spectra/s", "n_gpus": world, "steps": args.steps,
                           "warmup": args.warmup, "dry_run": True, "max_elapsed_s": float(el),
-                          "configs": configs}),
+                          "configs": configs, "cpu_baseline": cb}),
               flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -1221,6 +1365,8 @@ def child_configs(want) -> dict:
                                                    {"GPU_MAX_HW_QUEUES": "32"})]
     if "0" in want:
         runs.append(("configs[0]", "--c0-only", {}))
+    if "h" in want:
+        runs.append(("reference_harness", "--harness-only", {}))
     for key, flag, extra in runs:
         p = subprocess.run([sys.executable, os.path.abspath(__file__), flag],
                            env=dict(os.environ, **extra), capture_output=True, text=True, timeout=300)
@@ -1250,7 +1396,8 @@ def main():
     if args.dry_run:
         return dry_run(args, world, rank)
     pre = {}
-    if world == 1 and rank == 0 and not (args.c0_only or args.c4_only or args.no_configs or args.force_dist):
+    if world == 1 and rank == 0 and not (args.c0_only or args.c4_only or args.harness_only or
+                                         args.no_configs or args.force_dist):
         pre = child_configs({c.strip() for c in args.configs.split(",") if c.strip()})
 
     import torch
@@ -1261,8 +1408,12 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if (world > 1 or args.force_dist) and not args.no_configs and not (args.c0_only or args.c4_only):
+    if (world > 1 or args.force_dist) and not args.no_configs and not (args.c0_only or args.c4_only or
+                                                                       args.harness_only):
         pre["dist_configs[4]"] = dist_c4(args, nat, torch, dist, dev, rank, world)
+    if args.harness_only:
+        print(json.dumps(harness_gpu(args, nat, torch, dev)), flush=True)
+        return
     if args.c0_only:
         _, c0 = blood_gpu(args, nat, torch, dev)
         print(json.dumps(c0), flush=True)
@@ -1350,6 +1501,13 @@ def queue_line(args, h, world, nat):
                    "parallelism": f"dp{world}" if world > 1 else "single"},
         "verified_detail": h["verified"],
         "rccl_gather_ms": h["gather_ms"],
+        # the timed exchange's size (rank 0's figures; every rank sends the same)
+        "rccl_gather": (None if not h.get("gather") else dict(
+            h["gather"], ms=h["gather_ms"],
+            note=("bytes_per_rank: the packed [status, count, mse, table] records one rank "
+                  "sends to rank 0 in the timed region (tables padded to the widest count); "
+                  "one all_reduce + one gather per step, so rank 0's receive buffer is "
+                  "world x one step's records"))),
         "roofline": roof,
         "roofline_pipeline": pipe,
         "hbm_pipeline": hbm,
@@ -1408,6 +1566,19 @@ def finish(args, line, value, nat, torch, dist, dev, rank, world, local, pre=Non
         if pre and "dist_configs[4]" in pre:
             dc["configs[4]"] = pre.pop("dist_configs[4]")
         line["configs" if world > 1 else "configs_dist"] = dc
+    if (world > 1 or args.force_dist) and not args.no_cpu_baseline:
+        torch.cuda.synchronize()
+
+        def sample(threads):  # the headline's generator (device, bit-identical to the host one)
+            ctx = nat.Context(local)
+            xd, yd = synth_device(nat, ctx, torch, 2 * threads, args.n, args.peaks, 0, dev)
+            xh, yh = xd.cpu().numpy(), yd.cpu().numpy()
+            ctx.close()
+            return xh, yh
+        cb = cpu_baseline_ranks(args, dist, rank, world, sample)
+        if rank == 0:
+            line["cpu_baseline"] = cb
+            line["speedup_vs_cpu"] = value / cb["value"]
     if rank == 0 and world == 1:
         torch.cuda.synchronize()
         want = set() if args.no_configs else {c.strip() for c in args.configs.split(",") if c.strip()}
@@ -1420,7 +1591,9 @@ def finish(args, line, value, nat, torch, dist, dev, rank, world, local, pre=Non
         # them: in this one the headline's contexts and torch's streams hold hardware
         # queues (HIP's default 4) and the small calls' streams share them.
         # Normally measured before this process touched the GPU (child_configs).
-        kids = dict(pre) if pre else child_configs(want & {"0", "4"})
+        kids = dict(pre) if pre else child_configs(want & {"0", "4", "h"})
+        if "h" in want:
+            configs["reference_harness"] = kids.get("reference_harness", {"error": "not measured"})
         if "4" in want:
             import metabodecon as md
             blood_set = md.Spectrum.read_bruker_set(BLOOD, 10, 10, (-2.2, 11.8))
@@ -1460,6 +1633,15 @@ def finish(args, line, value, nat, torch, dist, dev, rank, world, local, pre=Non
             ctx.close()
             del xd, yd
             cb = cpu_baselines(args, threads, Yh, xh, blood_sp, blood_set, c3)
+            if "h" in want:
+                cb["reference_harness"] = harness_cpu(threads)
+                hz = configs.get("reference_harness", {})
+                for k in ("deconvolute_sim_spectrum", "parallel_deconvolute_sim_spectrum",
+                          "parallel_deconvolute_sim_spectra"):
+                    if isinstance(hz.get(k), dict) and "value" in hz[k]:
+                        hz[k]["cpu_value"] = cb["reference_harness"][k]
+                        hz[k]["cpu_threads"] = cb["reference_harness"]["threads"][k]
+                        hz[k]["speedup_vs_cpu"] = hz[k]["value"] / cb["reference_harness"][k]
             cb["affinity_cpus"], cb["cgroup_quota_cpus"] = aff, quota
             line["cpu_baseline"] = cb["synthetic"]
             line["cpu_baselines"] = {k: v for k, v in cb.items() if k != "synthetic"}

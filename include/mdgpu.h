@@ -271,6 +271,17 @@ int mdg_ctx_last_peaks(mdg_ctx* ctx, size_t spectrum, int which, int32_t* left,
  * moving-average smoother. */
 int mdg_ctx_last_smoothed(mdg_ctx* ctx, size_t spectrum, double* out, size_t n);
 
+/* Test hook (no reference counterpart): the fast-division range flags of `spectrum`
+ * in the context's last batch. x_ok: both axis ends within |x| <= 2^100.
+ * slow_mask: bit it (it < 29; bit 29 for later iterations) = fit iteration it ran the
+ * plain IEEE division (its parameters or the axis outside the fast ranges; DESIGN.md
+ * §2), bit 30 = the MSE summed every term directly with `/`, bit 31 = the exact-order
+ * MSE (MDG_OPTION_EXACT_MSE) did. unsafe_kept: retained Lorentzians outside the
+ * ranges. The reference always divides with `/` (lorentzian.rs:546-548); these show
+ * which of the engine's two bit-identical forms ran. */
+int mdg_ctx_last_range_flags(mdg_ctx* ctx, size_t spectrum, int32_t* x_ok, uint32_t* slow_mask,
+                             int32_t* unsafe_kept);
+
 /* Deconvoluter::optimize_settings (deconvoluter.rs:762-825): grid search over 27
  * moving-average x 10 noise-score x 3 analytical-fit settings on the reference
  * spectrum (x, y: n host values; sb0/sb1 and ignore as for mdg_deconvolute).

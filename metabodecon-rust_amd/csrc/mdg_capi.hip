@@ -89,6 +89,7 @@ struct mdg_ctx {
     int latency = 1;
     // roctx ranges around the pipeline's stages (mdg_ctx_set_tracing, MDG_ROCTX=1)
     bool tracing = false;
+    bool tracing_set = false;  // mdg_ctx_set_tracing was called (reloads keep its choice)
     std::mutex mu;
     // workspace arena
     Buffer arena;
@@ -881,6 +882,14 @@ EngineSwitches mdg::read_engine_switches() {
     return w;
 }
 
+// the device's compute units (the batch-wide fit's grid; 256 on MI355X)
+static int device_cus(int device) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
+        cus = 256;
+    return cus;
+}
+
 extern "C" {
 
 int mdg_ctx_create(int device, mdg_ctx** out) {
@@ -900,6 +909,7 @@ int mdg_ctx_create(int device, mdg_ctx** out) {
     }
     c->stream = c->own;
     c->sw = read_engine_switches();
+    c->sw.cus = device_cus(device);
     c->tracing = c->sw.roctx != 0;
     *out = c;
     return MDG_OK;
@@ -1013,10 +1023,13 @@ int mdg_ctx_set_latency_mode(mdg_ctx* c, int on) {
 
 int mdg_ctx_reload_switches(mdg_ctx* c) {
     if (!c) return MDG_INVALID_ARGUMENT;
-    const EngineSwitches w = read_engine_switches();
+    EngineSwitches w = read_engine_switches();
     std::lock_guard<std::mutex> g(c->mu);
+    w.cus = c->sw.cus;
     c->sw = w;
-    c->tracing = w.roctx != 0;
+    // MDG_ROCTX is the default of the tracing flag; an explicit mdg_ctx_set_tracing
+    // stays in force across reloads
+    if (!c->tracing_set) c->tracing = w.roctx != 0;
     return MDG_OK;
 }
 
@@ -1024,6 +1037,7 @@ int mdg_ctx_set_tracing(mdg_ctx* c, int on) {
     if (!c || (on != 0 && on != 1)) return MDG_INVALID_ARGUMENT;
     std::lock_guard<std::mutex> g(c->mu);
     c->tracing = on != 0;
+    c->tracing_set = true;
     return c->tracing && !roctx().push ? MDG_ERR_HIP : MDG_OK;
 }
 
@@ -1058,6 +1072,24 @@ int mdg_ctx_last_smoothed(mdg_ctx* c, size_t spectrum, double* out, size_t n) {
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipMemcpy(out, c->w.smooth + spectrum * (size_t)c->last_N, n * 8, hipMemcpyDeviceToHost));
+    return MDG_OK;
+}
+
+int mdg_ctx_last_range_flags(mdg_ctx* c, size_t spectrum, int32_t* x_ok, uint32_t* slow_mask,
+                              int32_t* unsafe_kept) {
+    if (!c) return MDG_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (!c->arena.p || spectrum >= (size_t)c->last_B) return MDG_INVALID_ARGUMENT;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const Workspace& w = c->w;
+    int32_t v[3] = {0, 0, 0};
+    HIPCHK(hipMemcpy(&v[0], w.x_ok + spectrum, 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&v[1], w.unsafe + 4 * spectrum + 3, 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&v[2], w.unsafe_kept + spectrum, 4, hipMemcpyDeviceToHost));
+    if (x_ok) *x_ok = v[0];
+    if (slow_mask) *slow_mask = (uint32_t)v[1];
+    if (unsafe_kept) *unsafe_kept = v[2];
     return MDG_OK;
 }
 
@@ -1949,6 +1981,10 @@ int mdg_queue_create(int device, size_t n, size_t max_batch, int lanes, const md
     int rc = MDG_OK;
     for (auto& L : q->lanes) {
         if ((rc = mdg_ctx_create(device, &L.ctx))) break;
+        // lanes > 1: a B = 1 batch (a deadline flush, a flush per submit at low load)
+        // shares the GPU with the other lanes' pipelines, so it takes tw7's fewer, wider
+        // workgroups rather than latency mode's tf12
+        if (lanes > 1) L.ctx->latency = 0;
         if ((rc = ensure(L.y, max_batch * n * 8)) || (rc = ensure(L.x, max_batch * n * 8)) ||
             (rc = ensure(L.sb, max_batch * 16)) || (rc = ensure(L.out, max_batch * cap * 24)) ||
             (rc = ensure(L.cnt, max_batch * 4)) || (rc = ensure(L.mse, max_batch * 8)) ||

@@ -2498,6 +2498,18 @@ __device__ __forceinline__ bool fit_done(const Workspace& w, int s, int it) {
     return w.fit_iters_s && it >= w.fit_iters_s[s];
 }
 
+// Record that spectrum s took the plain-division path (slot 3 of its range flags,
+// cleared by prep_spectrum): bit min(it, 29) for fit iteration it, kSlowMse for
+// k_mse_local's direct sums, kSlowMseExact for k_mse_exact_res. One lane of one
+// workgroup per launch and spectrum, and only on the slow path, so the fast path
+// pays a branch. mdg_ctx_last_range_flags reads it back: the tests' proof that a
+// spectrum outside the fast ranges really ran the IEEE division.
+constexpr int kSlowMse = 30, kSlowMseExact = 31;
+__device__ __forceinline__ void mark_slow(const Workspace& w, int s, int bit) {
+    atomicOr(&w.unsafe[4 * s + 3], (int)(1u << bit));
+}
+__device__ __forceinline__ int slow_bit(int it) { return it < 29 ? it : 29; }
+
 // What a term-fold launch needs of spectrum s before its first parameter load, read
 // together: one memory round trip. Written as branches (status, then fit_iters_s,
 // then sel_count, then x_ok and unsafe) they were a chain of dependent loads, each
@@ -2657,7 +2669,10 @@ __global__ __launch_bounds__(64 * (kTfEW + 1)) void k_fit_sup_tf(BatchArgs a, Wo
     const int s = blockIdx.y;
     const FitHead h = fit_head(w, s, it);
     if (!h.live) return;
-    if (blockIdx.x == 0 && threadIdx.x == 0) w.unsafe[4 * s + (it + 2) % 3] = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        w.unsafe[4 * s + (it + 2) % 3] = 0;
+        if (!h.fast) mark_slow(w, s, slow_bit(it));
+    }
     if (h.fast) fit_tf_body<true, Q>(w, s, h.P, it, T);
     else fit_tf_body<false, Q>(w, s, h.P, it, T);
 }
@@ -2856,7 +2871,10 @@ __global__ __launch_bounds__(64 * (SH::EW + 1)) void k_fit_sup_tw(BatchArgs a, W
     const int s = blockIdx.y;
     const FitHead h = fit_head(w, s, it);
     if (!h.live) return;
-    if (blockIdx.x == 0 && threadIdx.x == 0) w.unsafe[4 * s + (it + 2) % 3] = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        w.unsafe[4 * s + (it + 2) % 3] = 0;
+        if (!h.fast) mark_slow(w, s, slow_bit(it));
+    }
     if (h.fast) fit_tw_body<true, SH>(w, s, h.P, it, T, blockIdx.x, gridDim.x);
     else fit_tw_body<false, SH>(w, s, h.P, it, T, blockIdx.x, gridDim.x);
 }
@@ -2952,7 +2970,10 @@ __global__ __launch_bounds__(64 * (SH::EW + 1)) void k_fit_sup_twf(BatchArgs a, 
                 P = h.P;
                 tiles = (3 * P + QQ - 1) / QQ;
                 fast = h.fast;
-                if (blockIdx.x == 0) w.unsafe[4 * s + (it + 2) % 3] = 0;
+                if (blockIdx.x == 0) {
+                    w.unsafe[4 * s + (it + 2) % 3] = 0;
+                    if (!h.fast) mark_slow(w, s, slow_bit(it));
+                }
             }
         }
         int x = tiles;
@@ -2992,8 +3013,11 @@ __global__ void k_fit_sup(BatchArgs a, Workspace w, int it) {
     const int P = w.sel_count[s];
     const size_t base = (size_t)s * w.capD;
     const double* __restrict__ params = w.params + 3 * base;
-    if (part == 0 && threadIdx.x == 0) w.unsafe[4 * s + ((it + 1) & 1)] = 0;
     const bool fast = w.x_ok[s] && w.unsafe[4 * s + (it & 1)] == 0;
+    if (part == 0 && threadIdx.x == 0) {
+        w.unsafe[4 * s + ((it + 1) & 1)] = 0;
+        if (!fast) mark_slow(w, s, slow_bit(it));
+    }
     for (int i = part * blockDim.x + threadIdx.x; i < 3 * P; i += parts * blockDim.x) {
         const double sup = superpose(w.rx[3 * base + i], params, P, fast);
         w.ratio[3 * base + i] = w.ry[3 * base + i] / sup;
@@ -3377,6 +3401,7 @@ __global__ __launch_bounds__(256) void k_mse_local(BatchArgs a, Workspace w, int
     int kept_n;
     (void)block_exclusive_scan<BS>(cnt, lds_i, &kept_n);
     const bool fast = xok && !__syncthreads_or(uns);
+    if (!fast && part == 0 && tid == 0) mark_slow(w, s, kSlowMse);
     KSTAMP(31);
     double acc = 0.0;
     for (int64_t v0 = (int64_t)part * TP; v0 < total; v0 += (int64_t)nparts * TP) {
@@ -3619,6 +3644,7 @@ __global__ void k_mse_exact_res(BatchArgs a, Workspace w, double* res, int64_t r
     const int nig = w.n_ig[s];
     const int64_t total = mse_len(w, s);
     const bool fast = w.x_ok[s] && w.unsafe_kept[s] == 0;
+    if (!fast && part == 0 && threadIdx.x == 0) mark_slow(w, s, kSlowMseExact);
     double* r = res + (size_t)s * res_row;
     for (int64_t v = (int64_t)part * blockDim.x + threadIdx.x; v < total; v += (int64_t)parts * blockDim.x) {
         const int64_t idx = mse_index(w, s, nig, v);
@@ -3914,13 +3940,7 @@ const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int i
     if ((f == "twf" || f == "twf1" || f == "twf3s") && a.B <= kTwfMaxB) {
         // one list of the batch's tiles over about one workgroup per slot: <63, 2, 7>
         // (15 waves, 131 KB of LDS) one per CU, <63, 1, 7> (8 waves, 66 KB) two
-        static int cus = 0;
-        if (!cus) {
-            int dev = 0;
-            (void)hipGetDevice(&dev);
-            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-                cus = 256;
-        }
+        const int cus = sw.cus;
         if (f == "twf3s") {
             using SH = TwShape<63, 1, 3, true>;
             const int g = tg ? tg : 4 * cus;

@@ -93,7 +93,8 @@ struct Workspace {
     int32_t* kept_count;
     int32_t* x_ok;            // B: axis inside the fast-division range
     int32_t* unsafe;          // B x 4: count of fit params outside it, per params version
-                              // (k_fit_update path: version & 1; fused k_fit_sup_tf: version % 3)
+                              // (k_fit_update path: version & 1; fused k_fit_sup_tf: version % 3);
+                              // slot 3: the launches that took the plain division (mark_slow)
     int32_t* unsafe_kept;     // B: same for the retained Lorentzians
     int32_t* mse_done;        // B: k_mse_local workgroups finished (the last one folds, resets)
     int32_t* peak_cnt;        // B x ceil(W/64) u64: k_peaks slots {valid, bordered, kept} per mask chunk
@@ -131,13 +132,16 @@ struct EngineSwitches {
     int gfit = 24;               // MDG_GFIT: k_fit_sup workgroups per spectrum
     int mse_npt = 0;             // MDG_MSE_NPT = 2 | 4 (0: by batch size)
     int mse_parts = 0;           // MDG_MSE_PARTS (0: by shape)
-    int mse_pk = 0;              // MDG_MSE_PK = 20 | 30 expansion powers (0: by batch size)
+    int mse_pk = 0;              // MDG_MSE_PK: 0 = 30 powers at radius 3 (every batch size);
+                                 // 20 selects the round-4 radius-5 form
     int mse_nearcap = -1;        // MDG_MSE_NEARCAP (-1: kLocNear)
     int prep_separate = 0;      // MDG_PREP=separate
     int graphs = 0;              // MDG_GRAPHS=1
     int host_direct = 1;         // MDG_HOST_DIRECT=0: device copies of the small inputs / results
     int dec_overlap = 1;         // MDG_DEC_OVERLAP=0: compact rows by DMA + decode launch
     int roctx = 0;               // MDG_ROCTX=1: roctx ranges around the pipeline stages
+    int cus = 256;               // not a switch: the device's CU count, set by mdg_ctx_create
+                                 // (once per context, not per launch)
     // diagnostic builds only (make diag)
     char diag_skip[32] = {};
     char diag_dup[64] = {};

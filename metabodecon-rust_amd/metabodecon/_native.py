@@ -47,7 +47,8 @@ EXPORTS = [
     "mdg_deconvolute", "mdg_deconvolute_batch", "mdg_deconvolute_rows", "mdg_deconvolute_batch_device",
     "mdg_deconvolute_rows_i32", "mdg_decode_rows_i32_device",
     "mdg_superposition_vec", "mdg_superposition_vec_device", "mdg_synth_batch_device",
-    "mdg_ctx_last_peaks", "mdg_ctx_last_smoothed", "mdg_ctx_set_profiling_mask",
+    "mdg_ctx_last_peaks", "mdg_ctx_last_smoothed", "mdg_ctx_last_range_flags",
+    "mdg_ctx_set_profiling_mask",
     "mdg_optimize_settings", "mdg_ordered_sum", "mdg_check_fast_division",
     "mdg_check_division", "mdg_division_hard_case", "mdg_ctx_stage_kernel", "mdg_ctx_get_stream",
     "mdg_synth_lorentzians_hw", "mdg_synth_batch_device_hw",
@@ -257,6 +258,7 @@ def _declare(L):
     L.mdg_superposition_vec_device.argtypes = [_vp, _vp, _sz, _vp, _sz, _vp]
     L.mdg_ctx_last_peaks.argtypes = [_vp, _sz, ctypes.c_int, _i32p, _i32p, _i32p, _sz, _szp]
     L.mdg_ctx_last_smoothed.argtypes = [_vp, _sz, _dp, _sz]
+    L.mdg_ctx_last_range_flags.argtypes = [_vp, _sz, _i32p, ctypes.POINTER(ctypes.c_uint32), _i32p]
     L.mdg_optimize_settings.argtypes = [_vp, _dp, _dp, _sz, ctypes.c_double, ctypes.c_double, _dp,
                                         _sz, sp, _dp]
     L.mdg_ordered_sum.argtypes = [_vp, _dp, _sz, ctypes.c_double, _dp]
@@ -457,6 +459,17 @@ class Context:
             if p.value:
                 out[name] = p.value.decode()
         return out
+
+    def last_range_flags(self, spectrum: int) -> tuple[int, int, int]:
+        """(x_ok, slow_mask, unsafe_kept) of `spectrum` from the last batch run (test
+        hook, mdg_ctx_last_range_flags): which launches took the plain division."""
+        xo, uk = ctypes.c_int32(0), ctypes.c_int32(0)
+        m = ctypes.c_uint32(0)
+        st = lib().mdg_ctx_last_range_flags(self.handle, spectrum, ctypes.byref(xo), ctypes.byref(m),
+                                            ctypes.byref(uk))
+        if st:
+            raise RuntimeError(strerror(st))
+        return xo.value, m.value, uk.value
 
     def last_smoothed(self, spectrum: int, n: int) -> np.ndarray:
         """Smoothed intensities of `spectrum` from the last batch run (diagnostic)."""

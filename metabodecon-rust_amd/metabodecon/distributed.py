@@ -44,13 +44,39 @@ def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
     return lo, lo + base + (1 if rank < rem else 0)
 
 
-_BUFS: dict = {}
+# The exchange buffers (grow-only, kept across calls) live in thread-local storage:
+# one set per thread and process group, so two threads or two groups collecting on
+# the same device never share them, and a thread's buffers are freed with the thread
+# (a module dict keyed by thread ident and id(group) was never evicted,
+# and a later object could reuse either id). Each entry holds its group object and
+# is used only for that very object; release_buffers() drops the calling thread's
+# buffers (e.g. before destroying a group).
+_TLS = threading.local()
 
 
-def _key(key, dtype, dev, group):
-    # one set of buffers per process group and thread: two groups, or two threads
-    # collecting on the same device, never share them
-    return (key, dtype, str(dev), id(group), threading.get_ident())
+def _store() -> dict:
+    d = getattr(_TLS, "bufs", None)
+    if d is None:
+        d = _TLS.bufs = {}
+    return d
+
+
+def _get(key, group):
+    e = _store().get((key, id(group)))
+    return e[1] if e is not None and e[0] is group else None
+
+
+def _put(key, group, value):
+    _store()[(key, id(group))] = (group, value)
+    return value
+
+
+def release_buffers(group=None, all_groups: bool = False) -> None:
+    """Free the calling thread's exchange buffers for ``group`` (every group with
+    ``all_groups``). They are re-created on the next call."""
+    d = _store()
+    for k in [k for k, (g, _) in d.items() if all_groups or g is group]:
+        del d[k]
 
 
 def _buf(key, shape, dtype, dev, group=None):
@@ -60,12 +86,12 @@ def _buf(key, shape, dtype, dev, group=None):
     n = 1
     for d in shape:
         n *= int(d)
-    k = _key(key, dtype, dev, group)
-    t = _BUFS.get(k)
+    k = (key, dtype, str(dev))
+    t = _get(k, group)
     if t is None or t.numel() < n:
         pin = str(dev) == "pinned"
-        t = torch.empty(max(n, 1), dtype=dtype, device="cpu" if pin else dev, pin_memory=pin)
-        _BUFS[k] = t
+        t = _put(k, group, torch.empty(max(n, 1), dtype=dtype, device="cpu" if pin else dev,
+                                       pin_memory=pin))
     return t[:n].view(*shape)
 
 
@@ -216,11 +242,11 @@ def gather_host(local: Sequence[Result], n_total: int, group=None, dst=0, error:
     if n_total == 0:  # the same on every rank: nothing to agree on or exchange
         return None, ([] if dst is None or rank == dst else None)
     nccl = dist.get_backend(group) == "nccl"
-    key = _key("exchange", None, torch.cuda.current_device() if nccl else "cpu", group)
-    ex = _BUFS.get(key)
+    key = ("exchange", str(torch.cuda.current_device()) if nccl else "cpu")
+    ex = _get(key, group)
     if ex is None:
-        ex = _BUFS[key] = _Exchange(nccl, torch.device("cuda", torch.cuda.current_device()) if nccl
-                                    else torch.device("cpu"))
+        ex = _put(key, group, _Exchange(nccl, torch.device("cuda", torch.cuda.current_device())
+                                        if nccl else torch.device("cpu")))
     base, rem = divmod(n_total, world)
     max_items = base + (1 if rem else 0)
     lo = shard_range(n_total, rank, world)[0]
@@ -331,6 +357,10 @@ def par_deconvolute_spectra(deconvoluter, spectra: Sequence, group=None, dst=0):
             err = e
     first, got = gather_host(local, len(spectra), group, dst, error=None if err is None else repr(err))
     if err is not None:
+        # every rank raises the first failure in global order: a failing
+        # spectrum before this rank's block on another rank wins over the engine error
+        if first is not None and first[1] is not None:
+            raise from_status(first[1]) from err
         raise err
     if first is not None:
         if first[1] is None:

@@ -66,6 +66,9 @@ class Diag(ctypes.Structure):
         ("sel_center", ctypes.POINTER(ctypes.c_int64)),
         ("sel_right", ctypes.POINTER(ctypes.c_int64)),
         ("sel_cap", ctypes.c_size_t),
+        ("range_mask", ctypes.c_uint64),
+        ("unsafe_kept", ctypes.c_int64),
+        ("x_ok", ctypes.c_int32),
     ]
 
 
@@ -280,6 +283,11 @@ class OracleResult:
     sbi: tuple[int, int]
     sfr_mean: float
     sfr_sd: float
+    # the engine's fast-division ranges (mdo_diag): bit v = parameter version v has a
+    # peak outside them; retained Lorentzians outside them; axis ends inside them
+    range_mask: int = 0
+    unsafe_kept: int = 0
+    x_ok: int = 1
 
 
 def deconvolute(x, y, sb, settings: Settings | None = None, ignore=(), threads: int = 1,
@@ -305,7 +313,7 @@ def deconvolute(x, y, sb, settings: Settings | None = None, ignore=(), threads: 
     ns = max(int(d.n_selected), 0) if rc == 0 else 0
     return OracleResult(rc, out[:k].copy(), mse.value, int(d.n_detected), int(d.n_selected),
                         np.stack([a[:ns] for a in sel], axis=1), (int(d.sbi0), int(d.sbi1)),
-                        d.sfr_mean, d.sfr_sd)
+                        d.sfr_mean, d.sfr_sd, int(d.range_mask), int(d.unsafe_kept), int(d.x_ok))
 
 
 def deconvolute_batch(x, y, sb, settings: Settings | None = None, ignore=(), threads: int = 1,

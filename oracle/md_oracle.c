@@ -387,6 +387,20 @@ static int in_ignore(int64_t v, const int64_t* pairs, long n_pairs) {
     return 0;
 }
 
+/* The engine's fast-division range predicates (csrc/mdg_kernels.hip peak_fast_ok /
+ * x_fast_ok), restated for the test hooks: a spectrum whose parameters or axis fail
+ * them must take the plain IEEE division. Not part of the reference. */
+static int fast_peak(const double* L) {
+    double as = fabs(L[0]);
+    return as >= 0x1p-200 && as <= 0x1p200 && L[1] >= 0x1p-200 && L[1] <= 0x1p200 &&
+           fabs(L[2]) <= 0x1p100;
+}
+static uint64_t range_bit(const double* params, size_t P, unsigned v) {
+    for (size_t p = 0; p < P; ++p)
+        if (!fast_peak(params + 3 * p)) return (uint64_t)1 << (v < 63 ? v : 63);
+    return 0;
+}
+
 /* deconvoluter.rs:530-552 (and par_deconvolute_spectrum :591-613) */
 int mdo_deconvolute(const double* x, const double* y, size_t n, double sb0, double sb1,
                     const mdo_settings* s, const double* ignore, size_t n_ignore,
@@ -420,7 +434,13 @@ int mdo_deconvolute(const double* x, const double* y, size_t n, double sb0, doub
     signal_boundaries_indices(x, sb0, sb1, &sbi0, &sbi1);
     long n_ig = 0;
     if (n_ignore > 0) n_ig = mdo_ignore_region_indices(x, n, sb0, sb1, ignore, n_ignore, ig);
-    if (diag) { diag->sbi0 = (int64_t)sbi0; diag->sbi1 = (int64_t)sbi1; }
+    if (diag) {
+        diag->sbi0 = (int64_t)sbi0;
+        diag->sbi1 = (int64_t)sbi1;
+        diag->range_mask = 0;
+        diag->unsafe_kept = 0;
+        diag->x_ok = fabs(x[0]) <= 0x1p100 && fabs(x[n - 1]) <= 0x1p100;
+    }
 
     /* selector.select_peaks */
     size_t n_sd = n >= 2 ? n - 2 : 0;
@@ -515,6 +535,7 @@ int mdo_deconvolute(const double* x, const double* y, size_t n, double sb0, doub
             mdo_mirror_shoulder(st6 + 6 * p);
             mdo_solve_stencil(st6 + 6 * p, &params[3 * p], &params[3 * p + 1], &params[3 * p + 2]);
         }
+        if (diag) diag->range_mask |= range_bit(params, P, 0);
         for (uint32_t it = 0; it < s->fit_iterations; ++it) {
             mdo_superposition_vec(rx, 3 * P, params, P, sup, threads);
             for (size_t p = 0; p < P; ++p) {
@@ -526,6 +547,7 @@ int mdo_deconvolute(const double* x, const double* y, size_t n, double sb0, doub
             }
             for (size_t p = 0; p < P; ++p)
                 mdo_solve_stencil(st6 + 6 * p, &params[3 * p], &params[3 * p + 1], &params[3 * p + 2]);
+            if (diag) diag->range_mask |= range_bit(params, P, it + 1);
         }
         size_t kept = 0;
         for (size_t p = 0; p < P; ++p) {
@@ -536,7 +558,10 @@ int mdo_deconvolute(const double* x, const double* y, size_t n, double sb0, doub
                 ++kept;
             }
         }
-        if (diag) diag->n_kept = (int64_t)kept;
+        if (diag) {
+            diag->n_kept = (int64_t)kept;
+            for (size_t p = 0; p < kept; ++p) diag->unsafe_kept += !fast_peak(params + 3 * p);
+        }
         if (out_count) *out_count = kept;
         if (kept > cap) { rc = MDO_CAPACITY; goto done; }
         if (out_params) memcpy(out_params, params, sizeof(double) * 3 * kept);

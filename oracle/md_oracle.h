@@ -58,6 +58,13 @@ typedef struct mdo_diag {
     int64_t* sel_center;
     int64_t* sel_right;
     size_t sel_cap;
+    /* the engine's fast-division ranges (test hooks, mdgpu.h mdg_ctx_last_range_flags):
+     * bit v of range_mask: some parameter of version v (0 = initial solve, v = after
+     * iteration v-1's update) lies outside them; unsafe_kept: retained Lorentzians
+     * outside them; x_ok: both axis ends inside |x| <= 2^100 */
+    uint64_t range_mask;
+    int64_t unsafe_kept;
+    int32_t x_ok;
 } mdo_diag;
 
 void mdo_default_settings(mdo_settings* s);

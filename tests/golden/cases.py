@@ -60,7 +60,10 @@ def _settings(**kw):
 CASES = [f"sim_{i:02d}" for i in range(1, 17)] + [f"blood_{i:02d}" for i in range(1, 17)] + [
     "blood_01_water", "blood_02_two_regions_increasing", "sim_01_detector_only",
     "sim_01_identity", "sim_01_ma5x2_thr3", "synth_128k_2k_s0", "synth_128k_2k_s1",
-]
+] + [f"sim_{i:02d}_harness" for i in range(1, 17)]
+# "_harness": the sim spectra with the signal boundaries of the reference's own
+# benchmark harness, (3.34, 3.56) (benches/deconvoluter.rs:17-19, 40-44; the
+# integration test, tests/deconvoluter.rs, uses (3.35, 3.55) as the plain sim cases)
 
 
 @functools.lru_cache(maxsize=None)
@@ -71,6 +74,8 @@ def _load(name: str):
         x, y, sb = _spectrum("sim", int(name[4:]), (3.35, 3.55))
     elif name.startswith("blood_") and len(name) == 8:
         x, y, sb = _spectrum("blood", int(name[6:]), (-2.2, 11.8))
+    elif name.startswith("sim_") and name.endswith("_harness"):
+        x, y, sb = _spectrum("sim", int(name[4:6]), (3.34, 3.56))
     elif name == "blood_01_water":
         x, y, sb = _spectrum("blood", 1, (-2.2, 11.8))
         ign = ((4.7, 4.9),)

@@ -9,7 +9,7 @@ Inputs: the reference's Bruker fixtures copied verbatim to tests/golden/bruker/
 (data files only) and the synthetic generator of libmdgpu (host functions
 mdg_synth_lorentzians / mdg_synth_noise; no GPU needed).
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py [case ...]
 """
 import os
 import sys
@@ -24,10 +24,11 @@ import oracle  # noqa: E402
 from tests.golden.cases import CASES, load_case  # noqa: E402
 
 
-def main():
+def main(names=None):
+    """Every case, or only `names` (the others' files stay as they are)."""
     out_dir = os.path.join(HERE, "expected")
     os.makedirs(out_dir, exist_ok=True)
-    for name in CASES:
+    for name in names or CASES:
         x, y, sb, settings, ignore = load_case(name)
         r = oracle.deconvolute(x, y, sb, settings, ignore=ignore)
         np.savez_compressed(
@@ -40,4 +41,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:])

@@ -240,7 +240,23 @@ def _par_worker(rank, world, port, q, mode):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         spectra = [load_case(f"sim_{i:02d}") for i in range(1, 8)]
-        if mode == "results":
+        if mode == "blood":  # the 16 blood spectra (configs[4]'s set)
+            blood = [load_case(f"blood_{i:02d}") for i in range(1, 17)]
+            res = par_deconvolute_spectra(_OracleDeconvoluter(), blood)
+            q.put((rank, None if res is None else [(d.params.tolist(), d.mse) for d in res]))
+        elif mode == "mixed_fail":
+            # an engine failure on rank 2 and a failing spectrum before its
+            # block (index 1, rank 0): every rank raises the spectrum's error
+            x, y, sb, st, ign = spectra[1]
+            spectra[1] = (x, np.full_like(y, 3.0), sb, st, ign)  # NoPeaksDetected
+            try:
+                par_deconvolute_spectra(_OracleDeconvoluter(fail_rank=2), spectra, dst=None)
+                q.put((rank, "no error"))
+            except mexc.NoPeaksDetected as e:
+                q.put((rank, "NoPeaksDetected" + ("+cause" if e.__cause__ is not None else "")))
+            except Exception as e:
+                q.put((rank, type(e).__name__))
+        elif mode == "results":
             res = par_deconvolute_spectra(_OracleDeconvoluter(), spectra)
             q.put((rank, None if res is None else [(d.params.tolist(), d.mse) for d in res]))
         elif mode == "fail":
@@ -279,7 +295,7 @@ def _spawn(world, mode):
     procs = [ctx.Process(target=_par_worker, args=(r, world, port, q, mode)) for r in range(world)]
     for p in procs:
         p.start()
-    got = dict(q.get(timeout=240) for _ in procs)
+    got = dict(q.get(timeout=400) for _ in procs)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -297,8 +313,8 @@ def _oracle_sim():
     return out
 
 
-@pytest.mark.timeout(300)
-@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.timeout(500)
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_par_deconvolute_spectra_host_exchange(world):
     """distributed.par_deconvolute_spectra (round 5: every rank's block through the
     host path, the packed results exchanged by gather_host) with an oracle engine:
@@ -338,3 +354,62 @@ def test_par_deconvolute_spectra_subgroup_without_global_rank_0():
     want = _oracle_sim()
     for (p, m), (wp, wm) in zip(got[1], want):
         assert np.array_equal(np.array(p).reshape(-1, 3), wp) and m == wm
+
+
+@pytest.mark.timeout(600)
+def test_par_deconvolute_spectra_blood_world_8():
+    """World 8, the configs[4] shape: the 16 blood spectra, two per
+    rank, through par_deconvolute_spectra's host exchange; rank 0 gets every result in
+    input order, bit for bit (the goldens), the other ranks None."""
+    import os as _os
+    from tests.conftest import GOLDEN
+    got = _spawn(8, "blood")
+    assert all(got[r] is None for r in range(1, 8))
+    assert len(got[0]) == 16
+    for i, (p, m) in enumerate(got[0]):
+        g = np.load(_os.path.join(GOLDEN, "expected", f"blood_{i + 1:02d}.npz"))
+        assert np.array_equal(np.array(p).reshape(-1, 3), g["params"]) and m == float(g["mse"]), i
+
+
+@pytest.mark.timeout(300)
+def test_par_deconvolute_spectra_engine_and_spectrum_failures():
+    """a failing spectrum at index 1 (rank 0's block) and an engine failure
+    on rank 2 (a later block): every rank raises the spectrum's error, the engine-failing
+    rank with its own exception as the cause."""
+    got = _spawn(3, "mixed_fail")
+    assert got[0] == got[1] == "NoPeaksDetected", got
+    assert got[2] == "NoPeaksDetected+cause", got
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world,n", [(8, 4096), (8, 5)])
+def test_gather_tables_world_8(world, n):
+    """gather_tables / gather_packed at world 8: 4096 records (512 per rank, the
+    configs[3] sharding) and 5 records (three ranks own none)."""
+    test_gather_tables_worlds_uneven_and_empty_ranks(world, n)
+
+
+@pytest.mark.timeout(600)
+def test_bench_gpus_8_dry_run_carries_cpu_baseline():
+    """`bench.py --gpus 8 --dry-run`: eight gloo ranks run the
+    launcher, rendezvous, sharding and gathers of the multi-rank path, and the rank-0
+    line carries the host-core CPU baseline, measured by rank 0 while the other seven
+    wait on the store."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8",
+                        "--dry-run", "--steps", "2", "--cpu-reps", "1", "--n", "16384",
+                        "--peaks", "256"], capture_output=True, text=True, timeout=540, env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 8 and rec["dry_run"] is True
+    c3 = rec["configs"]["configs[3]"]
+    assert c3["n_ranks"] == 8 and c3["spectra_per_rank"] == 512
+    cb = rec["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1
+    assert "rank 0 of 8" in cb["measured"]

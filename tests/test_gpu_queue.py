@@ -281,3 +281,31 @@ def test_queue_failed_launch_is_sticky_and_never_hangs():
     msg = nat.strerror(nat.ERR_OUT_OF_MEMORY)
     assert msg in errors.get("submit", "") and msg in errors["flush"] and msg in errors["synchronize"]
     assert errors["stats"]["batches"] == 0 and errors["stats"]["open"] >= 1
+
+
+@pytest.mark.parametrize("lanes,kernel", [(1, "k_fit_sup_tf<12>"), (2, "k_fit_sup_tw<63, 1, 7>")])
+def test_queue_single_spectrum_batch_fit_kernel(lanes, kernel):
+    """a queue with more than one lane runs its lanes' pipelines side by
+    side, so a B = 1 batch (a flush after one submission) must not take latency mode's
+    tf12 (256 workgroups for the GPU alone) but tw7's fewer, wider workgroups, as the
+    engine chose before latency mode became a context property; a
+    one-lane queue keeps latency mode. Results equal the golden either way."""
+    torch = pytest.importorskip("torch")
+    x, y, sb, _, _ = load_case("blood_02")
+    n = y.size
+    cap = n // 2 + 2
+    X = torch.from_numpy(x).cuda()
+    Y = torch.from_numpy(y).cuda()
+    out, cnt, mse, st = _outputs(torch, 1, cap)
+    torch.cuda.synchronize()
+    q = nat.SpectrumQueue(0, n, 8, lanes, nat.default_settings())
+    try:
+        q.submit(X.data_ptr(), Y.data_ptr(), sb, out[0].data_ptr(), cap, cnt.data_ptr(),
+                 mse.data_ptr(), st.data_ptr())
+        q.synchronize()
+        assert q.lane(0).stage_kernels()["fit_superposition"] == kernel
+    finally:
+        q.close()
+    g = np.load(os.path.join(GOLDEN, "expected", "blood_02.npz"))
+    assert int(st[0]) == 0 and int(cnt[0]) == g["params"].shape[0]
+    assert np.array_equal(out[0, : int(cnt[0])].cpu().numpy(), g["params"])

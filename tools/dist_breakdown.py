@@ -98,7 +98,7 @@ def main():
 
     def stamped_gather(loc):  # gather_host's steps (nccl, dst 0) with a stamp after each
         t = [time.perf_counter()]
-        ex = D._BUFS[D._key("exchange", None, torch.cuda.current_device(), None)]
+        ex = D._get(("exchange", str(torch.cuda.current_device())), None)
         width = max([int(p.shape[0]) for _, p, _ in loc] + [1])
         ex.hdr_np[0], ex.hdr_np[1] = width, D._FAIL_NONE
         ex.hdr_d.copy_(ex.hdr_h, non_blocking=True)
