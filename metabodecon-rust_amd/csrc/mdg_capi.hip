@@ -460,6 +460,7 @@ int validate_common(const mdg_settings* s, size_t n_ignore, const double* ignore
 
 // Runs the whole pipeline for a device-resident batch. Caller holds c->mu.
 int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
+    a.det_only = s->selector == MDG_SELECT_DETECTOR_ONLY;
     int rc = ensure_workspace(c, a.B, a.N, a.n_ignore);
     if (rc) return rc;
     // Row strides follow the current shape; the arena is sized for the largest
@@ -583,7 +584,12 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
         StageTimer t(c, ST_SELECT);
         for (int r = reps("select"); r > 0; --r) kn[ST_SELECT] = launch_select(a, w, det_only, s->threshold, st);
     }
-    for (uint32_t it = 0; it < s->fit_iterations; ++it) {
+    const bool small_fit = fit_is_small(a, sw);
+    if (small_fit) {  // every iteration in one launch
+        StageTimer t(c, ST_FIT_SUP);
+        kn[ST_FIT_SUP] = launch_fit_small(a, w, st);
+    }
+    for (uint32_t it = 0; it < (small_fit ? 0u : s->fit_iterations); ++it) {
         {
             StageTimer t(c, ST_FIT_SUP);
             kn[ST_FIT_SUP] = launch_fit_sup(a, w, gfit, (int)it, sw, st);
@@ -852,6 +858,7 @@ EngineSwitches mdg::read_engine_switches() {
     const std::string f = str("MDG_FITSUP");
     copy(w.fitsup, sizeof(w.fitsup), "");
     if (f == "tf" || f == "tf12" || f == "tw7" || f == "tw3s" || f == "twf" || f == "twf1" || f == "twf3s" ||
+        f == "small" ||
         f == "plain")
         copy(w.fitsup, sizeof(w.fitsup), f);
 #ifdef MDG_DIAG
@@ -1160,6 +1167,7 @@ int run_pipeline_graphed(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
         drop_graphs(c);
         c->graphs_gen = c->ws_gen;
     }
+    a.det_only = s->selector == MDG_SELECT_DETECTOR_ONLY;
     BatchArgs ka = a;
     clear_io(ka);
     // the kernel-choice switches (tests, diagnostics) select other kernels, so they

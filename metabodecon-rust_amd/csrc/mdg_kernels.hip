@@ -650,6 +650,12 @@ constexpr int kChainScalers = 2;         // scaler waves (round-robin batches)
 #define MDG_CHAIN_SCB 8  // chain_diag ms: 2: 1.27, 4: 0.77, 8: 0.595, 12: 0.589, 16: 0.596; bench: 12 is 1% slower
 #endif
 constexpr int kChainScBatch = MDG_CHAIN_SCB;  // output blocks per scaler batch
+// (round 6, measured and removed: batches of 1, 2, 4 blocks at the start and halving
+// over the last 16 blocks, to shorten the three-pass pipeline's fill and drain.
+// chain_diag, B = 1: 2048 points 46 -> 54 us, 131072 points 589 -> 603 us; the
+// downstream chains ran 18-19 instead of 10.6-11 cycles per tick at 2048 points,
+// starved by small batches whose fixed cost -- staging loads, the vmcnt drain, the
+// ordered publication -- the scalers pay per batch.)
 constexpr int kChainG = MDG_CHAIN_G;      // ticks per stored checkpoint in steady blocks
 static_assert(kChainG % 8 == 0 && kChainCB % kChainG == 0, "checkpoint groups tile the blocks");
 constexpr int kChainPrefetch = MDG_CHAIN_PF;  // input blocks touched into the scalar cache ahead
@@ -3045,6 +3051,180 @@ __global__ void k_fit_update(BatchArgs a, Workspace w, int it) {
     }
 }
 
+// K6s  the whole fit of a small spectrum in ONE workgroup ("small": N <= kSmallN, one
+// workgroup per spectrum, all iterations in one launch). Each iteration: the
+// superposition at the 3P reduced points, one thread per point, the reference's left
+// fold over the peaks in their order (lorentzian.rs:606-611: the same adds as every
+// fit kernel, so the same bits); the ratios y/sup (fitter_analytical.rs:40-47); the
+// stencil update, mirror and re-solve of each peak (:48-65) -- with __syncthreads
+// between the phases instead of kernel boundaries. Measured before it (sim_01, 2048
+// points, 26 peaks; the reference's own benchmark case): ten k_fit_sup_tf<12>
+// launches of 4.6 us each whose work is a few hundred cycles. Parameters, stencils and
+// ratios stay in LDS for P <= kSmallP; a larger P (a small spectrum with that many
+// selected peaks is pathological) runs the same loops over the global rows (params /
+// params_alt versions, the stencil rows in place, the kept rows as ratio scratch):
+// bit-identical, but one CU does all of it. Range flags per iteration from the version
+// the iteration reads (every parameter through peak_fast_ok, and x_ok), as the tile
+// kernels count them; slow iterations recorded by mark_slow. The retain and the MSE
+// stay with k_mse_local (many workgroups): an exact-order MSE inside this one
+// workgroup (38k evaluations and a 1468-term windowed fold for sim_01) measured 41
+// against 23 + 11 us for the fit here and k_mse_local after it (round 6).
+// Superposition per iteration: with 3 P^2 <= kSmallT terms (P <= 45: the sim spectra)
+// every (point, peak) term is evaluated by its own thread into LDS and each point's
+// thread then folds its row in peak order; otherwise each point's thread evaluates and
+// folds its P terms itself (fold_small).
+constexpr int kSmallN = 4096, kSmallP = 512, kSmallBS = 512, kSmallT = 6144;
+
+// acc + sum_j<P sfhw_j / (hw2_j + (x - maxp_j)^2), a left fold in j order (the adds
+// stay in order: the reference's bits); eight Lorentzians' parameters are read (LDS
+// broadcasts, or wave-uniform global loads) and their eight divisions issued together
+// before the eight adds. Folding term by term, each division waited on its own loads
+// and latency chain: ~230 cycles per term (k_fit_small's phase stamps, round 6).
+template <bool FAST>
+__device__ __forceinline__ double fold_small(double x, const double* prm, int P, double acc = -0.0) {
+    int j = 0;
+    for (; j + 8 <= P; j += 8) {
+        double t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            t[u] = lorentz_t<FAST>(x, prm[3 * (j + u)], prm[3 * (j + u) + 1], prm[3 * (j + u) + 2]);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += t[u];
+    }
+    for (; j < P; ++j) acc += lorentz_t<FAST>(x, prm[3 * j], prm[3 * j + 1], prm[3 * j + 2]);
+    return acc;
+}
+
+template <int BS, class PT, class ST, class RT>
+__device__ __forceinline__ void fit_small_body(const Workspace& w, int s, int P, int iters, int xok,
+                                               PT prm_in, PT prm_out, ST stn, RT rat, bool lds) {
+    const size_t base = (size_t)s * w.capD;
+    const double* __restrict__ rx = w.rx + 3 * base;
+    const double* __restrict__ ry = w.ry + 3 * base;
+    const int tid = threadIdx.x, npts = 3 * P;
+    KSTAMP(71);
+    for (int it = 0; it < iters; ++it) {
+        // LDS: one parameter row updated in place; global: versions it (read) and it + 1
+        PT prm = lds ? prm_in : (PT)params_version(w, base, it);
+        PT nxt = lds ? prm_in : (PT)params_version(w, base, it + 1);
+        int bad = 0;
+        for (int p = tid; p < P; p += BS) bad |= !peak_fast_ok(prm[3 * p], prm[3 * p + 1], prm[3 * p + 2]);
+        const bool fast = xok && !__syncthreads_or(bad);
+        if (!fast && tid == 0) mark_slow(w, s, slow_bit(it));
+        for (int i = tid; i < npts; i += BS) {
+            const double x = rx[i];
+            const double acc = fast ? fold_small<true>(x, prm, P) : fold_small<false>(x, prm, P);
+            rat[i] = ry[i] / acc;
+        }
+        __syncthreads();
+        if (it == 0) KSTAMP(72);
+        for (int p = tid; p < P; p += BS) {
+            Stencil q{stn[6 * p], stn[6 * p + 1], stn[6 * p + 2], stn[6 * p + 3], stn[6 * p + 4], stn[6 * p + 5]};
+            q.y1 = q.y1 * rat[3 * p];
+            q.y2 = q.y2 * rat[3 * p + 1];
+            q.y3 = q.y3 * rat[3 * p + 2];
+            mirror_shoulder(q);
+            stn[6 * p] = q.x1; stn[6 * p + 1] = q.x2; stn[6 * p + 2] = q.x3;
+            stn[6 * p + 3] = q.y1; stn[6 * p + 4] = q.y2; stn[6 * p + 5] = q.y3;
+            double L[3];
+            solve(q, L);
+            nxt[3 * p] = L[0]; nxt[3 * p + 1] = L[1]; nxt[3 * p + 2] = L[2];
+        }
+        __syncthreads();
+        if (it == 0) KSTAMP(73);
+    }
+    KSTAMP(74);
+}
+
+// k_fit_small for 3 P^2 <= kSmallT (P <= 45): the iteration's 3 P^2 terms are spread
+// over the workgroup, kSmallT / BS per thread, every (point, peak) assignment and its x
+// fixed in registers before the first iteration, all their LDS parameter reads issued
+// together; each point's thread then folds its row of T in peak order (eight reads
+// ahead of the adds), divides its y by the sum, and the peaks' threads update the
+// stencils and re-solve; the range check of the new parameters rides on that update's
+// barrier. The same operations as every fit kernel, so the same bits.
+template <int BS>
+__device__ __forceinline__ void fit_small_terms(const Workspace& w, int s, int P, int iters, int xok,
+                                                double* prm, double* stn, double* rat, double* T) {
+    constexpr int U = kSmallT / BS;
+    const size_t base = (size_t)s * w.capD;
+    const int tid = threadIdx.x, npts = 3 * P, nt = npts * P;
+    const int RS = P | 1;  // row stride of T (odd: fewer bank conflicts in the folds)
+    double xu[U];
+    int ju[U], eu[U];
+    {
+        int i = tid / P, j = tid - (tid / P) * P;
+        const int stI = BS / P, stJ = BS - (BS / P) * P;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool ok = tid + u * BS < nt;
+            xu[u] = w.rx[3 * base + (ok ? i : 0)];
+            ju[u] = ok ? j : 0;
+            eu[u] = ok ? i * RS + j : -1;
+            i += stI;
+            j += stJ;
+            if (j >= P) {
+                j -= P;
+                ++i;
+            }
+        }
+    }
+    const double yq = tid < npts ? w.ry[3 * base + tid] : 1.0;
+    int bad = 0;
+    for (int p = tid; p < P; p += BS) bad |= !peak_fast_ok(prm[3 * p], prm[3 * p + 1], prm[3 * p + 2]);
+    bool fast = xok && !__syncthreads_or(bad);
+    KSTAMP(71);
+    for (int it = 0; it < iters; ++it) {
+        if (!fast && tid == 0) mark_slow(w, s, slow_bit(it));
+        double t[U];
+        if (fast) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) t[u] = lorentz_t<true>(xu[u], prm[3 * ju[u]], prm[3 * ju[u] + 1], prm[3 * ju[u] + 2]);
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; ++u) t[u] = lorentz_t<false>(xu[u], prm[3 * ju[u]], prm[3 * ju[u] + 1], prm[3 * ju[u] + 2]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (eu[u] >= 0) T[eu[u]] = t[u];
+        lds_barrier();
+        if (tid < npts) {
+            const double* row = T + tid * RS;
+            double acc = -0.0;
+            int k = 0;
+            for (; k + 8 <= P; k += 8) {
+                double v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = row[k + u];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) acc += v[u];
+            }
+            for (; k < P; ++k) acc += row[k];
+            rat[tid] = yq / acc;
+        }
+        lds_barrier();
+        if (it == 0) KSTAMP(72);
+        bad = 0;
+        if (tid < P) {
+            const int p = tid;
+            Stencil q{stn[6 * p], stn[6 * p + 1], stn[6 * p + 2], stn[6 * p + 3], stn[6 * p + 4], stn[6 * p + 5]};
+            q.y1 = q.y1 * rat[3 * p];
+            q.y2 = q.y2 * rat[3 * p + 1];
+            q.y3 = q.y3 * rat[3 * p + 2];
+            mirror_shoulder(q);
+            stn[6 * p] = q.x1; stn[6 * p + 1] = q.x2; stn[6 * p + 2] = q.x3;
+            stn[6 * p + 3] = q.y1; stn[6 * p + 4] = q.y2; stn[6 * p + 5] = q.y3;
+            double L[3];
+            solve(q, L);
+            prm[3 * p] = L[0]; prm[3 * p + 1] = L[1]; prm[3 * p + 2] = L[2];
+            bad = !peak_fast_ok(L[0], L[1], L[2]);
+        }
+        fast = xok && !__syncthreads_or(bad);
+        if (it == 0) KSTAMP(73);
+    }
+    KSTAMP(74);
+}
+
 // K8  retain sfhw > CHECK_PRECISION && hw2 > CHECK_PRECISION, order preserving
 // (fitter_analytical.rs:67-69); copies min(count, cap) rows to the caller's output.
 // the fitted parameters of spectrum s: k_fit_sup_tf / _tw leave version
@@ -3690,6 +3870,40 @@ __global__ __launch_bounds__(kExactFoldBS) void k_mse_exact_fold(BatchArgs a, Wo
     if (threadIdx.x == 0) a.out_mse[s] = total / (double)cum[nig + 1];
 }
 
+template <int BS>
+__global__ __launch_bounds__(BS) void k_fit_small(BatchArgs a, Workspace w) {
+    __shared__ double prm[3 * kSmallP];
+    __shared__ double buf[9 * kSmallP];  // stencils (6 per peak), ratios (3 per point)
+    __shared__ double T[kSmallT];        // the terms of one iteration (3 P^2 <= kSmallT)
+    double* const stn = buf;
+    double* const rat = buf + 6 * kSmallP;
+    const int s = blockIdx.x;
+    KSTAMP(70);
+    const int st = w.status[s], P = w.sel_count[s], xok = w.x_ok[s];
+    const int fis = w.fit_iters_s ? w.fit_iters_s[s] : 0x7fffffff;
+    if (st) return;
+    const int iters = min(fis, w.fit_iters);
+    const size_t base = (size_t)s * w.capD;
+    if (P <= kSmallP) {
+        for (int k = threadIdx.x; k < 3 * P; k += BS) prm[k] = w.params[3 * base + k];
+        for (int k = threadIdx.x; k < 6 * P; k += BS) stn[k] = w.stencil[6 * base + k];
+        __syncthreads();
+        if (P > 0 && 3 * P * (P | 1) <= kSmallT && P <= BS) {
+            static_assert(kSmallT % BS == 0, "whole term slots per thread");
+            fit_small_terms<BS>(w, s, P, iters, xok, prm, stn, rat, T);
+        } else {
+            fit_small_body<BS>(w, s, P, iters, xok, (double*)prm, (double*)prm, stn, rat, true);
+        }
+        // the version k_mse_local's retain reads (final_params)
+        double* out = (double*)params_version(w, base, iters);
+        for (int k = threadIdx.x; k < 3 * P; k += BS) out[k] = prm[k];
+    } else {
+        fit_small_body<BS>(w, s, P, iters, xok, (double*)nullptr, (double*)nullptr, w.stencil + 6 * base,
+                           w.kept + 3 * base, false);
+    }
+    KSTAMP(75);
+}
+
 __global__ void k_range_check(const double* __restrict__ x, int64_t n,
                               const double* __restrict__ params, int P, int* flag) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < P;
@@ -3901,12 +4115,23 @@ const char* launch_select(const BatchArgs& a, const Workspace& w, int detector_o
 // other value is ignored).
 static std::string fit_choice(const BatchArgs& a, const EngineSwitches& sw) {
     if (sw.fitsup[0]) return sw.fitsup;
+    // small spectra: the whole fit in one workgroup per spectrum (k_fit_small). Not with
+    // the detector-only selector: it keeps every detected peak (~250 in a 2048-point sim
+    // spectrum), and one workgroup cannot evaluate 3 P^2 terms per iteration as fast as
+    // the tile fits' hundreds (P ~ 100 is about even, measured at P = 26: 2.3 against
+    // 4.6 us per iteration). A noise-score selection keeps ~25-35 peaks of the sims.
+    if (a.N <= kSmallN && !a.det_only) return "small";
     if (a.B == 1) return a.latency ? "tf12" : "tw7";
     return a.B <= 4 ? "tf" : a.B <= 24 ? "twf1" : "plain";
 }
 bool fit_sup_fused(const BatchArgs& a, const EngineSwitches& sw) {
     const std::string f = fit_choice(a, sw);
     return f != "plain" && f != "mfma";  // those two leave the stencil update to k_fit_update
+}
+bool fit_is_small(const BatchArgs& a, const EngineSwitches& sw) { return fit_choice(a, sw) == "small"; }
+const char* launch_fit_small(const BatchArgs& a, const Workspace& w, hipStream_t st) {
+    launch_k(k_fit_small<kSmallBS>, dim3(a.B), dim3(kSmallBS), 0, st, a, w);
+    return "k_fit_small";
 }
 const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int it, const EngineSwitches& sw,
                            hipStream_t st) {

@@ -35,6 +35,7 @@ struct BatchArgs {
     double* out_mse;
     int32_t* out_status;
     int latency;          // the context's latency mode (mdg_ctx_set_latency_mode; kernel choice only)
+    int det_only;         // the detector-only selector (run_pipeline; host-side kernel choice only)
     // mdg_deconvolute_rows_i32 with page-locked rows: the pipeline decodes the rows
     // into y / x itself, reading them from host memory (null: y and x hold them)
     const int32_t* const* dec_rows;  // B host-mapped int32 rows (device copy of the table)
@@ -202,6 +203,9 @@ const char* launch_select(const BatchArgs& a, const Workspace& w, int detector_o
                           double threshold, hipStream_t st);
 // returns true when the launched kernel also did the stencil update (no k_fit_update)
 bool fit_sup_fused(const BatchArgs& a, const EngineSwitches& sw);
+// small spectra (N <= kSmallN, or MDG_FITSUP=small): every fit iteration in one launch
+bool fit_is_small(const BatchArgs& a, const EngineSwitches& sw);
+const char* launch_fit_small(const BatchArgs& a, const Workspace& w, hipStream_t st);
 const char* launch_fit_sup(const BatchArgs& a, const Workspace& w, int gx, int it, const EngineSwitches& sw,
                            hipStream_t st);
 void launch_fit_update(const BatchArgs& a, const Workspace& w, int gx, int it, hipStream_t st);

@@ -500,8 +500,10 @@ def test_chain_smoother_repeated_launches(ctx, monkeypatch, engine_env):
 
 
 # the library's fit kernels (fit_choice, mdg_kernels.hip); "twf*" are the batch-wide
-# tile lists, "tw3s"/"twf3s" single-buffered; ":G" = G workgroups (many tiles each)
-FIT_KERNELS = ["tf", "tf12", "tw7", "tw3s", "twf", "twf1", "twf3s", "twf:5", "twf3s:7", "plain"]
+# tile lists, "tw3s"/"twf3s" single-buffered; ":G" = G workgroups (many tiles each);
+# "small" = every iteration in one workgroup per spectrum (k_fit_small, the default for
+# N <= 4096; forced on the 131072-point cases it takes its global-row form, P > 512)
+FIT_KERNELS = ["tf", "tf12", "tw7", "tw3s", "twf", "twf1", "twf3s", "twf:5", "twf3s:7", "plain", "small"]
 
 
 @pytest.mark.parametrize("mode", ["fine", "coarse"])
@@ -1089,3 +1091,34 @@ def test_concurrent_contexts_stream_bit_exact(graphs, monkeypatch, engine_env):
     finally:
         for c in ctxs:
             c.close()
+
+
+@pytest.mark.parametrize("selector,forced", [("noise_score", None), ("detector_only", None),
+                                             ("detector_only", "small")])
+def test_small_spectra_take_the_one_launch_fit(ctx, selector, forced, monkeypatch, engine_env):
+    """N <= 4096 with the noise-score selector (the sim spectra, 2048 points, ~26 peaks;
+    the reference's benchmark case at sb (3.34, 3.56)): the whole fit runs in one
+    k_fit_small launch per call -- its term-parallel form (3 P^2 <= 6144) -- single and
+    batched, bit-identical to the oracle, MSE within 1e-12. Detector-only keeps ~250
+    peaks: the engine takes the tile fits; forced onto k_fit_small it runs the
+    per-point LDS form (P <= 512)."""
+    if forced:
+        engine_env.setenv("MDG_FITSUP", forced)
+    want = "k_fit_small" if (selector == "noise_score" or forced) else None
+    st = oracle.make_settings(selector=selector)
+    names = [f"sim_{i:02d}_harness" for i in (1, 2, 11)]
+    data = [load_case(n) for n in names]
+    for x, y, sb, _, _ in data[:1]:
+        o = oracle.deconvolute(x, y, sb, st)
+        status, counts, out, mse = gpu_batch(ctx, x, y[None, :], [sb], st)
+        k = ctx.stage_kernels()["fit_superposition"]
+        assert k == want if want else k != "k_fit_small", k
+        check_against(o.params, o.mse, status[0], counts[0], out[0], mse[0])
+    xs = np.stack([d[0] for d in data])
+    ys = np.stack([d[1] for d in data])
+    status, counts, out, mse = gpu_batch(ctx, xs, ys, [d[2] for d in data], st)
+    k = ctx.stage_kernels()["fit_superposition"]
+    assert k == want if want else k != "k_fit_small", k
+    for k, (x, y, sb, _, _) in enumerate(data):
+        o = oracle.deconvolute(x, y, sb, st)
+        check_against(o.params, o.mse, status[k], counts[k], out[k], mse[k])

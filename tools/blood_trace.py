@@ -55,6 +55,7 @@ def main():
     ap.add_argument("batch", nargs="?", type=int, default=16, help="blood spectra per call")
     ap.add_argument("--summary", metavar="CSV", help="print the last call's kernels of a trace")
     ap.add_argument("--brief", metavar="CSV", help="mean duration per kernel of the last call")
+    ap.add_argument("--sim", action="store_true", help="the sim set at sb (3.34, 3.56) instead of blood")
     args = ap.parse_args()
     if args.summary:
         return summary(args.summary)
@@ -64,8 +65,12 @@ def main():
     import metabodecon as md
     from metabodecon import _native as nat
     b = args.batch
-    S = md.Spectrum.read_bruker_set(os.path.join(ROOT, "tests/golden/bruker/blood"), 10, 10,
-                                    (-2.2, 11.8))[:b]
+    if args.sim:
+        S = md.Spectrum.read_bruker_set(os.path.join(ROOT, "tests/golden/bruker/sim"), 10, 10,
+                                        (3.34, 3.56))[:b]
+    else:
+        S = md.Spectrum.read_bruker_set(os.path.join(ROOT, "tests/golden/bruker/blood"), 10, 10,
+                                        (-2.2, 11.8))[:b]
     dec = md.Deconvoluter()
     ctx = nat.context(nat.default_device())
     for _ in range(5):

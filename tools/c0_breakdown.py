@@ -35,12 +35,20 @@ def main():
     import argparse
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("calls", nargs="?", type=int, default=200)
-    calls = ap.parse_args().calls
+    ap.add_argument("--sim", action="store_true",
+                    help="sim_01 at sb (3.34, 3.56) (the reference's benches/deconvoluter.rs case) "
+                         "instead of blood_01")
+    a = ap.parse_args()
+    calls = a.calls
     import torch
     import metabodecon as md
     from metabodecon import _native as nat
-    sp = md.Spectrum.read_bruker(os.path.join(ROOT, "tests/golden/bruker/blood/blood_01"), 10, 10,
-                                 (-2.2, 11.8))
+    if a.sim:
+        sp = md.Spectrum.read_bruker(os.path.join(ROOT, "tests/golden/bruker/sim/sim_01"), 10, 10,
+                                     (3.34, 3.56))
+    else:
+        sp = md.Spectrum.read_bruker(os.path.join(ROOT, "tests/golden/bruker/blood/blood_01"), 10, 10,
+                                     (-2.2, 11.8))
     dec = md.Deconvoluter()
     out = {"py": med(lambda: dec.deconvolute_spectrum(sp), calls)}
     ctx = nat.context()

@@ -15,12 +15,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def main():
     ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
     ap.add_argument("batch", nargs="?", type=int, default=1)
-    B = ap.parse_args().batch
+    ap.add_argument("--sim", action="store_true",
+                    help="sim_01 at sb (3.34, 3.56) (2048 points: k_fit_small) instead of the synthetic spectrum")
+    args = ap.parse_args()
+    B = args.batch
     os.environ.setdefault("MDGPU_LIB", os.path.join(ROOT, "tools", "ubench", "libmdgpu_diag.so"))
     sys.path[:0] = [ROOT, os.path.join(ROOT, "metabodecon-rust_amd")]
     import torch
     from metabodecon import _native as nat
-    n = 131072
+    n = 2048 if args.sim else 131072
     L = nat.lib()
     L.mdg_debug_set_diag.argtypes = [ctypes.c_void_p]
     ctx = nat.Context(0)
@@ -28,9 +31,16 @@ def main():
     ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     x = torch.empty(n, dtype=torch.float64, device=dev)
     y = torch.empty((B, n), dtype=torch.float64, device=dev)
-    assert L.mdg_synth_batch_device(ctx.handle, B, n, 14.8, 20.0, 0, 2048, -1.8, 11.4, 1e3,
-                                    x.data_ptr(), y.data_ptr()) == 0
-    sb = torch.tensor([[11.8, -2.2]] * B, dtype=torch.float64, device=dev)
+    if args.sim:
+        import metabodecon as md
+        sp = md.Spectrum.read_bruker(os.path.join(ROOT, "tests/golden/bruker/sim/sim_01"), 10, 10, (3.34, 3.56))
+        x.copy_(torch.from_numpy(sp.chemical_shifts.copy()))
+        y.copy_(torch.from_numpy(sp.intensities.copy()).expand(B, n))
+        sb = torch.tensor([list(sp.signal_boundaries)] * B, dtype=torch.float64, device=dev)
+    else:
+        assert L.mdg_synth_batch_device(ctx.handle, B, n, 14.8, 20.0, 0, 2048, -1.8, 11.4, 1e3,
+                                        x.data_ptr(), y.data_ptr()) == 0
+        sb = torch.tensor([[11.8, -2.2]] * B, dtype=torch.float64, device=dev)
     out = torch.zeros((B, 4096, 3), dtype=torch.float64, device=dev)
     cnt = torch.zeros(B, dtype=torch.int32, device=dev)
     mse = torch.zeros(B, dtype=torch.float64, device=dev)
@@ -48,7 +58,8 @@ def main():
         torch.cuda.synchronize()
     d = diag[STAMPS:].cpu().tolist()
     groups = {"select": range(10, 19), "peaks": range(0, 5), "fit_dpp": range(20, 24),
-              "mse": range(30, 36), "window_mean": [45, 46, 40, 41, 42], "window_var": [55, 56, 50, 51, 52]}
+              "mse": range(30, 36), "window_mean": [45, 46, 40, 41, 42], "window_var": [55, 56, 50, 51, 52],
+              "small": range(70, 78), "window_small_mse": [65, 66, 60, 61, 62]}
     for name, r in groups.items():
         v = [d[k] for k in r]
         if not any(v):

@@ -1,13 +1,17 @@
 // Timeline of k_smooth_chain<3> (3 passes) on synthetic 131072-point spectra:
 // builds the library kernel source with -DMDG_DIAG; per (spectrum, pass) the
 // chain wave's head / steady / tail stamps and the feeder/scaler round counts.
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -DMDG_DIAG \
+//       tools/ubench/chain_diag.hip -o tools/ubench/chain_diag
+//   tools/ubench/chain_diag [B] [passes] [mode] [N]     (N: points, default 131072)
 #include "../../metabodecon-rust_amd/csrc/mdg_kernels.hip"
 #include <cstdio>
 #include <vector>
 using namespace mdg;
 int main(int argc, char** argv) {
-    const int N = 131072, B = argc > 1 ? atoi(argv[1]) : 1, P = argc > 2 ? atoi(argv[2]) : 3, WS = 3;
+    const int B = argc > 1 ? atoi(argv[1]) : 1, P = argc > 2 ? atoi(argv[2]) : 3, WS = 3;
     const int mode = argc > 3 ? atoi(argv[3]) : 0;
+    const int N = argc > 4 ? atoi(argv[4]) : 131072;
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_chain_mode), &mode, sizeof(mode));
     std::vector<double> h(N * (size_t)B);
     for (size_t i = 0; i < h.size(); ++i) h[i] = (double)((i * 2654435761u) % 1000003) * 1e-3;
