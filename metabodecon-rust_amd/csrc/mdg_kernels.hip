@@ -2701,6 +2701,13 @@ __global__ __launch_bounds__(64 * (kTfEW + 1)) void k_fit_sup_tf(BatchArgs a, Wo
 // evaluator waves a workgroup is four waves, and four of them -- 16 waves, VGPRs
 // for 4 per SIMD -- make 1024 tile slots: a B = 16 batch of ~1000-peak spectra
 // (768 tiles) runs in one round instead of 1.5.
+// (round 6, measured and removed: "twh", chunks of 32 peaks with an evaluator lane =
+// (peak, half of its wave's points), 34 KB of LDS at Q = 60, four 7-wave workgroups per
+// CU -- 1024 tile slots, so a B = 16 blood batch's 800 tiles in one round instead of
+// two. Bit-exact, 69 VGPRs at occupancy 7, but slower: ten launches 405 against 366 us
+// at B = 16, 295 against 263 at B = 8; PMC (profiles/r06_pmc_fit_b16_twh_rejected.json)
+// waits 48% against 45%, VALU active 16% against 19%, LDS bank conflicts 8% against 1%:
+// seven waves per SIMD leave the fold wave less issue, and the chunks' barriers double.)
 template <int Q_, int PB, int PS, bool SB_ = false>
 struct TwShape {
     static constexpr int Q = Q_;
