@@ -2131,6 +2131,7 @@ __device__ __forceinline__ void fit_init_pair(const BatchArgs& a, const Workspac
 // k_select's LDS: the SFR terms of the two windowed folds (up to kSfrLds; more go
 // through the workspace), reused afterwards for the selected peaks (up to kSelLds)
 constexpr int kSfrLds = 12288;         // 96 KB
+constexpr int kSelWinMin = 1024;       // signal-free-region terms from which the folds are windowed
 constexpr int kSelLds = 4096;          // 3 ints each: 48 KB of the same buffer
 // centers per thread counted directly: 1, i.e. only P <= 1024 (blood_01, P = 16100,
 // stamps at B = 1: the two-level search 7.2-8.1k cycles, 16 direct loads per thread
@@ -2237,9 +2238,12 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
     // peaks[..left] ++ peaks[right..], staged contiguously (all threads) and folded
     // by wave 0; then the squared deviations, staged in place, folded the same way
     const int n_sfr = left + (P - right);
-    // scores and squared deviations are >= +0: the windowed fold applies (one wave
-    // folds short sets itself)
-    const bool win = n_sfr >= 4 * kWinSeg;
+    // scores and squared deviations are >= +0: the windowed fold applies. One wave folds
+    // short sets itself (seg_fold: any address space), below kSelWinMin terms: its
+    // fixed phases -- the double-double segment sums, 64 candidate folds per segment,
+    // the walk, their barriers -- cost a 208-term set (sim_01) ~13k cycles per fold
+    // against ~1.7k for the direct left fold (round 6, k_select's phase stamps)
+    const bool win = n_sfr >= kSelWinMin;
     // staged in LDS when they fit (the folds' loads are then LDS reads, not L2 round
     // trips; the windowed fold's DPP segment folds measured 18.4k cycles against 29k
     // with scalar-loaded terms and 38k with LDS broadcast reads, blood_01, round 4);
@@ -2252,7 +2256,7 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
         const double sum = window_fold<BS>(-0.0, wl, sfr, n_sfr);  // every thread: barriers inside
         if (threadIdx.x == 0) thr_sh = sum / (double)n_sfr;
     } else if (threadIdx.x < 64) {
-        const double mean = dpp_fold(-0.0, sfr, n_sfr) / (double)n_sfr;
+        const double mean = seg_fold(-0.0, sfr, n_sfr) / (double)n_sfr;
         if (threadIdx.x == 0) thr_sh = mean;
     }
     __syncthreads();
@@ -2265,7 +2269,7 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
     __syncthreads();
     double var = 0.0;
     if (win) var = window_fold<BS>(-0.0, wl, sfr, n_sfr, 50) / (double)n_sfr;
-    else if (threadIdx.x < 64) var = dpp_fold(-0.0, sfr, n_sfr) / (double)n_sfr;
+    else if (threadIdx.x < 64) var = seg_fold(-0.0, sfr, n_sfr) / (double)n_sfr;
     KSTAMP(17);
     if (threadIdx.x == 0) {
         const double sd = __builtin_sqrt(var);
