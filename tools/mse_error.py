@@ -1,8 +1,9 @@
 """Relative deviation of the engine's MSE from the oracle's left-fold MSE
 (compute_mse, deconvoluter.rs:828-862) over all golden cases and two more synthetic
 spectra (GPU box), for each MSE form the library ships: the local expansions with 2
-and with 4 points per thread (MDG_MSE_NPT) and 20 or 30 powers (MDG_MSE_PK; the
-defaults pick both by batch size) and the exact-order option (MDG_OPTION_EXACT_MSE,
+and with 4 points per thread (MDG_MSE_NPT; the default picks it by batch size) and 20
+or 30 powers (MDG_MSE_PK; the default is 30 at every batch size, 20 selects the
+round-4 radius-5 form) and the exact-order option (MDG_OPTION_EXACT_MSE,
 expected 0). Prints the max |rel| per form.
 
     python tools/mse_error.py
