@@ -502,7 +502,7 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     if (ma) {
         const int P = (int)s->smooth_iterations, ws = (int)s->smooth_window;
         if ((sw.smooth == EngineSwitches::SM_DEFAULT || sw.smooth == EngineSwitches::SM_CHAIN) &&
-            chain_supported(a.B, a.N, P, ws) &&
+            !smooth_uses_small(a, P, ws, sw) && chain_supported(a.B, a.N, P, ws) &&
             ensure_chain(c, chain_bytes(a.B, a.N, ws, P)) == MDG_OK) {
             const int64_t L = chain_stride_for(a.N, ws);
             char* base = (char*)c->chain.p;
@@ -528,7 +528,7 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     const bool panic_shape = ma && (int64_t)(s->smooth_window / 2) > a.N;
     // the chain smoother does k_prep's work itself (MDG_PREP=separate: not)
     const bool fused_prep = ma && !panic_shape && !skip_smooth && !sw.prep_separate && reps("prep") == 1 &&
-                            smooth_uses_chain(a, w, sm_it, sm_ws, sw);
+                            smooth_fuses_prep(a, w, sm_it, sm_ws, sw);
     if (a.dec_rows) {
         // rows still in host memory (mdg_deconvolute_rows_i32): the chain launch
         // decodes them while it smooths (flags of this call's generation), any other
@@ -850,6 +850,7 @@ EngineSwitches mdg::read_engine_switches() {
                : sm == "chain" ? EngineSwitches::SM_CHAIN
                : sm == "pipe"  ? EngineSwitches::SM_PIPE
                : sm == "generic" ? EngineSwitches::SM_GENERIC
+               : sm == "small" ? EngineSwitches::SM_SMALL
                                  : EngineSwitches::SM_OTHER;
     w.chain_excl = str("MDG_CHAIN_EXCL").substr(0, 1) != "0";
     w.chain_l2ahead = std::max(0, num("MDG_CHAIN_L2AHEAD", 0));

@@ -1293,6 +1293,315 @@ __global__ void k_smooth(BatchArgs a, Workspace w, int iters, int ws) {
 // The per-center border scans of the reference become next/previous-set-bit
 // searches on these masks (K3): the predicates do not depend on the center.
 // ----------------------------------------------------------------------------------
+// ----------------------------------------------------------------------------------
+// K1s  the moving average of a SMALL spectrum (N <= kSmallN, round 6) in ONE workgroup:
+// one wave per pass, the passes pipelined through LDS (pass 0 reads the row staged in
+// LDS, pass p > 0 a ring of pass p - 1's outputs, the last pass writes the smoothed
+// row). moving_average.rs:53-83's recurrence exactly as k_smooth_chain runs it (sum +=
+// in[i + R]; sum -= in[i + R - WS] once the FIFO is full; div = 1/len; out = sum *
+// div): the scalar ticks (prefill, the FIFO filling, leftovers, the tail) in plain
+// code, the steady ticks sixteen at a time as DPP row_newbcast fmacs on row-replicated
+// operands (fma(+-t, 1, acc) rounds as the add / sub), tick k's sum captured into the
+// lanes k, k + 16, ... of the block's output by a masked select. A 2048-point
+// spectrum spent 46 us in k_smooth_chain, most of it filling and draining the
+// three-CU pipeline (8-block scaler batches through L2); here
+// the hand-off is a 16-tick block through LDS.
+// MEASURED SLOWER, so not the default (MDG_SMOOTH=small selects it; bit-exact, tested):
+// sim_01 (2048 points, three passes of width 3) 58-63 us against k_smooth_chain's 46-47.
+// The steady loop runs ~32 cycles a tick in the DPP blocks and ~42 with the hand-offs
+// (phase stamps, profiles/r06_smooth_small_stamps.txt) where the chain's folder runs
+// ~10 with scalar operands: the two DPP adds alone issue at 7.75 cycles each, and a
+// single workgroup cannot hide the per-pass lag of two superblocks.
+constexpr int kSmallN = 4096;  // "small" spectra: k_smooth_small, k_fit_small
+constexpr int kSmRing = 512;   // doubles per intermediate pass ring (a power of two)
+constexpr int kSmMaxP = 15;    // passes = waves (+ one wave for the spectrum's prep)
+constexpr int kSmMaxWS = 32;
+constexpr int kSmSpins = 1 << 22;
+constexpr int kSmStage = 16;  // row values per thread per staging round
+
+__device__ __forceinline__ int lds_ld(const int* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// 16 steady ticks: acc += A[k]; acc -= S[k] for k = 0..15 (lane k of each 16-lane row),
+// hist lane (l & 15) += the sum after tick k times mk[k] (1.0 in lanes k, k + 16, ...,
+// 0.0 elsewhere): with finite sums every other product is a zero and hist lane (l & 15)
+// ends as that tick's sum exactly (the caller redoes a block whose sum went non-finite).
+// The capture is an f64 fmac, not a select: a 32-bit select of the DPP fmac's result
+// waited on it ~20 cycles a tick (46 cycles/tick measured, 15.5 for the two fmacs).
+__device__ __forceinline__ void sm_block16(double& acc, double& hist, double A, double S, double one,
+                                           const double (&mk)[16]) {
+#define MDG_SMTICK(k)                                                                          \
+    "v_fmac_f64_dpp %[acc], %[A], %[one] row_newbcast:" #k " row_mask:0xf bank_mask:0xf\n"     \
+    "v_fmac_f64_dpp %[acc], -%[S], %[one] row_newbcast:" #k " row_mask:0xf bank_mask:0xf\n"    \
+    "v_fmac_f64 %[hist], %[acc], %[m" #k "]\n"
+    hist = 0.0;
+    asm volatile(
+        "s_nop 4\n"
+        MDG_SMTICK(0) MDG_SMTICK(1) MDG_SMTICK(2) MDG_SMTICK(3) MDG_SMTICK(4) MDG_SMTICK(5)
+        MDG_SMTICK(6) MDG_SMTICK(7) MDG_SMTICK(8) MDG_SMTICK(9) MDG_SMTICK(10) MDG_SMTICK(11)
+        MDG_SMTICK(12) MDG_SMTICK(13) MDG_SMTICK(14) MDG_SMTICK(15)
+        : [acc] "+v"(acc), [hist] "+v"(hist)
+        : [A] "v"(A), [S] "v"(S), [one] "v"(one), [m0] "v"(mk[0]), [m1] "v"(mk[1]), [m2] "v"(mk[2]),
+          [m3] "v"(mk[3]), [m4] "v"(mk[4]), [m5] "v"(mk[5]), [m6] "v"(mk[6]), [m7] "v"(mk[7]),
+          [m8] "v"(mk[8]), [m9] "v"(mk[9]), [m10] "v"(mk[10]), [m11] "v"(mk[11]), [m12] "v"(mk[12]),
+          [m13] "v"(mk[13]), [m14] "v"(mk[14]), [m15] "v"(mk[15]));
+#undef MDG_SMTICK
+}
+
+bool smooth_small_ok(int N, int iters, int ws) {
+    return N <= kSmallN && N >= 4 * kSmMaxWS + 64 && iters >= 1 && iters <= kSmMaxP && ws >= 1 &&
+           ws <= kSmMaxWS;
+}
+
+__global__ __launch_bounds__(64 * (kSmMaxP + 1)) void k_smooth_small(BatchArgs a, Workspace w, int P, int WS,
+                                                             int fused_prep) {
+    __shared__ double yl[kSmallN];
+    __shared__ double ring[kSmMaxP - 1][kSmRing];
+    __shared__ int prog[kSmMaxP];  // ticks (outputs) pass p has published
+    __shared__ int fail;
+    constexpr int RM = kSmRing - 1;
+    const int s = blockIdx.x, N = a.N, tid = threadIdx.x, lane = tid & 63, p = tid >> 6;
+    KSTAMP(88);
+    // the row (decoded here from page-locked int32 rows for mdg_deconvolute_rows_i32:
+    // y = raw * scale, the reader's operation; the x and y rows the later launches
+    // read are written back)
+    double* yg = const_cast<double*>(y_row(a, s));
+    if (a.dec_rows) {
+        const int32_t* __restrict__ r = a.dec_rows[s];
+        const double sc = a.dec_desc[4 * s + 3];
+        for (int b0 = 0; b0 < N; b0 += kSmStage * (int)blockDim.x) {
+            double v[kSmStage];  // every load issued before the first store
+#pragma unroll
+            for (int j = 0; j < kSmStage; ++j) {
+                const int i = b0 + j * blockDim.x + tid;
+                v[j] = i < N ? (double)r[i] * sc : 0.0;
+            }
+#pragma unroll
+            for (int j = 0; j < kSmStage; ++j) {
+                const int i = b0 + j * blockDim.x + tid;
+                if (i < N) {
+                    yl[i] = v[j];
+                    yg[i] = v[j];
+                }
+            }
+        }
+        if (a.x_stride || s == 0) {
+            const double* xd = a.dec_desc + 4 * s;
+            double* xr = const_cast<double*>(a.x) + (size_t)s * a.x_stride;
+            for (int i = tid; i < N; i += blockDim.x) xr[i] = dec_x(xd, i);
+        }
+    } else {
+        for (int b0 = 0; b0 < N; b0 += kSmStage * (int)blockDim.x) {
+            double v[kSmStage];
+#pragma unroll
+            for (int j = 0; j < kSmStage; ++j) {
+                const int i = b0 + j * blockDim.x + tid;
+                v[j] = i < N ? yg[i] : 0.0;
+            }
+#pragma unroll
+            for (int j = 0; j < kSmStage; ++j) {
+                const int i = b0 + j * blockDim.x + tid;
+                if (i < N) yl[i] = v[j];
+            }
+        }
+    }
+    if (tid < kSmMaxP) prog[tid] = 0;
+    if (tid == 0) fail = 0;
+    __syncthreads();
+#ifdef MDG_DIAG
+    // HW_ID of each wave (SIMD in bits 5:4): stage_diag.py prints slots 150 + wave
+    if (lane == 0 && blockIdx.x == 0 && g_diag && p < 16)
+        g_diag[kDiagStampBase + 150 + p] = 1 + (long long)(unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));
+#endif
+    if (p >= P) {  // the extra wave: the spectrum's prep, off the passes' critical path
+        if (lane == 0 && fused_prep) prep_spectrum(a, w, s);
+        return;
+    }
+#ifdef MDG_DIAG
+    // per-pass stamps (tools/stage_diag.py --sim): slots 90 + 4p + {0 start, 1 steady, 2 tail, 3 end}
+#define SM_STAMP(k)                                                                           \
+    if (lane == 0 && blockIdx.x == 0 && g_diag && p < 8)                                      \
+    g_diag[kDiagStampBase + 90 + 4 * p + (k)] = (long long)__builtin_amdgcn_s_memtime()
+#else
+#define SM_STAMP(k)
+#endif
+    SM_STAMP(0);
+    const int R = WS / 2;
+    const double* in = p == 0 ? yl : ring[p - 1];
+    const int im = p == 0 ? 0x7fffffff : RM;  // index mask of the input
+    double* outr = p < P - 1 ? ring[p] : nullptr;
+    double* outg = w.smooth + (size_t)s * N;
+    int spins = 0;
+    // wait until the input holds indices < need, and (a ring output) until the next
+    // pass no longer needs the slots of indices < upto - kSmRing
+    auto wait_for = [&](int need, int upto) {
+        if (p > 0) {
+            while (lds_ld(&prog[p - 1]) < need) {
+                if (++spins > kSmSpins || lds_ld(&fail)) {
+                    if (lane == 0) fail = 1;
+                    return false;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        if (outr) {
+            while (lds_ld(&prog[p + 1]) < upto - kSmRing + WS + 1) {
+                if (++spins > kSmSpins || lds_ld(&fail)) {
+                    if (lane == 0) fail = 1;
+                    return false;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        return true;
+    };
+    // (a wave's LDS requests are served in order, so a reader that sees the count it
+    // stores after the outputs also sees the outputs)
+    auto publish = [&](int n) {
+        if (lane == 0) __hip_atomic_store(&prog[p], n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    auto emit = [&](int i, double v) {  // one output (scalar ticks)
+        if (lane == 0) {
+            if (outr) outr[i & RM] = v;
+            else outg[i] = v;
+        }
+        publish(i + 1);
+    };
+    bool ok = true;
+    double sum = 0.0, div = 1.0;
+    int len = 0;
+    // prefill: the first R values pushed (moving_average.rs:60-65)
+    ok = wait_for(R, 0);
+    for (int k = 0; ok && k < R; ++k) {
+        sum += in[k & im];
+        ++len;
+    }
+    const int nm = N - R;  // main ticks
+    int i = 0;
+    // the FIFO filling: no pop, div = 1/len
+    for (; ok && i < nm && len < WS; ++i) {
+        if (!(ok = wait_for(i + R + 1, i + 1))) break;
+        sum += in[(i + R) & im];
+        ++len;
+        div = 1.0 / (double)len;
+        emit(i, sum * div);
+    }
+    // steady: sixteen ticks per DPP block, kSmSuper blocks per wait and publication
+    // (their operands loaded together: one round of LDS latency per 64 ticks)
+    const double one = 1.0;
+    const int l = lane & 15;
+    double mk[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) mk[k] = l == k ? 1.0 : 0.0;
+    // one 16-tick block from index b; a block whose sum went non-finite (the capture
+    // multiplies every tick's sum by 0.0 or 1.0) is redone tick by tick
+    auto block = [&](int b, double A, double S) {
+        const double s0 = sum;
+        double hist;
+        sm_block16(sum, hist, A, S, one, mk);
+        if (!__builtin_isfinite(sum)) {
+            sum = s0;
+            hist = 0.0;
+            for (int k = 0; k < 16; ++k) {
+                sum += in[(b + R + k) & im];
+                sum -= in[(b + R - WS + k) & im];
+                if (l == k) hist = sum;
+            }
+        }
+        return hist;
+    };
+    SM_STAMP(1);
+    constexpr int kSmSuper = 4;
+#ifdef MDG_DIAG
+    // one superblock of pass 0 (the eighth) split: slots 160 wait, 161 waited, 162 loaded, 163 blocks, 164 published
+    int sbk = 0;
+#define SB_STAMP(k)                                                                           \
+    if (lane == 0 && blockIdx.x == 0 && g_diag && p == 0 && sbk == 8)                          \
+    g_diag[kDiagStampBase + 160 + (k)] = (long long)__builtin_amdgcn_s_memtime()
+#else
+#define SB_STAMP(k)
+#endif
+    // the next superblock's operands are loaded before this one's blocks run when the
+    // previous pass has already published them (no wait: a pass never blocks on its
+    // input while holding outputs back)
+    double A[kSmSuper], S[kSmSuper];
+    bool have = false;
+    auto load_super = [&](int b) {
+#pragma unroll
+        for (int u = 0; u < kSmSuper; ++u) {
+            A[u] = in[(b + 16 * u + R + l) & im];
+            S[u] = in[(b + 16 * u + R - WS + l) & im];
+        }
+    };
+    for (; ok && i + 16 * kSmSuper <= nm; i += 16 * kSmSuper) {
+        SB_STAMP(0);
+        if (!(ok = wait_for(have ? 0 : i + 16 * kSmSuper + R, i + 16 * kSmSuper))) break;
+        SB_STAMP(1);
+        if (!have) load_super(i);
+        double cA[kSmSuper], cS[kSmSuper];
+#pragma unroll
+        for (int u = 0; u < kSmSuper; ++u) {
+            cA[u] = A[u];
+            cS[u] = S[u];
+        }
+        const int nx = i + 32 * kSmSuper + R;
+        have = i + 32 * kSmSuper <= nm && (p == 0 || lds_ld(&prog[p - 1]) >= nx);
+        if (have) load_super(i + 16 * kSmSuper);
+#pragma unroll
+        for (int u = 0; u < kSmSuper; ++u) {
+            if (u == 0) SB_STAMP(2);
+            const double v = block(i + 16 * u, cA[u], cS[u]) * div;
+            if (lane < 16) {
+                if (outr) outr[(i + 16 * u + lane) & RM] = v;
+                else outg[i + 16 * u + lane] = v;
+            }
+        }
+        SB_STAMP(3);
+        publish(i + 16 * kSmSuper);
+        SB_STAMP(4);
+#ifdef MDG_DIAG
+        ++sbk;
+#endif
+    }
+#undef SB_STAMP
+    for (; ok && i + 16 <= nm; i += 16) {
+        if (!(ok = wait_for(i + 16 + R, i + 16))) break;
+        const double v = block(i, in[(i + R + l) & im], in[(i + R - WS + l) & im]) * div;
+        if (lane < 16) {
+            if (outr) outr[(i + lane) & RM] = v;
+            else outg[i + lane] = v;
+        }
+        publish(i + 16);
+    }
+    for (; ok && i < nm; ++i) {  // leftover steady ticks
+        if (!(ok = wait_for(i + R + 1, i + 1))) break;
+        sum += in[(i + R) & im];
+        sum -= in[(i + R - WS) & im];
+        emit(i, sum * div);
+    }
+    SM_STAMP(2);
+    // tail: pops only (moving_average.rs:76-81)
+    for (; ok && i < N; ++i) {
+        if (!(ok = wait_for(N, i + 1))) break;
+        if (len > 0) {
+            sum -= in[(i + R - WS) & im];
+            --len;
+            div = 1.0 / (double)len;
+            emit(i, sum * div);
+        }
+    }
+    if (!ok && lane == 0) w.status[s] = MDG_ERR_HIP;
+    SM_STAMP(3);
+#undef SM_STAMP
+}
+
+const char* launch_smooth_small(const BatchArgs& a, const Workspace& w, int iters, int ws, hipStream_t st,
+                                int fused_prep) {
+    launch_k(k_smooth_small, dim3(a.B), dim3(64 * (iters + 1)), 0, st, a, w, iters, ws, fused_prep);
+    return "k_smooth_small";
+}
+
 // look-back slots of k_peaks per spectrum (one per kPkSlotWords mask words)
 __device__ __forceinline__ int peak_slots(int W) { return (W + kPkSlotWords - 1) / kPkSlotWords; }
 __global__ void k_flags(BatchArgs a, Workspace w) {
@@ -3084,7 +3393,7 @@ __global__ void k_fit_update(BatchArgs a, Workspace w, int it) {
 // every (point, peak) term is evaluated by its own thread into LDS and each point's
 // thread then folds its row in peak order; otherwise each point's thread evaluates and
 // folds its P terms itself (fold_small).
-constexpr int kSmallN = 4096, kSmallP = 512, kSmallBS = 512, kSmallT = 6144;
+constexpr int kSmallP = 512, kSmallBS = 512, kSmallT = 6144;
 
 // acc + sum_j<P sfhw_j / (hw2_j + (x - maxp_j)^2), a left fold in j order (the adds
 // stay in order: the reference's bits); eight Lorentzians' parameters are read (LDS
@@ -4037,17 +4346,28 @@ static const char* launch_chain(const BatchArgs& a, const Workspace& w, int iter
 }
 // chain kernel (one CU per pass) for windows <= 8 and batches <= 512 (B * iters
 // <= 2048) when its buffers are set up and MDG_SMOOTH does not force another
+// small spectra (N <= kSmallN): k_smooth_small, one workgroup per spectrum (MDG_SMOOTH=small
+// forces it wherever its shape limits allow)
+bool smooth_uses_small(const BatchArgs& a, int iters, int ws, const EngineSwitches& sw) {
+    const bool ok = smooth_small_ok(a.N, iters, ws);
+    return ok && sw.smooth == EngineSwitches::SM_SMALL;  // MDG_SMOOTH=small only (slower, K1s)
+}
 bool smooth_uses_chain(const BatchArgs& a, const Workspace& w, int iters, int ws, const EngineSwitches& sw) {
     const bool chain = sw.smooth == EngineSwitches::SM_DEFAULT || sw.smooth == EngineSwitches::SM_CHAIN;
-    return chain && w.chain_P >= iters && chain_supported(a.B, a.N, iters, ws);
+    return chain && !smooth_uses_small(a, iters, ws, sw) && w.chain_P >= iters &&
+           chain_supported(a.B, a.N, iters, ws);
+}
+bool smooth_fuses_prep(const BatchArgs& a, const Workspace& w, int iters, int ws, const EngineSwitches& sw) {
+    return smooth_uses_small(a, iters, ws, sw) || smooth_uses_chain(a, w, iters, ws, sw);
 }
 const char* launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int ws, const EngineSwitches& sw,
                           hipStream_t st, int fused_prep) {
     // the chain kernel; then lane-pipelined (window fits the register FIFO); the
-    // one-lane-per-spectrum kernel otherwise.
-    // MDG_SMOOTH = chain | pipe | generic forces one (tests); an
-    // unsupported shape falls through. fused_prep (chain only): the chain kernel
+    // one-lane-per-spectrum kernel otherwise; small spectra k_smooth_small.
+    // MDG_SMOOTH = chain | pipe | generic | small forces one (tests); an
+    // unsupported shape falls through. fused_prep (chain and small only): the kernel
     // runs k_prep's work itself.
+    if (smooth_uses_small(a, iters, ws, sw)) return launch_smooth_small(a, w, iters, ws, st, fused_prep);
     if (smooth_uses_chain(a, w, iters, ws, sw)) {
         switch (ws) {
             case 2: return launch_chain<2>(a, w, iters, sw, st, fused_prep);

@@ -123,7 +123,7 @@ __device__ __host__ inline const double* y_row(const BatchArgs& a, int s) {
 // context's behaviour depend on when the variable was read).
 // (ints and char arrays only: no padding, the bytes are part of the graph keys)
 struct EngineSwitches {
-    enum { SM_DEFAULT = 0, SM_CHAIN, SM_PIPE, SM_GENERIC, SM_OTHER };
+    enum { SM_DEFAULT = 0, SM_CHAIN, SM_PIPE, SM_GENERIC, SM_OTHER, SM_SMALL };
     int smooth = SM_DEFAULT;     // MDG_SMOOTH = chain | pipe | generic (other values: the generic kernel)
     int chain_excl = 1;          // MDG_CHAIN_EXCL=0: never whole-CU chain workgroups
     int chain_l2ahead = 0;       // MDG_CHAIN_L2AHEAD: blocks each chain pulls into L2 ahead (0: by grid)
@@ -194,6 +194,9 @@ void launch_prep(const BatchArgs& a, const Workspace& w, hipStream_t st);
 void launch_diag_nop(const BatchArgs& a, const Workspace& w, const EngineSwitches& sw, hipStream_t st);
 #endif
 bool smooth_uses_chain(const BatchArgs& a, const Workspace& w, int iters, int ws, const EngineSwitches& sw);
+bool smooth_uses_small(const BatchArgs& a, int iters, int ws, const EngineSwitches& sw);
+// the smoother launch runs k_prep's work itself (k_smooth_chain, k_smooth_small)
+bool smooth_fuses_prep(const BatchArgs& a, const Workspace& w, int iters, int ws, const EngineSwitches& sw);
 const char* launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int ws, const EngineSwitches& sw,
                           hipStream_t st, int fused_prep = 0);
 void launch_flags(const BatchArgs& a, const Workspace& w, hipStream_t st);

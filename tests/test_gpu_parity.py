@@ -263,7 +263,9 @@ def test_fused_prep_after_failures_and_other_smoothers(monkeypatch, engine_env):
     """The chain smoother runs k_prep's work itself and never reads the status the
     previous run left; k_flags returns its progress counters to zero. On one
     context: a failing spectrum (NoPeaksDetected), then a good one, the same on
-    the lane-pipelined smoother, with k_prep launched separately, and the chain again --
+    the lane-pipelined smoother, on k_smooth_small (the 4096-point failing row; fused
+    prep on its extra wave; blood_07 is longer and takes the chain), with
+    k_prep launched separately, and the chain again --
     every result equal to the oracle."""
     c = nat.Context(0)
     st = oracle.default_settings()
@@ -272,7 +274,8 @@ def test_fused_prep_after_failures_and_other_smoothers(monkeypatch, engine_env):
     flat = np.full(n, 7.0)
     x, y, sb, cst, _ = load_case("blood_07")
     o = oracle.deconvolute(x, y, sb, cst)
-    for smooth, prep in [("chain", None), ("pipe", None), ("chain", "separate"), ("chain", None)]:
+    for smooth, prep in [("chain", None), ("pipe", None), ("small", None), ("chain", "separate"),
+                         ("chain", None)]:
         engine_env.setenv("MDG_SMOOTH", smooth)
         if prep:
             engine_env.setenv("MDG_PREP", prep)
@@ -1122,3 +1125,41 @@ def test_small_spectra_take_the_one_launch_fit(ctx, selector, forced, monkeypatc
     for k, (x, y, sb, _, _) in enumerate(data):
         o = oracle.deconvolute(x, y, sb, st)
         check_against(o.params, o.mse, status[k], counts[k], out[k], mse[k])
+
+
+@pytest.mark.parametrize("n,b,it,ws", [(192, 1, 1, 2), (193, 3, 2, 2), (500, 2, 3, 3), (2048, 4, 3, 3),
+                                       (2048, 1, 10, 7), (3001, 5, 15, 31), (4096, 2, 4, 32),
+                                       (4096, 1, 3, 5), (1000, 2, 9, 4)])
+def test_small_smoother_shapes(ctx, n, b, it, ws, monkeypatch, engine_env):
+    """k_smooth_small (N <= 4096: one workgroup per spectrum, one wave per pass, the
+    passes handing 16-tick blocks over through LDS rings): smoothed rows equal the
+    oracle's moving average bit for bit at the edges of its range -- the shortest rows
+    it takes, lengths off the 16-tick grid, 1 to 15 passes, windows 2 to 32. Selected
+    with MDG_SMOOTH=small: measured slower than k_smooth_chain, not the default."""
+    rng = np.random.default_rng(n + ws)
+    t = np.linspace(0, 1, n)
+    ys = rng.normal(0, 1, (b, n)) * 10.0 ** rng.integers(0, 6, (b, 1)) + 1e4 * np.sin(40 * t)[None, :]
+    engine_env.setenv("MDG_SMOOTH", "small")
+    rows = _smooth_rows(ctx, ys, it, ws)
+    assert ctx.stage_kernels()["smooth"] == "k_smooth_small"
+    for s, row in enumerate(rows):
+        assert np.array_equal(row, oracle.moving_average(ys[s], it, ws)), (n, b, it, ws, s)
+
+
+@pytest.mark.parametrize("smooth", [None, "small"])
+def test_small_spectra_compact_rows_through_the_python_surface(smooth, engine_env):
+    """The sim spectra as the Bruker reader keeps them (int32 samples decoded by the
+    smoother launch itself from page-locked memory) through Deconvoluter: one at a
+    time and the 16 as one set, against the sim_XX_harness goldens -- with the
+    default smoother and with k_smooth_small."""
+    import metabodecon as md
+    if smooth:
+        engine_env.setenv("MDG_SMOOTH", smooth)
+    sims = md.Spectrum.read_bruker_set(os.path.join(GOLDEN, "bruker", "sim"), 10, 10, (3.34, 3.56))
+    dec = md.Deconvoluter()
+    res = dec.par_deconvolute_spectra(sims)
+    one = [dec.deconvolute_spectrum(sims[k]) for k in (0, 9)]
+    for k, d in list(enumerate(res)) + [(0, one[0]), (9, one[1])]:
+        g = np.load(os.path.join(GOLDEN, "expected", f"sim_{k + 1:02d}_harness.npz"))
+        assert np.array_equal(d.params, g["params"]), k
+        assert abs(d.mse - float(g["mse"])) <= MSE_RTOL * abs(float(g["mse"])), k

@@ -59,13 +59,17 @@ def main():
     d = diag[STAMPS:].cpu().tolist()
     groups = {"select": range(10, 19), "peaks": range(0, 5), "fit_dpp": range(20, 24),
               "mse": range(30, 36), "window_mean": [45, 46, 40, 41, 42], "window_var": [55, 56, 50, 51, 52],
-              "small": range(70, 78), "window_small_mse": [65, 66, 60, 61, 62]}
+              "small": range(70, 78), "window_small_mse": [65, 66, 60, 61, 62],
+              "smooth_small": [88] + list(range(90, 102)), "smooth_small_sb": range(160, 165)}
     for name, r in groups.items():
         v = [d[k] for k in r]
         if not any(v):
             continue
         t0 = v[0]
         print(f"{name:10s}", " ".join(f"s{k}:{(d[k] - t0) if d[k] else '-'}" for k in r))
+    hw = [d[150 + k] - 1 for k in range(16) if d[150 + k]]
+    if hw:  # k_smooth_small's waves: (CU, SIMD) of each
+        print("smooth_small waves (cu,simd):", " ".join(f"({(v >> 8) & 15},{(v >> 4) & 3})" for v in hw))
     print("window fallbacks mean/var (3 runs):", d[47], d[57])
 
 
