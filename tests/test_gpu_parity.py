@@ -1146,6 +1146,35 @@ def test_small_smoother_shapes(ctx, n, b, it, ws, monkeypatch, engine_env):
         assert np.array_equal(row, oracle.moving_average(ys[s], it, ws)), (n, b, it, ws, s)
 
 
+def _same_bits_or_nan(a, b):
+    na, nb = np.isnan(a), np.isnan(b)
+    return np.array_equal(na, nb) and np.array_equal(a[~na].view(np.uint64), b[~nb].view(np.uint64))
+
+
+@pytest.mark.parametrize("path", ["chain", "small", "pipe"])
+def test_smoothers_on_non_finite_rows(ctx, path, engine_env):
+    """Intensities are not checked for finiteness (neither here nor in the reference),
+    so infinities and NaNs reach the moving average: every smoother keeps the IEEE
+    results of the reference's adds -- NaN where the oracle has NaN, the same bits
+    elsewhere. For k_smooth_small this is its redo path: a 16-tick DPP block whose sum
+    went non-finite is recomputed tick by tick (its 0/1 capture would turn inf * 0 into
+    NaN)."""
+    engine_env.setenv("MDG_SMOOTH", path)
+    n = 2048
+    rng = np.random.default_rng(7)
+    ys = rng.normal(0, 1, (4, n)) + 1e3 * np.sin(np.linspace(0, 30, n))[None, :]
+    ys[0, n - 40] = np.nan
+    ys[1, n - 100] = np.inf
+    ys[1, n - 60] = -np.inf
+    ys[2, 700:703] = 1.5e308  # the running sum overflows mid-row and stays infinite
+    ys[3, 1000] = -np.inf
+    rows = _smooth_rows(ctx, ys, 3, 5)
+    if path == "small":
+        assert ctx.stage_kernels()["smooth"] == "k_smooth_small"
+    for s, row in enumerate(rows):
+        assert _same_bits_or_nan(row, oracle.moving_average(ys[s], 3, 5)), (path, s)
+
+
 @pytest.mark.parametrize("smooth", [None, "small"])
 def test_small_spectra_compact_rows_through_the_python_surface(smooth, engine_env):
     """The sim spectra as the Bruker reader keeps them (int32 samples decoded by the
