@@ -573,7 +573,9 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
             kn[ST_SMOOTH] = launch_smooth(a, w, sm_it, sm_ws, sw, st, fused_prep ? 1 : 0);
         }
     }
-    {
+    // small spectra: the detection runs inside the selection's workgroup
+    const bool det_fused = detect_fused(a, det_only, sw);
+    if (!det_fused) {
         StageTimer t(c, ST_DETECT);
         for (int r = reps("detect"); r > 0; --r) {
             launch_flags(a, w, st);
@@ -582,7 +584,9 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     }
     {
         StageTimer t(c, ST_SELECT);
-        for (int r = reps("select"); r > 0; --r) kn[ST_SELECT] = launch_select(a, w, det_only, s->threshold, st);
+        for (int r = reps("select"); r > 0; --r)
+            kn[ST_SELECT] = launch_select(a, w, det_only, s->threshold, st, det_fused);
+        if (det_fused) kn[ST_DETECT] = kn[ST_SELECT];
     }
     const bool small_fit = fit_is_small(a, sw);
     if (small_fit) {  // every iteration in one launch
@@ -856,6 +860,8 @@ EngineSwitches mdg::read_engine_switches() {
     w.chain_l2ahead = std::max(0, num("MDG_CHAIN_L2AHEAD", 0));
     const std::string pk = str("MDG_PEAKS");
     w.peaks = pk.empty() ? 0 : pk == "fine" ? 1 : 2;
+    const std::string dt = str("MDG_DETECT");
+    w.detect = dt == "separate" ? 1 : dt == "fused" ? 2 : 0;
     const std::string f = str("MDG_FITSUP");
     copy(w.fitsup, sizeof(w.fitsup), "");
     if (f == "tf" || f == "tf12" || f == "tw7" || f == "tw3s" || f == "twf" || f == "twf1" || f == "twf3s" ||

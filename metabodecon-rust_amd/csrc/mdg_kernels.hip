@@ -1672,12 +1672,15 @@ __device__ __forceinline__ bool in_ignore(int v, const int64_t* pairs, int n) {
 // The peaks of one mask word (64 points) whose centre bits are in sel, in centre
 // order: borders by bit scans, the detector-only and ignore-region filters. Counts
 // the bordered peaks; returns the kept ones, writing them at out.. when WRITE.
-template <bool WRITE>
+// (LDSM: the masks are the caller's copy in LDS, mlds, laid out as w.masks' row;
+// GOUT = false: WRITE fills only the pk copy, not the global peak rows)
+template <bool WRITE, bool LDSM = false, bool GOUT = true>
 __device__ __forceinline__ int word_peaks(const BatchArgs& a, const Workspace& w, int s, int wd, uint64_t sel,
                                           int detector_only, int* bordered, size_t out,
-                                          int* pk = nullptr, int pcap = 0, int po = 0) {
+                                          int* pk = nullptr, int pcap = 0, int po = 0,
+                                          const uint64_t* mlds = nullptr) {
     const int N = a.N, W = w.W;
-    const uint64_t* mc = w.masks + (size_t)s * 3 * W;
+    const uint64_t* mc = LDSM ? mlds : w.masks + (size_t)s * 3 * W;
     const uint64_t* mr = mc + W;
     const uint64_t* ml = mc + 2 * W;
     const int64_t* pairs = w.ig + (size_t)s * 2 * w.ig_cap;
@@ -1715,9 +1718,11 @@ __device__ __forceinline__ int word_peaks(const BatchArgs& a, const Workspace& w
         if (keep && a.n_ignore > 0) keep = !(in_ignore(l, pairs, nig) || in_ignore(r, pairs, nig));
         if (!keep) continue;
         if constexpr (WRITE) {
-            w.det_l[out + kept] = l;
-            w.det_c[out + kept] = c;
-            w.det_r[out + kept] = r;
+            if constexpr (GOUT) {
+                w.det_l[out + kept] = l;
+                w.det_c[out + kept] = c;
+                w.det_r[out + kept] = r;
+            }
             if (pk && po + kept < pcap) {  // the chunk's copy for its scoring (LDS)
                 pk[po + kept] = l;
                 pk[pcap + po + kept] = c;
@@ -2259,7 +2264,7 @@ __device__ __noinline__ double seg_fold(double acc, const double* __restrict__ t
 // t: global memory or LDS (a generic pointer: the windowed fold of k_select reads its
 // LDS-staged terms through it)
 template <int BS>
-__device__ double window_fold(double acc0, WinLds& L, const double* __restrict__ t, int n,
+__device__ __forceinline__ double window_fold(double acc0, WinLds& L, const double* __restrict__ t, int n,
                               int stamp = 40) {
     constexpr int NW = BS / 64;
     static_assert(kWinSeg <= 64, "one lane per segment in the prefix scan");
@@ -2448,7 +2453,85 @@ constexpr int kSelLds = 4096;          // 3 ints each: 48 KB of the same buffer
 constexpr int kSelCountDirect = 1;
 constexpr int kSelPerThread = 16;      // candidates per thread compacted from registers
 static_assert(3 * kSelLds * sizeof(int) <= kSfrLds * sizeof(double), "selection fits the SFR buffer");
+// K3s  detection of a SMALL spectrum (N <= kSmallN) inside k_select's workgroup (DET):
+// k_flags' predicates over the row staged in LDS (ys), the masks in LDS, k_peaks'
+// word scans and scoring (word_peaks, score_peak_lds: the same operations in the same
+// order), the peaks written where k_peaks writes them. Two launches and their
+// boundaries fewer for the reference's own benchmark spectra (sim, 2048 points:
+// k_flags 4.7 + k_peaks 10 us of dependent launches, round 6). Returns the kept
+// count, or -1 with the status set (NoPeaksDetected) when no peak has both borders.
+constexpr int kDetW = kSmallN / 64;  // mask words of a small spectrum
 template <int BS>
+__device__ __forceinline__ int detect_small(const BatchArgs& a, const Workspace& w, int s, double* ys, int* pk,
+                                            int* park, double* scl, uint64_t* mlds, int* lds_i, long long* lds_l) {
+    static_assert(BS >= 4 * kDetW, "four threads per mask word");
+    const int N = a.N, W = w.W, tid = threadIdx.x, lane = tid & 63;
+    const double* __restrict__ sm = w.smooth_ptr + (size_t)s * w.smooth_stride;
+    KSTAMP(80);
+    for (int k = tid; k < N; k += BS) ys[k] = sm[k];
+    __syncthreads();
+    KSTAMP(81);
+    // k_flags: centre, right-border and left-border predicates, one ballot per word
+    for (int k = tid; k < 64 * W; k += BS) {
+        bool fc = false, fr = false, fl = false;
+        if (k >= 2 && k <= N - 3) {
+            const double dm = dsd(ys, k - 1), d0 = dsd(ys, k), dp = dsd(ys, k + 1);
+            fc = d0 < 0. && d0 < dm && d0 < dp;
+            fr = d0 > dm && (d0 >= dp || (d0 < 0. && dp >= 0.));
+            fl = d0 > dp && (d0 >= dm || (d0 < 0. && dm >= 0.));
+        }
+        const uint64_t bc = __ballot(fc), br = __ballot(fr), bl = __ballot(fl);
+        if (lane == 0) {
+            mlds[k >> 6] = bc;
+            mlds[W + (k >> 6)] = br;
+            mlds[2 * W + (k >> 6)] = bl;
+        }
+    }
+    __syncthreads();
+    KSTAMP(82);
+    // k_peaks: four threads per mask word in centre order, each thread's kept peaks
+    // (at most 8 of its 16 centre bits: strict minima) parked in its own slots of
+    // park and moved to their places after the scan (one word pass, not two)
+    const int wd = tid >> 2;
+    const uint64_t sel = 0xffffull << (16 * (tid & 3));
+    constexpr int PARK = 4 * kDetW * 8;
+    int bordered = 0, kept = 0;
+    if (wd < W) kept = word_peaks<true, true, false>(a, w, s, wd, sel, 0, &bordered, 0, park, PARK, 8 * tid, mlds);
+    int total;
+    const int o = block_exclusive_scan<BS>(kept, lds_i, &total);
+    const long long b_all = block_sum_ll<BS>(bordered, lds_l);
+    if (b_all == 0) {
+        if (tid == 0) w.status[s] = MDG_NO_PEAKS_DETECTED;
+        return -1;
+    }
+    if (tid == 0) w.det_count[s] = total;
+    KSTAMP(83);
+    const size_t b0 = (size_t)s * w.capD;
+    constexpr int PCAP = kSmallN / 2;  // centres are strict minima
+    for (int i = 0; i < kept; ++i) {
+        const int l = park[8 * tid + i], c = park[PARK + 8 * tid + i], r = park[2 * PARK + 8 * tid + i];
+        w.det_l[b0 + o + i] = l;
+        w.det_c[b0 + o + i] = c;
+        w.det_r[b0 + o + i] = r;
+        pk[o + i] = l;
+        pk[PCAP + o + i] = c;
+        pk[2 * PCAP + o + i] = r;
+    }
+    __syncthreads();
+    KSTAMP(84);
+    // l >= 2 and r <= N - 3: every score's ticks l - 1 .. r + 1 lie in the staged row;
+    // the selection reads the LDS copies (scl over the parking slots, free by now)
+    for (int p = tid; p < total; p += BS) {
+        const double sc = score_peak_lds(ys, 0, pk[p], pk[PCAP + p], pk[2 * PCAP + p]);
+        w.scores[b0 + p] = sc;
+        scl[p] = sc;
+    }
+    __syncthreads();
+    KSTAMP(85);
+    return total;
+}
+
+template <int BS, bool DET = false>
 __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double threshold) {
     const int s = blockIdx.x;
     __shared__ int lds_i[BS / 64 + 1];
@@ -2458,19 +2541,37 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
     __shared__ double thr_sh;
     __shared__ WinLds wl;
     // the spectrum's scalars in one memory round trip (as fit_head)
-    const int st = w.status[s], P = w.det_count[s];
+    int st, P;
     const int64_t sbi0 = w.sbi[2 * s], sbi1 = w.sbi[2 * s + 1];
-    asm volatile("" ::"s"(st), "s"(P), "s"(sbi0), "s"(sbi1));
-    if (st) return;
+    // DET: the row, the peaks and the parking slots (then the scores) in the SFR buffer,
+    // free until the staging; that overwrites the row only (n_sfr <= P <= kSmallN / 2)
+    constexpr int kPk = 3 * (kSmallN / 2) / 2, kPark = 3 * (4 * kDetW * 8) / 2;  // doubles
+    static_assert(kSmallN + kPk + kPark <= kSfrLds, "row and peaks in the SFR buffer");
+    int* const dpk = (int*)(sfr_lds + kSmallN);
+    double* const dsc = sfr_lds + kSmallN + kPk;
+    if constexpr (DET) {
+        __shared__ uint64_t mlds[3 * kDetW];
+        st = w.status[s];
+        // k_flags' duty: the smoother's progress counters back to zero (any status)
+        if ((int)threadIdx.x < w.chain_P) w.chain_flags[((size_t)s * w.chain_P + threadIdx.x) * 32] = 0;
+        if (st) return;
+        P = detect_small<BS>(a, w, s, sfr_lds, dpk, (int*)dsc, dsc, mlds, lds_i, lds_l);
+        if (P < 0) return;
+    } else {
+        st = w.status[s];
+        P = w.det_count[s];
+        asm volatile("" ::"s"(st), "s"(P), "s"(sbi0), "s"(sbi1));
+        if (st) return;
+    }
     if (P == 0) {  // peaks.len() - 1 underflows in peak_region_boundaries
         if (threadIdx.x == 0) w.status[s] = MDG_REFERENCE_PANIC;
         return;
     }
     const size_t base = (size_t)s * w.capD;
-    const int* pl = w.det_l + base;
-    const int* pc = w.det_c + base;
-    const int* pr = w.det_r + base;
-    double* scores = w.scores + base;
+    const int* pl = DET ? dpk : w.det_l + base;
+    const int* pc = DET ? dpk + kSmallN / 2 : w.det_c + base;
+    const int* pr = DET ? dpk + kSmallN : w.det_r + base;
+    const double* scores = DET ? dsc : w.scores + base;
     KSTAMP(10);
     // #(center <= sbi0) and #(center <= sbi1) over the ascending centers (scores:
     // k_peaks), both counts packed in one sum: up to kSelCountDirect centers per
@@ -2603,10 +2704,17 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
         // the kept ones of the wave's earlier rounds and its lanes below it in round u
         const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
         const int wbase = left + 64 * per * wv;
+        // the rounds this wave has candidates in (wave-uniform): a short candidate range
+        // (the sim spectra: ~100) leaves most waves none and the others one round, and
+        // each skipped round is 4 loads per lane fewer (sim_01: compaction 13.4k cycles)
+        const int nu = min(per, max(0, (right - wbase + 63) >> 6));
         double sc[kSelPerThread];  // the scores stay in VGPRs; the ballots are redone
 #pragma unroll
-        for (int u = 0; u < kSelPerThread; ++u) sc[u] = scores[min(wbase + 64 * u + lane, P - 1)];
-        auto kept = [&](int u) { return u < per && wbase + 64 * u + lane < right && sc[u] >= thr; };
+        for (int u = 0; u < kSelPerThread; ++u) {
+            sc[u] = 0.0;
+            if (u < nu) sc[u] = scores[min(wbase + 64 * u + lane, P - 1)];
+        }
+        auto kept = [&](int u) { return u < nu && wbase + 64 * u + lane < right && sc[u] >= thr; };
         int wcount = 0;
 #pragma unroll
         for (int u = 0; u < kSelPerThread; ++u) wcount += __popcll(__ballot(kept(u)));
@@ -2618,13 +2726,17 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
 #pragma unroll
         for (int u = 0; u < kSelPerThread; ++u) {
             const int q = min(wbase + 64 * u + lane, P - 1);
-            lv[u] = kept(u) ? pl[q] : 0;
-            cv[u] = kept(u) ? pc[q] : 0;
-            rv[u] = kept(u) ? pr[q] : 0;
+            lv[u] = cv[u] = rv[u] = 0;
+            if (u < nu) {
+                lv[u] = kept(u) ? pl[q] : 0;
+                cv[u] = kept(u) ? pc[q] : 0;
+                rv[u] = kept(u) ? pr[q] : 0;
+            }
         }
         int o = wstart;
 #pragma unroll
         for (int u = 0; u < kSelPerThread; ++u) {
+            if (u >= nu) continue;  // (not break: the loop must unroll, or the arrays go to scratch)
             const uint64_t bu = __ballot(kept(u));
             if (bu >> lane & 1) {
                 const int pos = o + __builtin_amdgcn_mbcnt_hi((unsigned)(bu >> 32),
@@ -4420,11 +4532,20 @@ const char* launch_peaks(const BatchArgs& a, const Workspace& w, int detector_on
     launch_k(k_peaks<256, 1024>, dim3(cdiv(w.W, 256), a.B), dim3(1024), 0, st, a, w, detector_only, 1);
     return "k_flags+k_peaks<256>";
 }
+// detection inside k_select (k_select<1024, true>): small spectra, the noise-score
+// selector (MDG_DETECT = separate | fused forces either where the shape allows)
+bool detect_fused(const BatchArgs& a, int detector_only, const EngineSwitches& sw) {
+    return !detector_only && a.N <= kSmallN && sw.detect != 1;
+}
 const char* launch_select(const BatchArgs& a, const Workspace& w, int detector_only,
-                          double threshold, hipStream_t st) {
+                          double threshold, hipStream_t st, bool fused) {
     if (detector_only) {
         launch_k(k_select_detector_only, dim3(16, a.B), dim3(256), 0, st, a, w);
         return "k_select_detector_only";
+    }
+    if (fused) {
+        launch_k(k_select<1024, true>, dim3(a.B), dim3(1024), 0, st, a, w, threshold);
+        return "k_select<1024, det>";
     }
     launch_k(k_select<1024>, dim3(a.B), dim3(1024), 0, st, a, w, threshold);
     return "k_select<1024>";

@@ -128,6 +128,7 @@ struct EngineSwitches {
     int chain_excl = 1;          // MDG_CHAIN_EXCL=0: never whole-CU chain workgroups
     int chain_l2ahead = 0;       // MDG_CHAIN_L2AHEAD: blocks each chain pulls into L2 ahead (0: by grid)
     int peaks = 0;               // MDG_PEAKS: 0 by batch size, 1 fine, 2 coarse (any other value)
+    int detect = 0;              // MDG_DETECT: 0 by shape (N <= 4096: inside k_select), 1 separate, 2 fused
     char fitsup[8] = {};         // MDG_FITSUP: a shipped fit kernel's name ("": by batch size)
     int tw_g = 0;                // MDG_TW_G: term-fold workgroups (0: the kernel's default)
     int gfit = 24;               // MDG_GFIT: k_fit_sup workgroups per spectrum
@@ -202,8 +203,11 @@ const char* launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int
 void launch_flags(const BatchArgs& a, const Workspace& w, hipStream_t st);
 const char* launch_peaks(const BatchArgs& a, const Workspace& w, int detector_only, const EngineSwitches& sw,
                          hipStream_t st);
+// small spectra with the noise-score selector: detection inside k_select (no k_flags,
+// no k_peaks launch)
+bool detect_fused(const BatchArgs& a, int detector_only, const EngineSwitches& sw);
 const char* launch_select(const BatchArgs& a, const Workspace& w, int detector_only,
-                          double threshold, hipStream_t st);
+                          double threshold, hipStream_t st, bool fused = false);
 // returns true when the launched kernel also did the stencil update (no k_fit_update)
 bool fit_sup_fused(const BatchArgs& a, const EngineSwitches& sw);
 // small spectra (N <= kSmallN, or MDG_FITSUP=small): every fit iteration in one launch

@@ -1146,6 +1146,47 @@ def test_small_smoother_shapes(ctx, n, b, it, ws, monkeypatch, engine_env):
         assert np.array_equal(row, oracle.moving_average(ys[s], it, ws)), (n, b, it, ws, s)
 
 
+@pytest.mark.parametrize("detect", ["fused", "separate"])
+def test_small_spectra_detection_inside_select(ctx, detect, engine_env):
+    """Spectra of <= 4096 points run the detection inside k_select's workgroup
+    (k_flags' predicates and k_peaks' word scans and scores over the row staged in LDS;
+    MDG_DETECT=separate keeps the two launches): the 16 sim spectra at the harness's
+    boundaries as one batch equal their goldens and the detected triples the oracle's;
+    an ignore region inside the signal region, and the statuses the detection and
+    selection raise (no peaks, no signal-free peaks, no signal peaks), equal the
+    oracle's."""
+    engine_env.setenv("MDG_DETECT", detect)
+    data = [load_case(f"sim_{k:02d}_harness") for k in range(1, 17)]
+    x, st = data[0][0], data[0][3]
+    ys = np.stack([d[1] for d in data])
+    status, counts, out, mse = gpu_batch(ctx, x, ys, [d[2] for d in data], st)
+    want = "k_select<1024, det>" if detect == "fused" else "k_flags+k_peaks<64>"
+    assert ctx.stage_kernels()["detect"] == want
+    for k in range(16):
+        g = np.load(os.path.join(GOLDEN, "expected", f"sim_{k + 1:02d}_harness.npz"))
+        check_against(g["params"], float(g["mse"]), status[k], counts[k], out[k], mse[k])
+    det = ctx.last_peaks(15, "detected").astype(np.int64)
+    l, c, r = oracle.detect_peaks(oracle.second_derivative(oracle.moving_average(ys[15], 3, 3)))
+    assert np.array_equal(det, np.stack([l, c, r], axis=1))
+    # an ignore region over part of the signal region
+    sb = data[0][2]
+    ign = ((3.40, 3.45),)
+    o = oracle.deconvolute(x, ys[0], sb, st, ignore=ign)
+    status, counts, out, mse = gpu_batch(ctx, x, ys[:1], [sb], st, ignore=ign)
+    check_against(o.params, o.mse, status[0], counts[0], out[0], mse[0], o.status)
+    # statuses: a flat row, peaks only inside the signal region, peaks only outside it
+    n = x.size
+    t = np.arange(n, dtype=np.float64)
+    lor = lambda c0: 1e4 / (1.0 + ((t - c0) / 3.0) ** 2)
+    inside = float(np.searchsorted(-x, -0.5 * (sb[0] + sb[1])))
+    rows = np.stack([np.full(n, 5.0), lor(inside), lor(200.0) + lor(1800.0)])
+    status, counts, out, mse = gpu_batch(ctx, x, rows, [sb], st)
+    for k in range(rows.shape[0]):
+        o = oracle.deconvolute(x, rows[k], sb, st)
+        assert status[k] == o.status, (k, status[k], o.status)
+        assert o.status != 0, k
+
+
 def _same_bits_or_nan(a, b):
     na, nb = np.isnan(a), np.isnan(b)
     return np.array_equal(na, nb) and np.array_equal(a[~na].view(np.uint64), b[~nb].view(np.uint64))

@@ -121,6 +121,19 @@ def test_protocol_kernels_use_no_scratch_and_no_scalar_writes(isa):
                          text, re.M)
 
 
+def test_no_kernel_uses_scratch(isa):
+    """Every kernel of the library keeps its arrays in registers or LDS: an unrolled
+    loop that stops unrolling (a `break` in k_select's compaction did, round 6) moves
+    its per-round arrays to the scratch stack, 208 bytes there and a 35 -> 48 us
+    selection on blood_01; a non-inlined helper call adds a stack frame."""
+    text = "\n".join(isa)
+    kernels = re.findall(r"\.amdhsa_kernel (\S+)\n(.*?)\.end_amdhsa_kernel", text, re.S | re.M)
+    assert len(kernels) > 20
+    bad = [name for name, body in kernels
+           if not re.search(r"\.amdhsa_private_segment_fixed_size 0\b", body)]
+    assert not bad, bad
+
+
 def test_checker_flags_a_spill_in_a_guarded_region():
     """Power of the check above on a planted case: a lane-guarded atomic with an SGPR
     reload inside its region is found; the same atomic with the reload before the

@@ -60,7 +60,8 @@ def main():
     groups = {"select": range(10, 19), "peaks": range(0, 5), "fit_dpp": range(20, 24),
               "mse": range(30, 36), "window_mean": [45, 46, 40, 41, 42], "window_var": [55, 56, 50, 51, 52],
               "small": range(70, 78), "window_small_mse": [65, 66, 60, 61, 62],
-              "smooth_small": [88] + list(range(90, 102)), "smooth_small_sb": range(160, 165)}
+              "smooth_small": [88] + list(range(90, 102)), "smooth_small_sb": range(160, 165),
+              "det_small": range(80, 86)}
     for name, r in groups.items():
         v = [d[k] for k in r]
         if not any(v):
