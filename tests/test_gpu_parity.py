@@ -1152,7 +1152,8 @@ def test_small_spectra_detection_inside_select(ctx, detect, engine_env):
     (k_flags' predicates and k_peaks' word scans and scores over the row staged in LDS;
     MDG_DETECT=separate keeps the two launches): the 16 sim spectra at the harness's
     boundaries as one batch equal their goldens and the detected triples the oracle's;
-    an ignore region inside the signal region, and the statuses the detection and
+    an ignore region inside the signal region, 4096 noisy points whose ~1500 peaks send
+    the selection's folds down the windowed path, and the statuses the detection and
     selection raise (no peaks, no signal-free peaks, no signal peaks), equal the
     oracle's."""
     engine_env.setenv("MDG_DETECT", detect)
@@ -1174,6 +1175,18 @@ def test_small_spectra_detection_inside_select(ctx, detect, engine_env):
     o = oracle.deconvolute(x, ys[0], sb, st, ignore=ign)
     status, counts, out, mse = gpu_batch(ctx, x, ys[:1], [sb], st, ignore=ign)
     check_against(o.params, o.mse, status[0], counts[0], out[0], mse[0], o.status)
+    # 4096 points of noise around a few peaks, a narrow signal region: > 1024
+    # signal-free-region scores, so the selection's folds take the windowed path
+    rng = np.random.default_rng(11)
+    n4 = 4096
+    x4 = np.linspace(10.0, 0.0, n4)
+    t4 = np.arange(n4, dtype=np.float64)
+    y4 = rng.normal(0, 1, n4) + sum(3e3 / (1.0 + ((t4 - c0) / 4.0) ** 2) for c0 in (2000, 2050, 2110))
+    st4 = oracle.make_settings(smoother="identity")  # the noise peaks unsmoothed: ~1500
+    o = oracle.deconvolute(x4, y4, (5.3, 4.6), st4)
+    assert o.status == 0 and o.n_detected > 1400
+    status, counts, out, mse = gpu_batch(ctx, x4, y4[None, :], [(5.3, 4.6)], st4)
+    check_against(o.params, o.mse, status[0], counts[0], out[0], mse[0])
     # statuses: a flat row, peaks only inside the signal region, peaks only outside it
     n = x.size
     t = np.arange(n, dtype=np.float64)
