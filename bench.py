@@ -231,7 +231,7 @@ def hbm_pipeline(tag, batch, iterations, value, n):
     produces `value`. None when no summary is committed."""
     # (round 5: the queue reads each submission's row in place -- no k_queue_gather)
     launches = {"k_smooth_chain<3, false>": 1, "k_flags": 1,
-                "k_peaks<256, 1024>": 1, "k_select<1024>": 1, "k_fit_sup": iterations,
+                "k_peaks<256, 1024>": 1, "k_select<1024, false>": 1, "k_fit_sup": iterations,
                 "k_fit_update": iterations, "k_mse_local<4, 30>": 1, "k_queue_scatter": 1}
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{tag}.json")),
                        reverse=True):

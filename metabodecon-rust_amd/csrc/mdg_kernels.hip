@@ -2875,6 +2875,39 @@ __device__ __forceinline__ void solve(const Stencil& q, double* out3) {
     out3[2] = m;
 }
 
+// Stencil rows (round 6): per spectrum an x plane (x1 x2 x3 of each peak, 3 capD
+// doubles) followed by a y plane (y1 y2 y3). An update rewrites the three y values
+// and, of the x values, only the one mirror_shoulder replaced (x2 never changes):
+// with the six values of a peak in one 48-byte record the unchanged x values shared
+// the written lines, so every update rewrote all of them (k_fit_update: 144 bytes per
+// peak and iteration moved)
+__device__ __forceinline__ double* stencil_x(const Workspace& w, size_t base, int p) {
+    return w.stencil + 6 * base + 3 * (size_t)p;
+}
+__device__ __forceinline__ double* stencil_y(const Workspace& w, size_t base, int p) {
+    return w.stencil + 6 * base + 3 * (size_t)w.capD + 3 * (size_t)p;
+}
+__device__ __forceinline__ Stencil load_stencil(const Workspace& w, size_t base, int p) {
+    const double* sx = stencil_x(w, base, p);
+    const double* sy = stencil_y(w, base, p);
+    return Stencil{sx[0], sx[1], sx[2], sy[0], sy[1], sy[2]};
+}
+__device__ __forceinline__ void store_stencil(const Workspace& w, size_t base, int p, const Stencil& q) {
+    double* sx = stencil_x(w, base, p);
+    double* sy = stencil_y(w, base, p);
+    sx[0] = q.x1; sx[1] = q.x2; sx[2] = q.x3;
+    sy[0] = q.y1; sy[1] = q.y2; sy[2] = q.y3;
+}
+// q: the updated stencil of peak p, x1 / x3 as it held them before (old1 / old3)
+__device__ __forceinline__ void store_updated_stencil(const Workspace& w, size_t base, int p, const Stencil& q,
+                                                      double old1, double old3) {
+    double* sx = stencil_x(w, base, p);
+    double* sy = stencil_y(w, base, p);
+    if (__double_as_longlong(q.x1) != __double_as_longlong(old1)) sx[0] = q.x1;
+    if (__double_as_longlong(q.x3) != __double_as_longlong(old3)) sx[2] = q.x3;
+    sy[0] = q.y1; sy[1] = q.y2; sy[2] = q.y3;
+}
+
 // selected peak p of spectrum s with borders (l, c, r): its reduced points, the
 // mirrored stencil and the initial parameters (version 0)
 __device__ __forceinline__ void fit_init_peak(const BatchArgs& a, const Workspace& w, int s, size_t base,
@@ -2887,8 +2920,7 @@ __device__ __forceinline__ void fit_init_peak(const BatchArgs& a, const Workspac
     rx[0] = q.x1; rx[1] = q.x2; rx[2] = q.x3;
     ry[0] = q.y1; ry[1] = q.y2; ry[2] = q.y3;
     mirror_shoulder(q);
-    double* st = w.stencil + 6 * base + 6 * (size_t)p;
-    st[0] = q.x1; st[1] = q.x2; st[2] = q.x3; st[3] = q.y1; st[4] = q.y2; st[5] = q.y3;
+    store_stencil(w, base, p, q);
     double* L = w.params + 3 * base + 3 * (size_t)p;
     solve(q, L);
     if (!peak_fast_ok(L[0], L[1], L[2])) atomicAdd(&w.unsafe[4 * s], 1);
@@ -2912,8 +2944,7 @@ __device__ __forceinline__ void fit_init_pair(const BatchArgs& a, const Workspac
         rx[0] = q.x1; rx[1] = q.x2; rx[2] = q.x3;
         ry[0] = q.y1; ry[1] = q.y2; ry[2] = q.y3;
         mirror_shoulder(q);
-        double* st = w.stencil + 6 * base + 6 * (size_t)p;
-        st[0] = q.x1; st[1] = q.x2; st[2] = q.x3; st[3] = q.y1; st[4] = q.y2; st[5] = q.y3;
+        store_stencil(w, base, p, q);
         double* L = w.params + 3 * base + 3 * (size_t)p;
         solve(q, L);
         if (!peak_fast_ok(L[0], L[1], L[2])) atomicAdd(&w.unsafe[4 * s], 1);
@@ -3038,8 +3069,7 @@ __device__ __forceinline__ void fit_tf_body(const Workspace& w, int s, int P, in
             const double yq = w.ry[3 * base + min(p0 + q, npts - 1)];
             const int kq = lane < Q / 3 ? lane : 0;
             const int pkq = min(p0 / 3 + kq, P - 1);
-            const double* stq = w.stencil + 6 * base + 6 * (size_t)pkq;
-            const double s0 = stq[0], s1 = stq[1], s2 = stq[2], s3 = stq[3], s4 = stq[4], s5 = stq[5];
+            const Stencil sq0 = load_stencil(w, base, pkq);
             // acc = fma(t, 1, acc) rounds as acc + t; the VOP2 v_fmac_f64 chain issues
             // a cycle faster per term than dependent v_add_f64 (eval_cost.hip)
             double one = 1.0;
@@ -3077,13 +3107,12 @@ __device__ __forceinline__ void fit_tf_body(const Workspace& w, int s, int P, in
             const double r2 = __shfl(ratio, 3 * k + 2, 64);
             const int pk = p0 / 3 + lane;
             if (lane < Q / 3 && pk < P) {
-                double* st = w.stencil + 6 * base + 6 * (size_t)pk;
-                Stencil sq{s0, s1, s2, s3, s4, s5};
+                Stencil sq = sq0;
                 sq.y1 = sq.y1 * r0;
                 sq.y2 = sq.y2 * r1;
                 sq.y3 = sq.y3 * r2;
                 mirror_shoulder(sq);
-                st[0] = sq.x1; st[1] = sq.x2; st[2] = sq.x3; st[3] = sq.y1; st[4] = sq.y2; st[5] = sq.y3;
+                store_updated_stencil(w, base, pk, sq, sq0.x1, sq0.x3);
                 double* L = (((it + 1) & 1) ? w.params_alt : w.params) + 3 * base + 3 * (size_t)pk;
                 solve(sq, L);
                 if (!peak_fast_ok(L[0], L[1], L[2])) atomicAdd(&w.unsafe[4 * s + (it + 1) % 3], 1);
@@ -3239,8 +3268,7 @@ __device__ __forceinline__ void fit_tw_body(const Workspace& w, int s, int P, in
             const double yq = w.ry[3 * base + min(p0 + q, npts - 1)];
             const int kq = lane < QQ / 3 ? lane : 0;
             const int pkq = min(p0 / 3 + kq, P - 1);
-            const double* stq = w.stencil + 6 * base + 6 * (size_t)pkq;
-            const double s0 = stq[0], s1 = stq[1], s2 = stq[2], s3 = stq[3], s4 = stq[4], s5 = stq[5];
+            const Stencil sq0 = load_stencil(w, base, pkq);
             double one = 1.0;
             asm volatile("" : "+v"(one));
             if constexpr (!SH::SB) lds_barrier();  // chunk 0 written
@@ -3286,13 +3314,12 @@ __device__ __forceinline__ void fit_tw_body(const Workspace& w, int s, int P, in
             const double r2 = __shfl(ratio, 3 * k + 2, 64);
             const int pk = p0 / 3 + lane;
             if (lane < QQ / 3 && pk < P) {
-                double* st = w.stencil + 6 * base + 6 * (size_t)pk;
-                Stencil sq{s0, s1, s2, s3, s4, s5};
+                Stencil sq = sq0;
                 sq.y1 = sq.y1 * r0;
                 sq.y2 = sq.y2 * r1;
                 sq.y3 = sq.y3 * r2;
                 mirror_shoulder(sq);
-                st[0] = sq.x1; st[1] = sq.x2; st[2] = sq.x3; st[3] = sq.y1; st[4] = sq.y2; st[5] = sq.y3;
+                store_updated_stencil(w, base, pk, sq, sq0.x1, sq0.x3);
                 double* L = (((it + 1) & 1) ? w.params_alt : w.params) + 3 * base + 3 * (size_t)pk;
                 solve(sq, L);
                 if (!peak_fast_ok(L[0], L[1], L[2])) atomicAdd(&w.unsafe[4 * s + (it + 1) % 3], 1);
@@ -3469,14 +3496,14 @@ __global__ void k_fit_update(BatchArgs a, Workspace w, int it) {
     const int P = w.sel_count[s];
     const size_t base = (size_t)s * w.capD;
     for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
-        double* st = w.stencil + 6 * base + 6 * (size_t)p;
         const double* ra = w.ratio + 3 * base + 3 * (size_t)p;
-        Stencil q{st[0], st[1], st[2], st[3], st[4], st[5]};
+        const Stencil q0 = load_stencil(w, base, p);
+        Stencil q = q0;
         q.y1 = q.y1 * ra[0];
         q.y2 = q.y2 * ra[1];
         q.y3 = q.y3 * ra[2];
         mirror_shoulder(q);
-        st[0] = q.x1; st[1] = q.x2; st[2] = q.x3; st[3] = q.y1; st[4] = q.y2; st[5] = q.y3;
+        store_updated_stencil(w, base, p, q, q0.x1, q0.x3);
         double* L = w.params + 3 * base + 3 * (size_t)p;
         solve(q, L);
         if (!peak_fast_ok(L[0], L[1], L[2])) atomicAdd(&w.unsafe[4 * s + ((it + 1) & 1)], 1);
@@ -3529,7 +3556,8 @@ __device__ __forceinline__ double fold_small(double x, const double* prm, int P,
 
 template <int BS, class PT, class ST, class RT>
 __device__ __forceinline__ void fit_small_body(const Workspace& w, int s, int P, int iters, int xok,
-                                               PT prm_in, PT prm_out, ST stn, RT rat, bool lds) {
+                                               PT prm_in, PT prm_out, ST stn, RT rat, bool lds,
+                                               size_t ps) {  // ps: stencil y plane - x plane (doubles)
     const size_t base = (size_t)s * w.capD;
     const double* __restrict__ rx = w.rx + 3 * base;
     const double* __restrict__ ry = w.ry + 3 * base;
@@ -3551,13 +3579,14 @@ __device__ __forceinline__ void fit_small_body(const Workspace& w, int s, int P,
         __syncthreads();
         if (it == 0) KSTAMP(72);
         for (int p = tid; p < P; p += BS) {
-            Stencil q{stn[6 * p], stn[6 * p + 1], stn[6 * p + 2], stn[6 * p + 3], stn[6 * p + 4], stn[6 * p + 5]};
+            Stencil q{stn[3 * p], stn[3 * p + 1], stn[3 * p + 2], stn[ps + 3 * p], stn[ps + 3 * p + 1],
+                      stn[ps + 3 * p + 2]};
             q.y1 = q.y1 * rat[3 * p];
             q.y2 = q.y2 * rat[3 * p + 1];
             q.y3 = q.y3 * rat[3 * p + 2];
             mirror_shoulder(q);
-            stn[6 * p] = q.x1; stn[6 * p + 1] = q.x2; stn[6 * p + 2] = q.x3;
-            stn[6 * p + 3] = q.y1; stn[6 * p + 4] = q.y2; stn[6 * p + 5] = q.y3;
+            stn[3 * p] = q.x1; stn[3 * p + 1] = q.x2; stn[3 * p + 2] = q.x3;
+            stn[ps + 3 * p] = q.y1; stn[ps + 3 * p + 1] = q.y2; stn[ps + 3 * p + 2] = q.y3;
             double L[3];
             solve(q, L);
             nxt[3 * p] = L[0]; nxt[3 * p + 1] = L[1]; nxt[3 * p + 2] = L[2];
@@ -3579,6 +3608,7 @@ template <int BS>
 __device__ __forceinline__ void fit_small_terms(const Workspace& w, int s, int P, int iters, int xok,
                                                 double* prm, double* stn, double* rat, double* T) {
     constexpr int U = kSmallT / BS;
+    constexpr int ps = 3 * kSmallP;  // the LDS stencil planes
     const size_t base = (size_t)s * w.capD;
     const int tid = threadIdx.x, npts = 3 * P, nt = npts * P;
     const int RS = P | 1;  // row stride of T (odd: fewer bank conflicts in the folds)
@@ -3639,13 +3669,14 @@ __device__ __forceinline__ void fit_small_terms(const Workspace& w, int s, int P
         bad = 0;
         if (tid < P) {
             const int p = tid;
-            Stencil q{stn[6 * p], stn[6 * p + 1], stn[6 * p + 2], stn[6 * p + 3], stn[6 * p + 4], stn[6 * p + 5]};
+            Stencil q{stn[3 * p], stn[3 * p + 1], stn[3 * p + 2], stn[ps + 3 * p], stn[ps + 3 * p + 1],
+                      stn[ps + 3 * p + 2]};
             q.y1 = q.y1 * rat[3 * p];
             q.y2 = q.y2 * rat[3 * p + 1];
             q.y3 = q.y3 * rat[3 * p + 2];
             mirror_shoulder(q);
-            stn[6 * p] = q.x1; stn[6 * p + 1] = q.x2; stn[6 * p + 2] = q.x3;
-            stn[6 * p + 3] = q.y1; stn[6 * p + 4] = q.y2; stn[6 * p + 5] = q.y3;
+            stn[3 * p] = q.x1; stn[3 * p + 1] = q.x2; stn[3 * p + 2] = q.x3;
+            stn[ps + 3 * p] = q.y1; stn[ps + 3 * p + 1] = q.y2; stn[ps + 3 * p + 2] = q.y3;
             double L[3];
             solve(q, L);
             prm[3 * p] = L[0]; prm[3 * p + 1] = L[1]; prm[3 * p + 2] = L[2];
@@ -4305,7 +4336,7 @@ __global__ __launch_bounds__(kExactFoldBS) void k_mse_exact_fold(BatchArgs a, Wo
 template <int BS>
 __global__ __launch_bounds__(BS) void k_fit_small(BatchArgs a, Workspace w) {
     __shared__ double prm[3 * kSmallP];
-    __shared__ double buf[9 * kSmallP];  // stencils (6 per peak), ratios (3 per point)
+    __shared__ double buf[9 * kSmallP];  // stencil x and y planes (3 per peak each), ratios (3 per point)
     __shared__ double T[kSmallT];        // the terms of one iteration (3 P^2 <= kSmallT)
     double* const stn = buf;
     double* const rat = buf + 6 * kSmallP;
@@ -4318,20 +4349,23 @@ __global__ __launch_bounds__(BS) void k_fit_small(BatchArgs a, Workspace w) {
     const size_t base = (size_t)s * w.capD;
     if (P <= kSmallP) {
         for (int k = threadIdx.x; k < 3 * P; k += BS) prm[k] = w.params[3 * base + k];
-        for (int k = threadIdx.x; k < 6 * P; k += BS) stn[k] = w.stencil[6 * base + k];
+        for (int k = threadIdx.x; k < 3 * P; k += BS) {
+            stn[k] = w.stencil[6 * base + k];
+            stn[3 * kSmallP + k] = w.stencil[6 * base + 3 * (size_t)w.capD + k];
+        }
         __syncthreads();
         if (P > 0 && 3 * P * (P | 1) <= kSmallT && P <= BS) {
             static_assert(kSmallT % BS == 0, "whole term slots per thread");
             fit_small_terms<BS>(w, s, P, iters, xok, prm, stn, rat, T);
         } else {
-            fit_small_body<BS>(w, s, P, iters, xok, (double*)prm, (double*)prm, stn, rat, true);
+            fit_small_body<BS>(w, s, P, iters, xok, (double*)prm, (double*)prm, stn, rat, true, 3 * kSmallP);
         }
         // the version k_mse_local's retain reads (final_params)
         double* out = (double*)params_version(w, base, iters);
         for (int k = threadIdx.x; k < 3 * P; k += BS) out[k] = prm[k];
     } else {
         fit_small_body<BS>(w, s, P, iters, xok, (double*)nullptr, (double*)nullptr, w.stencil + 6 * base,
-                           w.kept + 3 * base, false);
+                           w.kept + 3 * base, false, 3 * (size_t)w.capD);
     }
     KSTAMP(75);
 }

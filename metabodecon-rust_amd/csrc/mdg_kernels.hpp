@@ -54,7 +54,7 @@ struct BatchArgs {
 //   det_* / sel_*      B x capD i32    (peak index triples, SoA)
 //   scores             B x capD f64
 //   params, kept       B x capD x 3 f64 (AoS {sfhw,hw2,maxp}: wave-uniform SMEM reads)
-//   stencil            B x capD x 6 f64
+//   stencil            B x capD x 6 f64 (per spectrum: x plane 3 capD, then y plane 3 capD)
 //   rx, ry, ratio      B x 3capD f64   (reduced spectrum, fitter order l,c,r)
 struct Workspace {
     int W;                    // mask words per spectrum = ceil(N/64)
