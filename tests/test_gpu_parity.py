@@ -1200,6 +1200,49 @@ def test_small_spectra_detection_inside_select(ctx, detect, engine_env):
         assert o.status != 0, k
 
 
+def _random_small_case(seed):
+    """A small spectrum of random shape (N 48..4096, a few Lorentzians over noise, a
+    random signal region, sometimes an ignore region, random smoothing, threshold and
+    iteration count) for the small-spectrum kernels (fused detection, k_fit_small)."""
+    rng = np.random.default_rng(1000 + seed)
+    n = int(rng.integers(48, 4097))
+    lo, hi = sorted(rng.uniform(-1.0, 12.0, 2))
+    hi = lo + max(hi - lo, 0.5)
+    desc = rng.random() < 0.7
+    x = np.linspace(hi, lo, n) if desc else np.linspace(lo, hi, n)
+    t = np.arange(n, dtype=np.float64)
+    y = rng.normal(0.0, 10.0 ** rng.uniform(-1, 1), n)
+    a0, b0 = np.sort(rng.uniform(0.15, 0.85, 2))
+    for _ in range(int(rng.integers(1, 12))):  # most of them inside the signal region
+        f = rng.uniform(a0, max(b0, a0 + 0.05)) if rng.random() < 0.7 else rng.uniform(0, 1)
+        c0, wd = ((1.0 - f) if desc else f) * (n - 1), rng.uniform(1.0, max(1.5, n / 60))
+        y += 10.0 ** rng.uniform(1, 4) / (1.0 + ((t - c0) / wd) ** 2)
+    sb = (lo + a0 * (hi - lo), lo + max(b0, a0 + 0.05) * (hi - lo))
+    if desc:
+        sb = sb[::-1]
+    ign = ()
+    if rng.random() < 0.3:
+        m = 0.5 * (sb[0] + sb[1])
+        ign = ((m, m + 0.02 * (hi - lo)),)
+    st = oracle.make_settings(smooth_iterations=int(rng.integers(1, 5)),
+                              smooth_window=int(rng.integers(2, 8)),
+                              threshold=float(rng.uniform(0.5, 4.0)),
+                              fit_iterations=int(rng.integers(1, 16)))
+    return x, y, sb, st, ign
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_small_spectra_random_shapes(ctx, seed):
+    """Random small spectra through the default small-spectrum path (the detection
+    inside k_select, k_fit_small, k_mse_local) against the oracle: status, selected
+    parameters bit for bit, MSE within MSE_RTOL -- whatever the length, axis
+    direction, signal region, ignore region and settings draw."""
+    x, y, sb, st, ign = _random_small_case(seed)
+    o = oracle.deconvolute(x, y, sb, st, ignore=ign)
+    status, counts, out, mse = gpu_batch(ctx, x, y[None, :], [sb], st, ignore=ign)
+    check_against(o.params, o.mse, status[0], counts[0], out[0], mse[0], o.status)
+
+
 def _same_bits_or_nan(a, b):
     na, nb = np.isnan(a), np.isnan(b)
     return np.array_equal(na, nb) and np.array_equal(a[~na].view(np.uint64), b[~nb].view(np.uint64))
