@@ -1200,12 +1200,12 @@ def test_small_spectra_detection_inside_select(ctx, detect, engine_env):
         assert o.status != 0, k
 
 
-def _random_small_case(seed):
+def _random_small_case(seed, n_range=(48, 4097)):
     """A small spectrum of random shape (N 48..4096, a few Lorentzians over noise, a
     random signal region, sometimes an ignore region, random smoothing, threshold and
     iteration count) for the small-spectrum kernels (fused detection, k_fit_small)."""
     rng = np.random.default_rng(1000 + seed)
-    n = int(rng.integers(48, 4097))
+    n = int(rng.integers(*n_range))
     lo, hi = sorted(rng.uniform(-1.0, 12.0, 2))
     hi = lo + max(hi - lo, 0.5)
     desc = rng.random() < 0.7
@@ -1238,6 +1238,16 @@ def test_small_spectra_random_shapes(ctx, seed):
     parameters bit for bit, MSE within MSE_RTOL -- whatever the length, axis
     direction, signal region, ignore region and settings draw."""
     x, y, sb, st, ign = _random_small_case(seed)
+    o = oracle.deconvolute(x, y, sb, st, ignore=ign)
+    status, counts, out, mse = gpu_batch(ctx, x, y[None, :], [sb], st, ignore=ign)
+    check_against(o.params, o.mse, status[0], counts[0], out[0], mse[0], o.status)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_shapes_beyond_the_small_path(ctx, seed):
+    """The same random shapes at 4097..60000 points (the general path: k_flags,
+    k_peaks, k_select, the batch-size fit kernels) against the oracle."""
+    x, y, sb, st, ign = _random_small_case(500 + seed, (4097, 60001))
     o = oracle.deconvolute(x, y, sb, st, ignore=ign)
     status, counts, out, mse = gpu_batch(ctx, x, y[None, :], [sb], st, ignore=ign)
     check_against(o.params, o.mse, status[0], counts[0], out[0], mse[0], o.status)
