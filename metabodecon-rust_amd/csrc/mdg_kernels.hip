@@ -3611,45 +3611,51 @@ __device__ __forceinline__ void fit_small_terms(const Workspace& w, int s, int P
     constexpr int ps = 3 * kSmallP;  // the LDS stencil planes
     const size_t base = (size_t)s * w.capD;
     const int tid = threadIdx.x, npts = 3 * P, nt = npts * P;
+    const int nu = __builtin_amdgcn_readfirstlane((nt + BS - 1) / BS);  // term slots in use
     const int RS = P | 1;  // row stride of T (odd: fewer bank conflicts in the folds)
+    // term e = tid + u * BS is (point i, peak j) = (e % npts, e / npts): the lanes of a
+    // wave share a peak, so its three parameters are LDS broadcasts (one address per
+    // wave, not 64: the point-major order cost sim_01's terms ~1.9k cycles an iteration)
     double xu[U];
     int ju[U], eu[U];
-    {
-        int i = tid / P, j = tid - (tid / P) * P;
-        const int stI = BS / P, stJ = BS - (BS / P) * P;
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const bool ok = tid + u * BS < nt;
-            xu[u] = w.rx[3 * base + (ok ? i : 0)];
-            ju[u] = ok ? j : 0;
-            eu[u] = ok ? i * RS + j : -1;
-            i += stI;
-            j += stJ;
-            if (j >= P) {
-                j -= P;
-                ++i;
-            }
-        }
+    for (int u = 0; u < U; ++u) {
+        const int e = tid + u * BS;
+        const bool ok = e < nt;
+        const int j = ok ? e / npts : 0, i = ok ? e - j * npts : 0;
+        xu[u] = w.rx[3 * base + i];
+        ju[u] = j;
+        eu[u] = ok ? i * RS + j : -1;
     }
     const double yq = tid < npts ? w.ry[3 * base + tid] : 1.0;
+    __shared__ int badf[2];
     int bad = 0;
     for (int p = tid; p < P; p += BS) bad |= !peak_fast_ok(prm[3 * p], prm[3 * p + 1], prm[3 * p + 2]);
     bool fast = xok && !__syncthreads_or(bad);
+    if (tid == 0) badf[0] = 0;  // iteration 0's flags (read after its update's barrier)
     KSTAMP(71);
     for (int it = 0; it < iters; ++it) {
         if (!fast && tid == 0) mark_slow(w, s, slow_bit(it));
+        // only the nu slots that hold terms (wave-uniform; sim_01: 4 of 12) -- evaluating
+        // all twelve tripled the iteration's division work
         double t[U];
-        if (fast) {
 #pragma unroll
-            for (int u = 0; u < U; ++u) t[u] = lorentz_t<true>(xu[u], prm[3 * ju[u]], prm[3 * ju[u] + 1], prm[3 * ju[u] + 2]);
+        for (int u = 0; u < U; ++u) t[u] = 0.0;
+        if (fast) {  // (one uniform branch around the loop: per term, both forms were computed)
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (u < nu) t[u] = lorentz_t<true>(xu[u], prm[3 * ju[u]], prm[3 * ju[u] + 1], prm[3 * ju[u] + 2]);
         } else {
 #pragma unroll
-            for (int u = 0; u < U; ++u) t[u] = lorentz_t<false>(xu[u], prm[3 * ju[u]], prm[3 * ju[u] + 1], prm[3 * ju[u] + 2]);
+            for (int u = 0; u < U; ++u)
+                if (u < nu) t[u] = lorentz_t<false>(xu[u], prm[3 * ju[u]], prm[3 * ju[u] + 1], prm[3 * ju[u] + 2]);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            if (eu[u] >= 0) T[eu[u]] = t[u];
+            if (u < nu && eu[u] >= 0) T[eu[u]] = t[u];
+        if (it == 1) KSTAMP(76);
         lds_barrier();
+        if (it == 1) KSTAMP(77);
         if (tid < npts) {
             const double* row = T + tid * RS;
             double acc = -0.0;
@@ -3664,8 +3670,10 @@ __device__ __forceinline__ void fit_small_terms(const Workspace& w, int s, int P
             for (; k < P; ++k) acc += row[k];
             rat[tid] = yq / acc;
         }
+        if (it == 1) KSTAMP(78);
         lds_barrier();
         if (it == 0) KSTAMP(72);
+        if (it == 1) KSTAMP(79);
         bad = 0;
         if (tid < P) {
             const int p = tid;
@@ -3682,8 +3690,18 @@ __device__ __forceinline__ void fit_small_terms(const Workspace& w, int s, int P
             prm[3 * p] = L[0]; prm[3 * p + 1] = L[1]; prm[3 * p + 2] = L[2];
             bad = !peak_fast_ok(L[0], L[1], L[2]);
         }
-        fast = xok && !__syncthreads_or(bad);
+        // the range check's reduction: the flags of iteration parity it & 1 set by the
+        // peaks out of range, the other parity's cleared for the next iteration (its
+        // last readers passed two barriers ago), one barrier -- __syncthreads_or here
+        // cost ~1.3k cycles an iteration (its own barriers and LDS reduction; phase
+        // stamps, sim_01)
+        if (bad) badf[it & 1] = 1;
+        if (tid == 0) badf[(it + 1) & 1] = 0;
+        if (it == 1) KSTAMP(86);
+        lds_barrier();
+        fast = xok && !badf[it & 1];
         if (it == 0) KSTAMP(73);
+        if (it == 1) KSTAMP(87);
     }
     KSTAMP(74);
 }
