@@ -2719,7 +2719,9 @@ __global__ __launch_bounds__(BS) void k_select(BatchArgs a, Workspace w, double 
 #pragma unroll
         for (int u = 0; u < kSelPerThread; ++u) wcount += __popcll(__ballot(kept(u)));
         int total;
+        KSTAMP(12);
         const int woff = block_exclusive_scan<BS>(lane == 0 ? wcount : 0, lds_i, &total);
+        KSTAMP(19);
         const int wstart = __shfl(woff, 0, 64);  // lane 0's exclusive prefix: the wave's offset
         // the kept candidates' borders, every load issued before the first is used
         int lv[kSelPerThread], cv[kSelPerThread], rv[kSelPerThread];
