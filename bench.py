@@ -245,9 +245,12 @@ def hbm_pipeline(tag, batch, iterations, value, n):
                 if k in kern:
                     return kern[k]
                 base = k.split("<")[0].strip()
-                return max((v for n, v in kern.items() if n.split("<")[0].strip() == base),
-                           key=lambda v: v["hbm_bytes_per_launch"])
-            per = {k: entry(k)["hbm_bytes_per_launch"] * m / batch for k, m in launches.items()}
+                same = [v for n, v in kern.items() if n.split("<")[0].strip() == base]
+                # (none: a kernel the pipeline no longer launches -- k_flags since round
+                # 6, its predicates inside k_peaks' coarse chunks)
+                return max(same, key=lambda v: v["hbm_bytes_per_launch"]) if same else None
+            per = {k: entry(k)["hbm_bytes_per_launch"] * m / batch for k, m in launches.items()
+                   if entry(k) is not None}
         except (OSError, KeyError, ValueError):
             continue
         total = sum(per.values())

@@ -578,7 +578,7 @@ int run_pipeline(mdg_ctx* c, BatchArgs& a, const mdg_settings* s) {
     if (!det_fused) {
         StageTimer t(c, ST_DETECT);
         for (int r = reps("detect"); r > 0; --r) {
-            launch_flags(a, w, st);
+            if (!peaks_fuse_flags(a, w, sw)) launch_flags(a, w, st);
             kn[ST_DETECT] = launch_peaks(a, w, det_only, sw, st);
         }
     }

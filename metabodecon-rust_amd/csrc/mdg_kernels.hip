@@ -289,6 +289,79 @@ __device__ __forceinline__ int find_prev_bit(const uint64_t* __restrict__ m, int
     }
 }
 
+// The border predicates of k_flags at position k (2 <= k <= N-3), from the row itself:
+// first right border >= pos (<= limit), last left border <= pos (>= lo), or -1. For
+// borders beyond a chunk's window of masks (k_peaks with the predicates fused).
+__device__ __forceinline__ int next_fr_row(const double* __restrict__ sm, int N, int pos, int limit) {
+    pos = max(pos, 2);
+    limit = min(limit, N - 3);
+    if (pos > limit) return -1;
+    double dm = dsd(sm, pos - 1), d0 = dsd(sm, pos);
+    for (int k = pos; k <= limit; ++k) {
+        const double dp = dsd(sm, k + 1);
+        if (d0 > dm && (d0 >= dp || (d0 < 0. && dp >= 0.))) return k;
+        dm = d0;
+        d0 = dp;
+    }
+    return -1;
+}
+__device__ __forceinline__ int prev_fl_row(const double* __restrict__ sm, int N, int pos, int lo) {
+    pos = min(pos, N - 3);
+    lo = max(lo, 2);
+    if (pos < lo) return -1;
+    double dp = dsd(sm, pos + 1), d0 = dsd(sm, pos);
+    for (int k = pos; k >= lo; --k) {
+        const double dm = dsd(sm, k - 1);
+        if (d0 > dp && (d0 >= dm || (d0 < 0. && dm >= 0.))) return k;
+        dp = d0;
+        d0 = dm;
+    }
+    return -1;
+}
+// find_next_bit / find_prev_bit over a window of mask words [wlo, wlo + nw) held in LDS
+// (m[0] = word wlo), continuing on the row (next_fr_row / prev_fl_row) past its ends
+__device__ __forceinline__ int next_bit_win(const uint64_t* m, int wlo, int nw, int pos, int limit,
+                                            const double* sm, int N) {
+    if (pos > limit) return -1;
+    int w = pos >> 6;
+    const int lastw = limit >> 6, whi = wlo + nw - 1;
+    if (w <= whi) {
+        uint64_t bits = m[w - wlo] & (~0ull << (pos & 63));
+        for (;;) {
+            if (bits) {
+                const int r = (w << 6) + __ffsll((unsigned long long)bits) - 1;
+                return r <= limit ? r : -1;
+            }
+            if (++w > lastw) return -1;
+            if (w > whi) break;
+            bits = m[w - wlo];
+        }
+        pos = w << 6;
+    }
+    return next_fr_row(sm, N, pos, limit);
+}
+__device__ __forceinline__ int prev_bit_win(const uint64_t* m, int wlo, int nw, int pos, int lo,
+                                            const double* sm, int N) {
+    if (pos < lo || pos < 0) return -1;
+    int w = pos >> 6;
+    const int firstw = lo >> 6;
+    if (w >= wlo) {
+        const int b = pos & 63;
+        uint64_t bits = m[w - wlo] & (b == 63 ? ~0ull : ((1ull << (b + 1)) - 1ull));
+        for (;;) {
+            if (bits) {
+                const int r = (w << 6) + 63 - __clzll((long long)bits);
+                return r >= lo ? r : -1;
+            }
+            if (--w < firstw) return -1;
+            if (w < wlo) break;
+            bits = m[w - wlo];
+        }
+        pos = (w << 6) + 63;
+    }
+    return prev_fl_row(sm, N, pos, lo);
+}
+
 // ----------------------------------------------------------------------------------
 // K0  prep: signal-boundary indices, ignore-region indices, MSE regions
 // spectrum.rs:633-635,741-746 ; deconvoluter.rs:828-904
@@ -303,6 +376,13 @@ __device__ __forceinline__ double dec_x(const double* d, int64_t i) {
 }
 
 __device__ __forceinline__ void prep_spectrum(const BatchArgs& a, const Workspace& w, int s) {
+    // k_peaks' look-back slots start empty (k_flags cleared them until round 6; with the
+    // predicates inside k_peaks no launch runs between the smoother and it)
+    {
+        const int ns = (w.W + kPkSlotWords - 1) / kPkSlotWords;
+        unsigned long long* slot = (unsigned long long*)w.peak_cnt + (size_t)s * ns;
+        for (int k = 0; k < ns; ++k) slot[k] = 0;
+    }
     // rows the chain launch is still decoding (a.dec_rows): the axis's end points from
     // its descriptor, the values the decoders write
     const double* x = a.x + (size_t)s * a.x_stride;
@@ -1672,25 +1752,30 @@ __device__ __forceinline__ bool in_ignore(int v, const int64_t* pairs, int n) {
 // The peaks of one mask word (64 points) whose centre bits are in sel, in centre
 // order: borders by bit scans, the detector-only and ignore-region filters. Counts
 // the bordered peaks; returns the kept ones, writing them at out.. when WRITE.
-// (LDSM: the masks are the caller's copy in LDS, mlds, laid out as w.masks' row;
-// GOUT = false: WRITE fills only the pk copy, not the global peak rows)
+// (LDSM: the masks are the caller's window of mask words [wlo, wlo + nw) in LDS, mlds:
+// the centre words, then the right-border words, then the left-border ones; a border
+// beyond the window is searched on the smoothed row smr itself. GOUT = false: WRITE
+// fills only the pk copy, not the global peak rows)
 template <bool WRITE, bool LDSM = false, bool GOUT = true>
 __device__ __forceinline__ int word_peaks(const BatchArgs& a, const Workspace& w, int s, int wd, uint64_t sel,
                                           int detector_only, int* bordered, size_t out,
                                           int* pk = nullptr, int pcap = 0, int po = 0,
-                                          const uint64_t* mlds = nullptr) {
+                                          const uint64_t* mlds = nullptr, int wlo = 0, int nw = 0,
+                                          const double* smr = nullptr, int nig_in = -1) {
     const int N = a.N, W = w.W;
+    const int mst = LDSM ? nw : W, off = LDSM ? wlo : 0;  // kind stride, first word held
     const uint64_t* mc = LDSM ? mlds : w.masks + (size_t)s * 3 * W;
-    const uint64_t* mr = mc + W;
-    const uint64_t* ml = mc + 2 * W;
+    const uint64_t* mr = mc + mst;
+    const uint64_t* ml = mc + 2 * mst;
     const int64_t* pairs = w.ig + (size_t)s * 2 * w.ig_cap;
-    const int nig = w.n_ig[s];
-    const int64_t sbi0 = w.sbi[2 * s], sbi1 = w.sbi[2 * s + 1];
+    // (nig_in: the caller loaded the region count ahead, with its other head loads)
+    const int nig = nig_in >= 0 ? nig_in : (a.n_ignore > 0 ? w.n_ig[s] : 0);
+    const int64_t sbi0 = detector_only ? w.sbi[2 * s] : 0, sbi1 = detector_only ? w.sbi[2 * s + 1] : 0;
     // the word and its neighbours' border masks in one round trip; a border farther
     // than the neighbouring word falls back to the scans over memory
-    uint64_t bits = mc[wd] & sel;
-    const uint64_t r0 = mr[wd], r1 = wd + 1 < W ? mr[wd + 1] : 0;
-    const uint64_t l0 = ml[wd], l1 = wd > 0 ? ml[wd - 1] : 0;
+    uint64_t bits = mc[wd - off] & sel;
+    const uint64_t r0 = mr[wd - off], r1 = wd + 1 < W ? mr[wd + 1 - off] : 0;
+    const uint64_t l0 = ml[wd - off], l1 = wd > 0 ? ml[wd - 1 - off] : 0;
     const int lim_r = N - 3, lim_l = 2;
     int kept = 0;
     while (bits) {
@@ -1702,14 +1787,16 @@ __device__ __forceinline__ int word_peaks(const BatchArgs& a, const Workspace& w
         const uint64_t ra = b == 63 ? 0 : (r0 & (~0ull << (b + 1)));
         if (ra) r = (wd << 6) + __ffsll((unsigned long long)ra) - 1;
         else if (r1) r = ((wd + 1) << 6) + __ffsll((unsigned long long)r1) - 1;
-        else r = find_next_bit(mr, (wd + 2) << 6, lim_r);
+        else r = LDSM ? next_bit_win(mr, wlo, nw, (wd + 2) << 6, lim_r, smr, N)
+                      : find_next_bit(mr, (wd + 2) << 6, lim_r);
         if (r > lim_r) r = -1;
         // last left-border bit < c (>= 2): this word below b, then the previous word
         int l;
         const uint64_t la = b == 0 ? 0 : (l0 & ((1ull << b) - 1ull));
         if (la) l = (wd << 6) + 63 - __clzll((long long)la);
         else if (l1) l = ((wd - 1) << 6) + 63 - __clzll((long long)l1);
-        else l = find_prev_bit(ml, ((wd - 1) << 6) - 1, lim_l);
+        else l = LDSM ? prev_bit_win(ml, wlo, nw, ((wd - 1) << 6) - 1, lim_l, smr, N)
+                      : find_prev_bit(ml, ((wd - 1) << 6) - 1, lim_l);
         if (l < lim_l) l = -1;
         if (r < 0 || l < 0) continue;  // right == N-1 or left == 0: dropped
         ++*bordered;
@@ -1790,10 +1877,18 @@ __device__ __forceinline__ double score_peak_lds(const double* ys, int lo, int l
 constexpr unsigned long long kPkValid = 1ull << 62;
 // BS = 4 WORDS threads per chunk: four per mask word; all of them score the chunk's
 // peaks afterwards
-template <int WORDS, int BS>
+// FUSE (round 6): k_flags' predicates computed here, for the chunk's words and one word
+// either side, into LDS (the row is read once, here, instead of by k_flags and again
+// for the scores: one launch and ~0.74 MB per 128k-point spectrum fewer); a border
+// beyond that window is found on the row itself (next_fr_row / prev_fl_row). k_flags'
+// other duties move too: the chain's progress counters are reset here, the look-back
+// slots are cleared by prep_spectrum.
+template <int WORDS, int BS, bool FUSE = false>
 __global__ __launch_bounds__(BS) void k_peaks(BatchArgs a, Workspace w, int detector_only, int score) {
     static_assert(WORDS % kPkSlotWords == 0 && BS == 4 * WORDS, "chunk shape");
     const int s = blockIdx.y, chunk = blockIdx.x;
+    if (FUSE && chunk == 0 && (int)threadIdx.x < w.chain_P)  // (whatever the status, as k_flags)
+        w.chain_flags[((size_t)s * w.chain_P + threadIdx.x) * 32] = 0;
     __shared__ int lds_i[BS / 64 + 1];
     __shared__ long long lds_l[BS / 64 + 1];
     // fine chunks (small batches, latency-bound) stage their stretch of the smoothed
@@ -1801,7 +1896,8 @@ __global__ __launch_bounds__(BS) void k_peaks(BatchArgs a, Workspace w, int dete
     // then overlap the word pass instead of following the peak writes (round 4:
     // 12k of a B = 1 launch's 36k cycles were the scoring's two memory round trips)
     constexpr bool STAGE = WORDS == 64;
-    constexpr int SPAN = WORDS * 64, MARG = 64, SN = STAGE ? SPAN + 2 * MARG : 1;
+    // (FUSE: the predicates of the words either side of the chunk read 66 ticks beyond it)
+    constexpr int SPAN = WORDS * 64, MARG = FUSE ? 128 : 64, SN = STAGE ? SPAN + 2 * MARG : 1;
     constexpr int PCAP = STAGE ? SPAN / 2 : 1;  // centres are strict minima: <= SPAN / 2
     constexpr int PER = STAGE ? (SN + BS - 1) / BS : 1;
     __shared__ double ys[SN];
@@ -1816,6 +1912,57 @@ __global__ __launch_bounds__(BS) void k_peaks(BatchArgs a, Workspace w, int dete
         for (int u = 0; u < PER; ++u) stv[u] = sm[min(max(lo + u * BS + (int)threadIdx.x, 0), a.N - 1)];
     }
     if (st) return;  // uniform per spectrum: no chunk waits for a returned one
+    constexpr int NWM = FUSE ? WORDS + 2 : 1;
+    __shared__ uint64_t mw[3 * NWM];
+    const int wlo = chunk * WORDS - 1;
+    if constexpr (FUSE) {
+        const int lane = threadIdx.x & 63, N = a.N, W = w.W;
+        if constexpr (STAGE) {  // the staged row first: the predicates read it in LDS
+#pragma unroll
+            for (int u = 0; u < PER; ++u)
+                if (u * BS + (int)threadIdx.x < SN) ys[u * BS + threadIdx.x] = stv[u];
+            __syncthreads();
+        }
+        KSTAMP(5);
+        // one word per wave and round, UW rounds' loads in flight together (a round
+        // trip per word and wave otherwise: LDS for the staged fine chunks, memory for
+        // the coarse ones)
+        constexpr int NWV = BS / 64, UW = 4;
+        for (int q0 = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6); q0 < NWM; q0 += UW * NWV) {
+            double v[UW][5];
+            bool val[UW];
+#pragma unroll
+            for (int u = 0; u < UW; ++u) {
+                const int q = q0 + u * NWV, k = 64 * (wlo + q) + lane;
+                val[u] = q < NWM && wlo + q >= 0 && wlo + q < W && k >= 2 && k <= N - 3;
+                // unconditional loads (no exec-masked branch per value): the staged
+                // window holds every index of the halo words; memory reads are clamped
+#pragma unroll
+                for (int d = 0; d < 5; ++d)
+                    v[u][d] = STAGE ? ys[min(max(k - 2 + d - lo, 0), SN - 1)] : sm[min(max(k - 2 + d, 0), N - 1)];
+            }
+#pragma unroll
+            for (int u = 0; u < UW; ++u) {
+                const int q = q0 + u * NWV;
+                if (q >= NWM) break;  // (wave-uniform)
+                // dsd(., k - 1), dsd(., k), dsd(., k + 1): the same operations as k_flags
+                const double dm = v[u][0] - 2.0 * v[u][1] + v[u][2];
+                const double d0 = v[u][1] - 2.0 * v[u][2] + v[u][3];
+                const double dp = v[u][2] - 2.0 * v[u][3] + v[u][4];
+                const bool fc = val[u] && d0 < 0. && d0 < dm && d0 < dp;
+                const bool fr = val[u] && d0 > dm && (d0 >= dp || (d0 < 0. && dp >= 0.));
+                const bool fl = val[u] && d0 > dp && (d0 >= dm || (d0 < 0. && dm >= 0.));
+                const uint64_t bc = __ballot(fc), br = __ballot(fr), bl = __ballot(fl);
+                if (lane == 0) {
+                    mw[q] = bc;
+                    mw[NWM + q] = br;
+                    mw[2 * NWM + q] = bl;
+                }
+            }
+        }
+        KSTAMP(6);
+        __syncthreads();
+    }
     const int nch = (w.W + WORDS - 1) / WORDS;
     unsigned long long* slot = (unsigned long long*)w.peak_cnt + (size_t)s * peak_slots(w.W);
     // four threads per mask word, each the peaks centred in 16 of its bits: thread
@@ -1824,8 +1971,9 @@ __global__ __launch_bounds__(BS) void k_peaks(BatchArgs a, Workspace w, int dete
     const int wd = chunk * WORDS + (threadIdx.x >> 2);
     const uint64_t sel = 0xffffull << (16 * (threadIdx.x & 3));
     int bordered = 0, kept = 0;
-    if (wd < w.W) kept = word_peaks<false>(a, w, s, wd, sel, detector_only, &bordered, 0);
-    if constexpr (STAGE) {
+    if (wd < w.W)
+        kept = word_peaks<false, FUSE>(a, w, s, wd, sel, detector_only, &bordered, 0, nullptr, 0, 0, mw, wlo, NWM, sm);
+    if constexpr (STAGE && !FUSE) {
 #pragma unroll
         for (int u = 0; u < PER; ++u)
             if (u * BS + (int)threadIdx.x < SN) ys[u * BS + threadIdx.x] = stv[u];
@@ -1873,7 +2021,9 @@ __global__ __launch_bounds__(BS) void k_peaks(BatchArgs a, Workspace w, int dete
     if (chunk == 0 && threadIdx.x == 0) w.det_count[s] = (int32_t)k_all;
     KSTAMP(2);
     const size_t b0 = (size_t)s * w.capD + before;
-    if (kept) word_peaks<true>(a, w, s, wd, sel, detector_only, &bordered, b0 + o, STAGE ? pk : nullptr, PCAP, o);
+    if (kept)
+        word_peaks<true, FUSE>(a, w, s, wd, sel, detector_only, &bordered, b0 + o, STAGE ? pk : nullptr, PCAP, o, mw,
+                               wlo, NWM, sm);
     if (detector_only || !score) return;
     KSTAMP(3);
     // k_scores' work for this chunk's peaks, spread evenly over the block
@@ -2496,7 +2646,8 @@ __device__ __forceinline__ int detect_small(const BatchArgs& a, const Workspace&
     const uint64_t sel = 0xffffull << (16 * (tid & 3));
     constexpr int PARK = 4 * kDetW * 8;
     int bordered = 0, kept = 0;
-    if (wd < W) kept = word_peaks<true, true, false>(a, w, s, wd, sel, 0, &bordered, 0, park, PARK, 8 * tid, mlds);
+    if (wd < W)
+        kept = word_peaks<true, true, false>(a, w, s, wd, sel, 0, &bordered, 0, park, PARK, 8 * tid, mlds, 0, W, sm);
     int total;
     const int o = block_exclusive_scan<BS>(kept, lds_i, &total);
     const long long b_all = block_sum_ll<BS>(bordered, lds_l);
@@ -4571,6 +4722,20 @@ const char* launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int
     launch_k(k_smooth, dim3(cdiv(a.B, 64)), dim3(64), 0, st, a, w, iters, ws);
     return "k_smooth";
 }
+// fine (staged) chunks up to 512 workgroups of 64-word chunks (launch_peaks)
+static bool peaks_fine(const BatchArgs& a, const Workspace& w, const EngineSwitches& sw) {
+    return sw.peaks ? sw.peaks == 1 : (size_t)cdiv(w.W, 64) * a.B <= 512;
+}
+// the predicates inside k_peaks only with MDG_DETECT=fused (bit-exact, tested): measured
+// slower (round 6) -- the fine chunks' predicate pass took 13.5k cycles per chunk
+// (stamps, B = 1: k_peaks 20 us against k_flags 4.8 + k_peaks 13.5), and the coarse
+// chunks at the headline saved only 0.19 MB per spectrum (k_peaks 1.91 MB against
+// k_flags 0.74 + k_peaks 1.36: the scores' row reads did not hit the lines the
+// predicates had just read) while the queue ran 16.0k against 16.6-16.7k spectra/s
+bool peaks_fuse_flags(const BatchArgs& a, const Workspace& w, const EngineSwitches& sw) {
+    (void)a, (void)w;
+    return sw.detect == 2;
+}
 void launch_flags(const BatchArgs& a, const Workspace& w, hipStream_t st) {
     launch_k(k_flags, dim3(cdiv(a.N, 256), a.B), dim3(256), 0, st, a, w);
 }
@@ -4581,7 +4746,15 @@ const char* launch_peaks(const BatchArgs& a, const Workspace& w, int detector_on
     // blood, 13.2 / 12.9 / 15.4 / 17.5 us at B = 1 / 4 / 8 / 16 against the coarse
     // chunks' 21.3 / 21.9 / 22.9 / 23.1; synthetic B = 64: 59.8 against 52.6, B = 256:
     // 230 against 216); MDG_PEAKS = fine | coarse forces one (tests)
-    const bool fine = sw.peaks ? sw.peaks == 1 : (size_t)cdiv(w.W, 64) * a.B <= 512;
+    const bool fine = peaks_fine(a, w, sw);
+    if (peaks_fuse_flags(a, w, sw)) {
+        if (fine) {
+            launch_k(k_peaks<64, 256, true>, dim3(cdiv(w.W, 64), a.B), dim3(256), 0, st, a, w, detector_only, 1);
+            return "k_peaks<64, flags>";
+        }
+        launch_k(k_peaks<256, 1024, true>, dim3(cdiv(w.W, 256), a.B), dim3(1024), 0, st, a, w, detector_only, 1);
+        return "k_peaks<256, flags>";
+    }
     if (fine) {
         launch_k(k_peaks<64, 256>, dim3(cdiv(w.W, 64), a.B), dim3(256), 0, st, a, w, detector_only, 1);
         return "k_flags+k_peaks<64>";

@@ -128,7 +128,9 @@ struct EngineSwitches {
     int chain_excl = 1;          // MDG_CHAIN_EXCL=0: never whole-CU chain workgroups
     int chain_l2ahead = 0;       // MDG_CHAIN_L2AHEAD: blocks each chain pulls into L2 ahead (0: by grid)
     int peaks = 0;               // MDG_PEAKS: 0 by batch size, 1 fine, 2 coarse (any other value)
-    int detect = 0;              // MDG_DETECT: 0 by shape (N <= 4096: inside k_select), 1 separate, 2 fused
+    int detect = 0;              // MDG_DETECT: 0 by shape (N <= 4096: inside k_select, else k_flags +
+                                 // k_peaks), 1 separate (k_flags + k_peaks at every N), 2 fused (also
+                                 // the predicates inside k_peaks; measured slower, §5)
     char fitsup[8] = {};         // MDG_FITSUP: a shipped fit kernel's name ("": by batch size)
     int tw_g = 0;                // MDG_TW_G: term-fold workgroups (0: the kernel's default)
     int gfit = 24;               // MDG_GFIT: k_fit_sup workgroups per spectrum
@@ -201,6 +203,8 @@ bool smooth_fuses_prep(const BatchArgs& a, const Workspace& w, int iters, int ws
 const char* launch_smooth(const BatchArgs& a, const Workspace& w, int iters, int ws, const EngineSwitches& sw,
                           hipStream_t st, int fused_prep = 0);
 void launch_flags(const BatchArgs& a, const Workspace& w, hipStream_t st);
+// k_peaks computes the detector's predicates itself (no k_flags launch)
+bool peaks_fuse_flags(const BatchArgs& a, const Workspace& w, const EngineSwitches& sw);
 const char* launch_peaks(const BatchArgs& a, const Workspace& w, int detector_only, const EngineSwitches& sw,
                          hipStream_t st);
 // small spectra with the noise-score selector: detection inside k_select (no k_flags,

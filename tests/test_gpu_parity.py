@@ -1253,6 +1253,40 @@ def test_random_shapes_beyond_the_small_path(ctx, seed):
     check_against(o.params, o.mse, status[0], counts[0], out[0], mse[0], o.status)
 
 
+@pytest.mark.parametrize("peaks", ["fine", "coarse"])
+@pytest.mark.parametrize("detect", ["fused", "separate"])
+def test_detection_with_borders_beyond_the_chunk(ctx, peaks, detect, engine_env):
+    """k_peaks with the predicates inside (the default) holds the masks of its chunk
+    and one word either side; a border farther away is found on the smoothed row. Broad
+    noise-free Lorentzians (half-widths of thousands of points) over narrow ones put
+    borders several chunks away: the detected triples equal the oracle's, and so does
+    the whole deconvolution, on both chunk sizes, against the separate k_flags."""
+    engine_env.setenv("MDG_PEAKS", peaks)
+    engine_env.setenv("MDG_DETECT", detect)
+    n = 131072
+    t = np.arange(n, dtype=np.float64)
+    x = np.linspace(14.8, -5.2, n)
+    rng = np.random.default_rng(5)
+    y = np.zeros(n)
+    for c0, wd, amp in [(15000, 9000.0, 1e6), (75000, 12000.0, 8e5), (110000, 7000.0, 6e5)]:
+        y += amp / (1.0 + ((t - c0) / wd) ** 2)
+    for c0 in rng.uniform(40000, 56000, 12):
+        y += rng.uniform(1e3, 1e5) / (1.0 + ((t - c0) / rng.uniform(3, 40)) ** 2)
+    st = oracle.default_settings()
+    sb = (11.8, -2.2)
+    o = oracle.deconvolute(x, y, sb, st)
+    status, counts, out, mse = gpu_batch(ctx, x, y[None, :], [sb], st)
+    want = {("fused", "fine"): "k_peaks<64, flags>", ("fused", "coarse"): "k_peaks<256, flags>",
+            ("separate", "fine"): "k_flags+k_peaks<64>", ("separate", "coarse"): "k_flags+k_peaks<256>"}
+    assert ctx.stage_kernels()["detect"] == want[(detect, peaks)]
+    det = ctx.last_peaks(0, "detected").astype(np.int64)
+    l, c, r = oracle.detect_peaks(oracle.second_derivative(oracle.moving_average(y, 3, 3)))
+    assert np.array_equal(det, np.stack([l, c, r], axis=1))
+    far = (np.abs(r - c) > 4200) | (np.abs(c - l) > 4200)
+    assert far.any()  # some border lies beyond a fine chunk's window
+    check_against(o.params, o.mse, status[0], counts[0], out[0], mse[0], o.status)
+
+
 def _same_bits_or_nan(a, b):
     na, nb = np.isnan(a), np.isnan(b)
     return np.array_equal(na, nb) and np.array_equal(a[~na].view(np.uint64), b[~nb].view(np.uint64))

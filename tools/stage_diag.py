@@ -57,7 +57,7 @@ def main():
         assert rc == 0
         torch.cuda.synchronize()
     d = diag[STAMPS:].cpu().tolist()
-    groups = {"select": range(10, 20), "peaks": range(0, 5), "fit_dpp": range(20, 24),
+    groups = {"select": range(10, 20), "peaks": [0, 5, 6, 1, 2, 3, 4], "fit_dpp": range(20, 24),
               "mse": range(30, 36), "window_mean": [45, 46, 40, 41, 42], "window_var": [55, 56, 50, 51, 52],
               "small": range(70, 78), "small_it1": [73, 76, 77, 78, 79, 86, 87], "window_small_mse": [65, 66, 60, 61, 62],
               "smooth_small": [88] + list(range(90, 102)), "smooth_small_sb": range(160, 165),
